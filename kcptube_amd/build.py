@@ -1,0 +1,70 @@
+"""Build libkfec.so (gfx950 HIP kernels + C ABI) in-tree with hipcc.
+
+    python -m kcptube_amd.build          # or __graft_entry__.build()
+
+The library lands at kcptube_amd/libkfec.so (git-ignored, but it travels to the GPU box with the
+repo snapshot).  A C++ example/test of the fecpp::fec_code drop-in header is built alongside.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libkfec.so")
+COMPAT_TEST = os.path.join(PKG, "compat_test")
+
+SOURCES = ["kfec_kernels.hip", "kfec_api.cpp"]
+HEADERS = ["kfec_gf.hpp", "kfec_internal.hpp"]
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: libkfec.so cannot be built")
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(force: bool = False, verbose: bool = False) -> str:
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "kfec.h")]
+    if force or _stale(LIB, deps):
+        cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wno-unused-result", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd, cwd=CSRC)
+        os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+def build_compat_test(force: bool = False) -> str:
+    """C++ program exercising include/fecpp_compat.hpp against libkfec.so (run by the GPU tests)."""
+    src = os.path.join(ROOT, "tests", "cpp", "compat_test.cpp")
+    deps = [src, os.path.join(ROOT, "include", "fecpp_compat.hpp"), os.path.join(ROOT, "include", "kfec.h"), LIB]
+    if force or _stale(COMPAT_TEST, deps):
+        cmd = ["g++", "-std=c++20", "-O2", "-I", os.path.join(ROOT, "include"), src, "-o", COMPAT_TEST,
+               "-L", PKG, "-lkfec", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath," + PKG]
+        subprocess.check_call(cmd)
+    return COMPAT_TEST
+
+
+def main() -> None:
+    force = "--force" in sys.argv
+    print(build_lib(force=force, verbose=True))
+    if os.path.exists(os.path.join(ROOT, "tests", "cpp", "compat_test.cpp")):
+        print(build_compat_test(force=force))
+
+
+if __name__ == "__main__":
+    main()

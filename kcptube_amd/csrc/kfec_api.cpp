@@ -1,0 +1,282 @@
+// kfec_api.cpp -- C ABI of libkfec.so (include/kfec.h): coder contexts, argument checking with the
+// reference's error conventions, single-group staging for the fecpp::fec_code drop-in, and the
+// batched device-resident entry points.  All arithmetic runs in the HIP kernels of kfec_kernels.hip.
+#include "../../include/kfec.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "kfec_internal.hpp"
+
+struct kfec_ctx {
+    size_t K = 0, N = 0;
+    kfec::DeviceInfo di;
+    uint8_t *d_enc = nullptr;  // N x K encoding matrix on the device
+    std::vector<uint8_t> h_enc;
+    hipStream_t stream = nullptr;  // private stream of the single-group API
+    std::mutex mu;                 // single-group staging is shared by encode and decode callers
+    uint8_t *d_stage = nullptr;
+    size_t stage_cap = 0;
+};
+
+namespace {
+
+bool kn_valid(size_t K, size_t N) { return !(K == 0 || N == 0 || K > 256 || N > 256 || K > N); }
+
+int probe_device(kfec::DeviceInfo &di)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return KFEC_ENODEV;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return KFEC_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return KFEC_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return KFEC_ENODEV;  // code objects are gfx950-only
+    di.device = dev;
+    di.cus = prop.multiProcessorCount;
+    return KFEC_OK;
+}
+
+int build_matrix(kfec_ctx *c)
+{
+    const size_t bytes = c->N * c->K;
+    if (c->d_enc) (void)hipFree(c->d_enc);
+    c->d_enc = nullptr;
+    if (hipMalloc(&c->d_enc, bytes) != hipSuccess) return KFEC_ENOMEM;
+    if (kfec::launch_build_matrix(c->d_enc, (int)c->K, (int)c->N, c->stream)) return KFEC_EHIP;
+    c->h_enc.assign(bytes, 0);
+    if (hipMemcpyAsync(c->h_enc.data(), c->d_enc, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        return KFEC_EHIP;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return KFEC_EHIP;
+    return KFEC_OK;
+}
+
+int ensure_stage(kfec_ctx *c, size_t bytes)
+{
+    if (bytes <= c->stage_cap) return KFEC_OK;
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    c->d_stage = nullptr;
+    c->stage_cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 64 * 1024);
+    if (hipMalloc(&c->d_stage, cap) != hipSuccess) return KFEC_ENOMEM;
+    c->stage_cap = cap;
+    return KFEC_OK;
+}
+
+inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+
+inline hipStream_t as_stream(void *s) { return static_cast<hipStream_t>(s); }
+
+inline int set_dev(const kfec_ctx *c) { return hipSetDevice(c->di.device) == hipSuccess ? KFEC_OK : KFEC_EHIP; }
+
+}  // namespace
+
+extern "C" {
+
+const char *kfec_version(void) { return "kfec 0.1 (gfx950 perm-MAC)"; }
+
+int kfec_device(const kfec_ctx *ctx) { return ctx ? ctx->di.device : -1; }
+
+int kfec_create(size_t K, size_t N, kfec_ctx **out)
+{
+    if (!out) return KFEC_EINVAL;
+    *out = nullptr;
+    if (!kn_valid(K, N)) return KFEC_EINVAL;
+    kfec::DeviceInfo di;
+    int rc = probe_device(di);
+    if (rc) return rc;
+    kfec_ctx *c = new (std::nothrow) kfec_ctx;
+    if (!c) return KFEC_ENOMEM;
+    c->K = K;
+    c->N = N;
+    c->di = di;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return KFEC_EHIP;
+    }
+    rc = build_matrix(c);
+    if (rc) {
+        kfec_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return KFEC_OK;
+}
+
+int kfec_reset(kfec_ctx *ctx, size_t K, size_t N)
+{
+    if (!ctx || !kn_valid(K, N)) return KFEC_EINVAL;  // reference throws before touching its state
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (set_dev(ctx)) return KFEC_EHIP;
+    ctx->K = K;
+    ctx->N = N;
+    return build_matrix(ctx);
+}
+
+void kfec_destroy(kfec_ctx *ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->di.device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_enc) (void)hipFree(ctx->d_enc);
+    if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+size_t kfec_get_K(const kfec_ctx *ctx) { return ctx ? ctx->K : 0; }
+size_t kfec_get_N(const kfec_ctx *ctx) { return ctx ? ctx->N : 0; }
+
+int kfec_enc_matrix(const kfec_ctx *ctx, uint8_t *enc)
+{
+    if (!ctx || !enc) return KFEC_EINVAL;
+    std::memcpy(enc, ctx->h_enc.data(), ctx->h_enc.size());
+    return KFEC_OK;
+}
+
+int kfec_encode(const kfec_ctx *cctx, const uint8_t *input, size_t data_length, size_t block_size,
+                uint8_t *parity_out)
+{
+    kfec_ctx *ctx = const_cast<kfec_ctx *>(cctx);
+    if (!ctx) return KFEC_EINVAL;
+    const size_t K = ctx->K, N = ctx->N, R = N - K, B = block_size;
+    // fecpp.cpp:497-498; plus the cases where the reference is undefined (B = 0, short input)
+    if (input == nullptr || B == 0 || (data_length / B) % K != 0 || data_length < K * B) return KFEC_EMPTY;
+    if (R == 0) return KFEC_OK;
+    if (!parity_out) return KFEC_EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (set_dev(ctx)) return KFEC_EHIP;
+    const size_t off_par = al256(K * B);
+    int rc = ensure_stage(ctx, off_par + al256(R * B));
+    if (rc) return rc;
+    uint8_t *d_data = ctx->d_stage, *d_par = ctx->d_stage + off_par;
+    if (hipMemcpyAsync(d_data, input, K * B, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) return KFEC_EHIP;
+    rc = kfec::launch_encode(ctx->di, ctx->d_enc, (int)K, (int)N, 1, B, B, d_data, d_par, ctx->stream);
+    if (rc) return KFEC_EHIP;
+    if (hipMemcpyAsync(parity_out, d_par, R * B, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) return KFEC_EHIP;
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return KFEC_EHIP;
+    return KFEC_OK;
+}
+
+int kfec_decode(const kfec_ctx *cctx, const size_t *share_ids, const uint8_t *const *share_ptrs, size_t n_shares,
+                size_t share_size, size_t *out_ids, uint8_t *out, size_t *n_out)
+{
+    kfec_ctx *ctx = const_cast<kfec_ctx *>(cctx);
+    if (!ctx || !n_out) return KFEC_EINVAL;
+    *n_out = 0;
+    const size_t K = ctx->K, N = ctx->N, R = N - K, B = share_size;
+    if (n_shares < K) return KFEC_EMPTY;  // fecpp.cpp:520-521
+    if (!share_ids || !share_ptrs) return KFEC_EINVAL;
+    for (size_t i = 1; i < n_shares; ++i)
+        if (share_ids[i] <= share_ids[i - 1]) return KFEC_EINVAL;  // must be a std::map's key order
+    // fecpp.cpp:550-551: a chosen id >= N returns {}.  Ids >= N are the highest ids, so they are chosen
+    // first whenever a data share is missing; with none missing the reference returns {} anyway.
+    if (n_shares && share_ids[n_shares - 1] >= N) return KFEC_EMPTY;
+    if (B == 0) return KFEC_OK;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (set_dev(ctx)) return KFEC_EHIP;
+    const size_t rs = kfec::record_stride(K, R);
+    const size_t o_data = 0, o_par = al256(K * B), o_out = o_par + al256(R * B), o_mask = o_out + al256(R * B);
+    const size_t o_idx = o_mask + 256, o_st = o_idx + al256(R + 1), o_rec = o_st + 256, total = o_rec + al256(rs);
+    int rc = ensure_stage(ctx, total);
+    if (rc) return rc;
+    uint8_t *base = ctx->d_stage;
+    uint64_t mask[4] = {0, 0, 0, 0};
+    for (size_t i = 0; i < n_shares; ++i) {
+        const size_t s = share_ids[i];
+        mask[s >> 6] |= 1ull << (s & 63);
+        uint8_t *dst = (s < K) ? base + o_data + s * B : base + o_par + (s - K) * B;
+        if (hipMemcpyAsync(dst, share_ptrs[i], B, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) return KFEC_EHIP;
+    }
+    if (hipMemcpyAsync(base + o_mask, mask, sizeof(mask), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+        return KFEC_EHIP;
+    rc = kfec::launch_decode(ctx->di, ctx->d_enc, (int)K, (int)N, 1, B, B, base + o_data, base + o_par,
+                             reinterpret_cast<const uint64_t *>(base + o_mask), base + o_out, base + o_idx,
+                             base + o_st, base + o_rec, ctx->stream);
+    if (rc) return KFEC_EHIP;
+    uint8_t idx[256], st = 0;
+    if (R && hipMemcpyAsync(idx, base + o_idx, R, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) return KFEC_EHIP;
+    if (hipMemcpyAsync(&st, base + o_st, 1, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) return KFEC_EHIP;
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return KFEC_EHIP;
+    if (st == KFEC_GROUP_EMPTY) return KFEC_EMPTY;
+    if (st == KFEC_GROUP_SINGULAR) return KFEC_ESINGULAR;
+    size_t m = 0;
+    while (m < R && idx[m] != 0xFF) ++m;
+    if (m) {
+        if (!out || !out_ids) return KFEC_EINVAL;
+        if (hipMemcpyAsync(out, base + o_out, m * B, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+            return KFEC_EHIP;
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess) return KFEC_EHIP;
+        for (size_t t = 0; t < m; ++t) out_ids[t] = idx[t];
+    }
+    *n_out = m;
+    return KFEC_OK;
+}
+
+int kfec_encode_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, const void *d_data, void *d_parity,
+                      void *stream)
+{
+    if (!ctx || pitch < B || (G && (!d_data || (!d_parity && ctx->N > ctx->K)))) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_encode(ctx->di, ctx->d_enc, (int)ctx->K, (int)ctx->N, G, B, pitch, d_data, d_parity,
+                               as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
+size_t kfec_decode_workspace_size(const kfec_ctx *ctx, size_t G)
+{
+    return ctx ? G * kfec::record_stride(ctx->K, ctx->N - ctx->K) : 0;
+}
+
+int kfec_decode_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, const void *d_data,
+                      const void *d_parity, const uint64_t *d_present, void *d_out, uint8_t *d_out_idx,
+                      uint8_t *d_status, void *d_workspace, void *stream)
+{
+    if (!ctx || pitch < B) return KFEC_EINVAL;
+    if (G && (!d_present || !d_status || !d_workspace || !d_data)) return KFEC_EINVAL;
+    if (G && ctx->N > ctx->K && (!d_parity || !d_out || !d_out_idx)) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_decode(ctx->di, ctx->d_enc, (int)ctx->K, (int)ctx->N, G, B, pitch, d_data, d_parity,
+                               d_present, d_out, d_out_idx, d_status, d_workspace, as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
+int kfec_synth(const kfec_ctx *ctx, uint64_t seed, size_t g0, size_t G, size_t s0, size_t ns, size_t B, size_t pitch,
+               void *d_out, void *stream)
+{
+    if (!ctx || pitch < B || (G && ns && !d_out)) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_synth(seed, (int)ctx->N, g0, G, s0, ns, B, pitch, d_out, as_stream(stream)) ? KFEC_EHIP
+                                                                                                     : KFEC_OK;
+}
+
+int kfec_erasure_masks(const kfec_ctx *ctx, uint64_t seed, size_t g0, size_t G, size_t pool, size_t count_max,
+                       int random_count, uint64_t *d_present, void *stream)
+{
+    if (!ctx || pool > ctx->N || (G && !d_present)) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_erasure_masks(seed, (int)ctx->N, g0, G, pool, count_max, random_count, d_present,
+                                      as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
+int kfec_verify_recovered(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, const void *d_data,
+                          const void *d_out, const uint8_t *d_out_idx, uint64_t *d_mismatch, void *stream)
+{
+    if (!ctx || pitch < B || !d_mismatch) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_verify((int)ctx->K, (int)ctx->N, G, B, pitch, d_data, d_out, d_out_idx, d_mismatch,
+                               as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
+}  // extern "C"

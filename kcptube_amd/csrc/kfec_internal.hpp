@@ -1,0 +1,35 @@
+// kfec_internal.hpp -- launch interface between the C ABI (kfec_api.cpp) and the kernels (kfec_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace kfec {
+
+// Per-group decode record written by the prep kernels and read by the MAC kernel (group-major, so the
+// few records a workgroup needs per iteration are a couple of contiguous cache lines):
+//   [0] status (KFEC_GROUP_*), [1] m = missing data shards, [2..3] 0,
+//   [4, 4+K)            src[j]    share id used as column j of the selected K x K system,
+//   [4+K, 4+K+R*K)      coef[u][j] row u (u < m) of the inverse decode matrix for missing shard u.
+inline size_t record_stride(size_t K, size_t R) { return (4 + K + R * K + 15) & ~size_t(15); }
+
+struct DeviceInfo {
+    int device = -1;
+    int cus = 0;
+};
+
+// every launcher returns 0 or a negative KFEC_E* code
+int launch_build_matrix(uint8_t *d_enc, int K, int N, hipStream_t s);
+int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, size_t B, size_t pitch,
+                  const void *d_data, void *d_parity, hipStream_t s);
+int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, size_t B, size_t pitch,
+                  const void *d_data, const void *d_parity, const uint64_t *d_present, void *d_out,
+                  uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s);
+int launch_synth(uint64_t seed, int N, size_t g0, size_t G, size_t s0, size_t ns, size_t B, size_t pitch,
+                 void *d_out, hipStream_t s);
+int launch_erasure_masks(uint64_t seed, int N, size_t g0, size_t G, size_t pool, size_t count_max,
+                         int random_count, uint64_t *d_present, hipStream_t s);
+int launch_verify(int K, int N, size_t G, size_t B, size_t pitch, const void *d_data, const void *d_out,
+                  const uint8_t *d_out_idx, uint64_t *d_mismatch, hipStream_t s);
+
+}  // namespace kfec

@@ -1,0 +1,881 @@
+// kfec_kernels.hip -- hand-written gfx950 (CDNA4) kernels of the kfec Reed-Solomon coder.
+//
+// Reference semantics (all /root/reference/src/3rd_party/):
+//   matrix   fecpp.cpp:368-415, 453-490   enc = [I_K ; Vbot * Vtop^-1]  (build_matrix_kernel)
+//   encode   fecpp.cpp:495-513            parity_r = XOR_j enc[K+r][j] * D_j   (mac_kernel<.., false>)
+//   decode   fecpp.cpp:518-587            share selection + K x K inverse + m output rows
+//                                           (decode_prep_* + mac_kernel<.., true>)
+//   addmul   fecpp.cpp:170-223, fecpp_ssse3.cpp:541-575   z ^= c * x  (the "perm MAC" below)
+//
+// Design (DESIGN.md has the numbers):
+// * perm MAC.  c * x for a constant c is linear over GF(2), so c*x = c*(x & 7) ^ c*(x & 0x38) ^ c*(x & 0xC0).
+//   Each term is an 8- or 4-entry table lookup, and v_perm_b32 does 4 such byte lookups (one per byte of a
+//   dword) in one VALU op.  Per data dword and coefficient: 3 v_perm_b32 + XORs; the 3 selector extractions
+//   are shared by all coefficients of a data dword.  No LDS traffic per data byte and no bank conflicts:
+//   the ~5 table dwords per coefficient are read once per shard per lane (LDS broadcast reads).
+// * Flattened work: one lane = one (group, V-byte column) item; consecutive lanes take consecutive columns
+//   (coalesced 1 KiB per wave-instruction at V = 16), wrapping into the next group.  Persistent grid-stride
+//   over items.  A workgroup iteration touches <= GMAX groups, whose per-group decode tables are expanded
+//   into LDS at the start of the iteration.
+// * Decode coefficients: per group only the m x m sub-system of the missing rows is inverted (Gauss-Jordan
+//   with LDS log/antilog tables); the rest of the K x K inverse follows by one product.  The inverse is
+//   unique, so the coefficients equal the reference's K x K Gauss-Jordan result bit for bit.
+#include "kfec_gf.hpp"
+#include "kfec_internal.hpp"
+
+#include <algorithm>
+
+namespace kfec {
+
+__constant__ GfTables c_gf = make_gf_tables();
+
+static constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void stage_gf(uint8_t *s_exp, uint8_t *s_log)
+{
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) s_exp[i] = c_gf.exp[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_log[i] = c_gf.log[i];
+}
+
+__device__ __forceinline__ uint32_t gmul(const uint8_t *e, const uint8_t *l, uint32_t a, uint32_t b)
+{
+    return (a && b) ? e[l[a] + l[b]] : 0u;
+}
+
+__device__ __forceinline__ uint32_t ginv(const uint8_t *e, const uint8_t *l, uint32_t a)
+{
+    return a ? e[255 - l[a]] : 0u;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// mask word q of a present bitmap to ids < n
+__device__ __forceinline__ uint64_t bits_below(int n, int q)
+{
+    const int v = n - 64 * q;
+    return v <= 0 ? 0ull : (v >= 64 ? ~0ull : ((1ull << v) - 1ull));
+}
+
+// ---------------------------------------------------------------------------------------------------
+// (A6) encoding matrix: Lagrange closed form of Vbot * Vtop^-1.
+// Evaluation points x_0 = 0, x_i = alpha^i (i >= 1) -- the rows of the reference's Vandermonde matrix
+// (fecpp.cpp:401 uses p_0 = 0, p_row = GF_EXP[row]; fecpp.cpp:467 alpha^(row*col)).  Systematic row r >= K,
+// column j:  enc[r][j] = L_j(x_r) = prod_{i<K, i!=j} (x_r ^ x_i) / (x_j ^ x_i), summed in the log domain.
+// ---------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) build_matrix_kernel(uint8_t *enc, int K, int N)
+{
+    __shared__ uint8_t s_exp[512], s_log[256];
+    stage_gf(s_exp, s_log);
+    __syncthreads();
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= N * K) return;
+    const int r = idx / K, j = idx - r * K;
+    if (r < K) {
+        enc[idx] = (r == j) ? 1 : 0;
+        return;
+    }
+    const uint32_t xr = s_exp[r], xj = (j == 0) ? 0u : s_exp[j];  // r >= 1 here; s_exp[255] == 1
+    uint32_t ln = 0, ld = 0;
+    for (int i = 0; i < K; ++i) {
+        if (i == j) continue;
+        const uint32_t xi = (i == 0) ? 0u : s_exp[i];
+        ln += s_log[xr ^ xi];
+        ld += s_log[xj ^ xi];
+    }
+    int e = (int)(ln % 255u) - (int)(ld % 255u);
+    if (e < 0) e += 255;
+    enc[idx] = s_exp[e];
+}
+
+int launch_build_matrix(uint8_t *d_enc, int K, int N, hipStream_t s)
+{
+    const int total = N * K;
+    hipLaunchKernelGGL(build_matrix_kernel, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0, s, d_enc, K, N);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// (A11/A12) decode preparation: share selection (fecpp.cpp:528-548), the m x m inverse and the
+// coefficient rows of the missing data shards.  One thread per group, for m <= MAXM.
+//   Selection: data share i fills row i; the missing rows, ascending, take the highest present ids,
+//   descending.  With >= K shares present those are always parity ids (present parity >= m).
+//   With S[t][u] = enc[P_t][M_u] (t,u < m; P_t the parity used for missing row M_t):
+//     coef[u][M_t] = Sinv[u][t]                                  (the parity share in column M_t)
+//     coef[u][k]   = XOR_t Sinv[u][t] * enc[P_t][k],  k present    (data shares)
+//   S is a square submatrix of the parity part of a systematic MDS generator, so every leading minor is
+//   non-singular and elimination needs no pivot search; a zero pivot is still detected and reported.
+// ---------------------------------------------------------------------------------------------------
+struct PrepArgs {
+    const uint64_t *present;
+    const uint8_t *enc;  // N x K
+    uint8_t *rec;
+    uint8_t *out_idx;
+    uint8_t *status;
+    uint64_t G;
+    int K, N, R;
+    uint32_t rec_stride;
+};
+
+__device__ __forceinline__ int pop_lowest(uint64_t (&w)[4])
+{
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (w[q]) {
+            const int b = __ffsll((unsigned long long)w[q]) - 1;
+            w[q] &= w[q] - 1;
+            return q * 64 + b;
+        }
+    return -1;
+}
+
+__device__ __forceinline__ int pop_highest(uint64_t (&w)[4])
+{
+#pragma unroll
+    for (int q = 3; q >= 0; --q)
+        if (w[q]) {
+            const int b = 63 - __clzll((unsigned long long)w[q]);
+            w[q] &= ~(1ull << b);
+            return q * 64 + b;
+        }
+    return -1;
+}
+
+__device__ __forceinline__ void write_empty(const PrepArgs &a, uint64_t g, uint8_t st)
+{
+    uint8_t *rec = a.rec + g * a.rec_stride;
+    rec[0] = st;
+    rec[1] = 0;
+    for (int t = 0; t < a.R; ++t) a.out_idx[g * a.R + t] = 0xFF;
+    a.status[g] = st;
+}
+
+template <int MAXM>
+__global__ void __launch_bounds__(kBlock) decode_prep_small(PrepArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *s_exp = smem, *s_log = smem + 512, *s_E = smem + 768;  // s_E: parity rows, R x K
+    stage_gf(s_exp, s_log);
+    const int K = a.K, N = a.N, R = a.R;
+    for (int i = threadIdx.x; i < R * K; i += blockDim.x) s_E[i] = a.enc[K * K + i];
+    __syncthreads();
+
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < a.G;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t w[4], dm[4];
+        int cnt = 0, m = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            w[q] = a.present[g * 4 + q] & bits_below(N, q);
+            dm[q] = ~w[q] & bits_below(K, q);
+            cnt += __popcll(w[q]);
+            m += __popcll(dm[q]);
+        }
+        if (cnt < K) {
+            write_empty(a, g, 1);
+            continue;
+        }
+        uint8_t *rec = a.rec + g * a.rec_stride;
+        int M[MAXM], P[MAXM];
+        uint64_t dmw[4] = {dm[0], dm[1], dm[2], dm[3]};
+        uint64_t pw[4] = {w[0], w[1], w[2], w[3]};
+#pragma unroll
+        for (int t = 0; t < MAXM; ++t) {
+            M[t] = (t < m) ? pop_lowest(dmw) : 0;
+            P[t] = (t < m) ? pop_highest(pw) : K;
+        }
+        // A = S extended by the identity to MAXM x MAXM; Iv accumulates the inverse
+        uint32_t A[MAXM][MAXM], Iv[MAXM][MAXM];
+#pragma unroll
+        for (int t = 0; t < MAXM; ++t)
+#pragma unroll
+            for (int u = 0; u < MAXM; ++u) {
+                A[t][u] = (t < m && u < m) ? s_E[(P[t] - K) * K + M[u]] : (uint32_t)(t == u);
+                Iv[t][u] = (uint32_t)(t == u);
+            }
+        bool singular = false;
+#pragma unroll
+        for (int c = 0; c < MAXM; ++c) {
+            if (c < m) {
+                const uint32_t piv = A[c][c];
+                singular |= (piv == 0);
+                const uint32_t inv = ginv(s_exp, s_log, piv);
+#pragma unroll
+                for (int u = 0; u < MAXM; ++u) {
+                    A[c][u] = gmul(s_exp, s_log, A[c][u], inv);
+                    Iv[c][u] = gmul(s_exp, s_log, Iv[c][u], inv);
+                }
+#pragma unroll
+                for (int r = 0; r < MAXM; ++r) {
+                    if (r == c) continue;
+                    const uint32_t f = A[r][c];
+                    if (f) {
+#pragma unroll
+                        for (int u = 0; u < MAXM; ++u) {
+                            A[r][u] ^= gmul(s_exp, s_log, f, A[c][u]);
+                            Iv[r][u] ^= gmul(s_exp, s_log, f, Iv[c][u]);
+                        }
+                    }
+                }
+            }
+        }
+        if (singular) {
+            write_empty(a, g, 2);
+            continue;
+        }
+        rec[0] = 0;
+        rec[1] = (uint8_t)m;
+        rec[2] = rec[3] = 0;
+        // log of the inverse, so each product below is one antilog lookup
+        uint32_t lS[MAXM][MAXM];
+#pragma unroll
+        for (int u = 0; u < MAXM; ++u)
+#pragma unroll
+            for (int t = 0; t < MAXM; ++t) lS[u][t] = Iv[u][t] ? s_log[Iv[u][t]] : 0x1FFu;
+        uint8_t *src = rec + 4, *coef = rec + 4 + K;
+        for (int j = 0; j < K; ++j) {
+            const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
+            if (miss) {
+                // rank of j among the missing ids
+                int t = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    t += (q < (j >> 6)) ? __popcll(dm[q]) : (q == (j >> 6) ? __popcll(dm[q] & ((1ull << (j & 63)) - 1ull)) : 0);
+                int pt = 0;
+#pragma unroll
+                for (int tt = 0; tt < MAXM; ++tt) pt = (tt == t) ? P[tt] : pt;
+                src[j] = (uint8_t)pt;
+#pragma unroll
+                for (int u = 0; u < MAXM; ++u) {
+                    if (u < m) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (int tt = 0; tt < MAXM; ++tt) v = (tt == t) ? Iv[u][tt] : v;
+                        coef[u * K + j] = (uint8_t)v;
+                    }
+                }
+            } else {
+                src[j] = (uint8_t)j;
+                uint32_t le[MAXM];
+#pragma unroll
+                for (int t = 0; t < MAXM; ++t) {
+                    const uint32_t e = (t < m) ? s_E[(P[t] - K) * K + j] : 0u;
+                    le[t] = e ? s_log[e] : 0x1FFu;
+                }
+#pragma unroll
+                for (int u = 0; u < MAXM; ++u) {
+                    if (u < m) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (int t = 0; t < MAXM; ++t)
+                            if (t < m && lS[u][t] != 0x1FFu && le[t] != 0x1FFu) v ^= s_exp[lS[u][t] + le[t]];
+                        coef[u * K + j] = (uint8_t)v;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < MAXM; ++t)
+            if (t < R) a.out_idx[g * R + t] = (t < m) ? (uint8_t)M[t] : (uint8_t)0xFF;
+        for (int t = MAXM; t < R; ++t) a.out_idx[g * R + t] = 0xFF;
+        a.status[g] = 0;
+    }
+}
+
+// General m (up to min(K, R) <= 128): one wave per group, lanes over matrix elements.
+__global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int K = a.K, N = a.N, R = a.R;
+    uint8_t *s_exp = smem, *s_log = smem + 512;
+    uint8_t *s_M = smem + 768, *s_P = s_M + 256, *s_rank = s_P + 256, *s_f = s_rank + 256;  // 4 x 256
+    uint8_t *s_E = s_f + 256;                                                              // R x K
+    uint8_t *s_A = s_E + ((R * K + 15) & ~15);                                             // MMAX x 2*MMAX
+    const int lane = threadIdx.x;
+    stage_gf(s_exp, s_log);
+    for (int i = lane; i < R * K; i += 64) s_E[i] = a.enc[K * K + i];
+    __syncthreads();
+
+    for (uint64_t g = blockIdx.x; g < a.G; g += gridDim.x) {
+        uint64_t w[4], dm[4];
+        int cnt = 0, m = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            w[q] = a.present[g * 4 + q] & bits_below(N, q);
+            dm[q] = ~w[q] & bits_below(K, q);
+            cnt += __popcll(w[q]);
+            m += __popcll(dm[q]);
+        }
+        uint8_t *rec = a.rec + g * a.rec_stride;
+        if (cnt < K || m > MMAX) {
+            if (lane == 0) {
+                rec[0] = 1;
+                rec[1] = 0;
+                a.status[g] = 1;
+            }
+            for (int t = lane; t < R; t += 64) a.out_idx[g * R + t] = 0xFF;
+            __syncthreads();
+            continue;
+        }
+        // missing data ids ascending, and their ranks
+        int base = 0;
+        for (int q = 0; q < 4; ++q) {
+            const bool f = (dm[q] >> lane) & 1ull;
+            const uint64_t below = __popcll(dm[q] & ((1ull << lane) - 1ull));
+            if (f) {
+                s_M[base + below] = (uint8_t)(q * 64 + lane);
+                s_rank[q * 64 + lane] = (uint8_t)(base + below);
+            }
+            base += __popcll(dm[q]);
+        }
+        // highest present ids, descending
+        base = 0;
+        for (int q = 3; q >= 0; --q) {
+            const bool f = (w[q] >> lane) & 1ull;
+            const int above = __popcll(lane == 63 ? 0ull : (w[q] & ~((2ull << lane) - 1ull)));
+            if (f && base + above < m) s_P[base + above] = (uint8_t)(q * 64 + lane);
+            base += __popcll(w[q]);
+        }
+        __syncthreads();
+        const int W2 = 2 * m;
+        for (int e = lane; e < m * W2; e += 64) {
+            const int t = e / W2, c = e - t * W2;
+            s_A[t * W2 + c] = (c < m) ? s_E[(s_P[t] - K) * K + s_M[c]] : (uint8_t)((c - m) == t);
+        }
+        __syncthreads();
+        bool singular = false;
+        for (int c = 0; c < m; ++c) {
+            const uint32_t piv = s_A[c * W2 + c];
+            singular |= (piv == 0);
+            const uint32_t inv = ginv(s_exp, s_log, piv);
+            __syncthreads();
+            for (int col = lane; col < W2; col += 64) s_A[c * W2 + col] = (uint8_t)gmul(s_exp, s_log, s_A[c * W2 + col], inv);
+            for (int r = lane; r < m; r += 64) s_f[r] = s_A[r * W2 + c];
+            __syncthreads();
+            for (int e = lane; e < m * W2; e += 64) {
+                const int r = e / W2, col = e - r * W2;
+                if (r == c) continue;
+                const uint32_t f = s_f[r];
+                if (f) s_A[e] ^= (uint8_t)gmul(s_exp, s_log, f, s_A[c * W2 + col]);
+            }
+            __syncthreads();
+        }
+        if (singular) {
+            if (lane == 0) {
+                rec[0] = 2;
+                rec[1] = 0;
+                a.status[g] = 2;
+            }
+            for (int t = lane; t < R; t += 64) a.out_idx[g * R + t] = 0xFF;
+            __syncthreads();
+            continue;
+        }
+        uint8_t *src = rec + 4, *coef = rec + 4 + K;
+        for (int j = lane; j < K; j += 64) {
+            const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
+            src[j] = miss ? s_P[s_rank[j]] : (uint8_t)j;
+        }
+        for (int e = lane; e < m * K; e += 64) {
+            const int u = e / K, j = e - u * K;
+            const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
+            uint32_t v = 0;
+            if (miss) {
+                v = s_A[u * W2 + m + s_rank[j]];
+            } else {
+                for (int t = 0; t < m; ++t) v ^= gmul(s_exp, s_log, s_A[u * W2 + m + t], s_E[(s_P[t] - K) * K + j]);
+            }
+            coef[u * K + j] = (uint8_t)v;
+        }
+        for (int t = lane; t < R; t += 64) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
+        if (lane == 0) {
+            rec[0] = 0;
+            rec[1] = (uint8_t)m;
+            rec[2] = rec[3] = 0;
+            a.status[g] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// (A4/A5/A8/A11) perm-MAC kernel: out[g][row] = XOR_j coef[row][j] * share_j[g]  over V-byte columns.
+// ---------------------------------------------------------------------------------------------------
+struct MacArgs {
+    const uint8_t *data;    // [G][K][pitch]
+    const uint8_t *parity;  // [G][R][pitch]
+    uint8_t *out;           // encode: parity, decode: recovered [G][R][pitch]
+    const uint8_t *enc;     // N x K encoding matrix (encode)
+    const uint8_t *rec;     // per-group records (decode)
+    uint64_t pitch;
+    uint32_t total;         // G * cols work items
+    uint32_t cols;          // granules per shard
+    uint32_t G, K, R, B;
+    uint32_t rec_stride;
+    uint32_t JC;            // shards per LDS chunk
+    uint32_t gmax;          // group slots per chunk
+};
+
+template <int VEC>
+struct Gran {
+    static constexpr int W = VEC >= 4 ? VEC / 4 : 1;
+    uint32_t d[W];
+};
+
+template <int VEC>
+__device__ __forceinline__ Gran<VEC> load_gran(const uint8_t *p, uint32_t col, uint32_t B)
+{
+    Gran<VEC> v;
+    if constexpr (VEC == 16) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(p);
+        v.d[0] = x.x; v.d[1] = x.y; v.d[2] = x.z; v.d[3] = x.w;
+    } else if constexpr (VEC == 8) {
+        const uint2 x = *reinterpret_cast<const uint2 *>(p);
+        v.d[0] = x.x; v.d[1] = x.y;
+    } else if constexpr (VEC == 4) {
+        v.d[0] = *reinterpret_cast<const uint32_t *>(p);
+    } else {  // bytewise: 4 bytes at p, only those below B
+        uint32_t x = 0;
+        const uint32_t b0 = col * 4;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (b0 + b < B) x |= (uint32_t)p[b] << (8 * b);
+        v.d[0] = x;
+    }
+    return v;
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_gran(uint8_t *p, const uint32_t *d, uint32_t col, uint32_t B)
+{
+    if constexpr (VEC == 16) {
+        *reinterpret_cast<uint4 *>(p) = make_uint4(d[0], d[1], d[2], d[3]);
+    } else if constexpr (VEC == 8) {
+        *reinterpret_cast<uint2 *>(p) = make_uint2(d[0], d[1]);
+    } else if constexpr (VEC == 4) {
+        *reinterpret_cast<uint32_t *>(p) = d[0];
+    } else {
+        const uint32_t b0 = col * 4;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (b0 + b < B) p[b] = (uint8_t)(d[0] >> (8 * b));
+    }
+}
+
+// z ^= c * x for 4 bytes, c given by its 5 permute tables (kfec_gf.hpp gf_perm_tables)
+__device__ __forceinline__ uint32_t perm_mul(const uint32_t *t, uint32_t s0, uint32_t s1, uint32_t s2)
+{
+    return __builtin_amdgcn_perm(t[1], t[0], s0) ^ __builtin_amdgcn_perm(t[3], t[2], s1) ^
+           __builtin_amdgcn_perm(t[4], t[4], s2);
+}
+
+template <int MT>
+struct MacLayout {
+    static constexpr int TBL_DW = ((5 * MT + 3) / 4) * 4;  // table dwords per (group, shard)
+    static constexpr int ENTRY = 16 + 4 * TBL_DW;          // + 8-byte share pointer, 8 pad
+};
+
+// expand coefficients of shards [c0, c0+nj) for group slots [0, ng) into LDS entries
+template <int MT, bool DEC>
+__device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uint32_t gfirst, uint32_t ng,
+                                           uint32_t c0, uint32_t nj, uint32_t row0)
+{
+    using L = MacLayout<MT>;
+    const uint32_t items = ng * nj * MT;
+    for (uint32_t e = threadIdx.x; e < items; e += blockDim.x) {
+        const uint32_t r = e % MT, q = e / MT;
+        const uint32_t jj = q % nj, gs = q / nj;
+        const uint32_t j = c0 + jj, u = row0 + r;
+        uint8_t *ent = s_ent + (gs * a.JC + jj) * L::ENTRY;
+        uint32_t c = 0;
+        if constexpr (DEC) {
+            const uint32_t g = gfirst + gs;
+            const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
+            const uint32_t st = rec[0], m = rec[1];
+            if (st == 0 && u < m) c = rec[4 + a.K + u * a.K + j];
+            if (r == 0) {
+                const uint32_t src = rec[4 + j];
+                const uint8_t *p = (src < a.K) ? a.data + ((uint64_t)g * a.K + src) * a.pitch
+                                               : a.parity + ((uint64_t)g * a.R + (src - a.K)) * a.pitch;
+                *reinterpret_cast<const uint8_t **>(ent) = p;
+            }
+        } else {
+            if (u < a.R) c = a.enc[(uint64_t)(a.K + u) * a.K + j];
+        }
+        uint32_t t[5];
+        gf_perm_tables(c, t);
+        uint32_t *tp = reinterpret_cast<uint32_t *>(ent + 16) + 5 * r;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) tp[i] = t[i];
+    }
+}
+
+template <int VEC, int MT, bool DEC>
+__global__ void __launch_bounds__(kBlock) mac_kernel(MacArgs a)
+{
+    using L = MacLayout<MT>;
+    constexpr int W = Gran<VEC>::W;
+    constexpr int PD = 4;  // shards in flight per lane
+    constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
+
+    const uint32_t row0 = blockIdx.y * MT;
+    const uint32_t K = a.K, cols = a.cols;
+    const bool enc_once = !DEC && K <= a.JC;
+    if (enc_once) {
+        mac_expand<MT, false>(a, s_ent, 0, 1, 0, K, row0);
+        __syncthreads();
+    }
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t base = blockIdx.x * kBlock; base < a.total; base += stride) {
+        const uint32_t item = base + threadIdx.x;
+        const bool in = item < a.total;
+        const uint32_t g = in ? item / cols : 0;
+        const uint32_t col = in ? item - g * cols : 0;
+        const uint32_t gfirst = base / cols;
+        const uint32_t glast = min(base + kBlock - 1, a.total - 1) / cols;
+        const uint32_t ng = glast - gfirst + 1;
+        const uint32_t gs = DEC ? g - gfirst : 0;
+
+        uint32_t rows = 0;
+        if (in) {
+            if constexpr (DEC) {
+                const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
+                const uint32_t st = rec[0], m = rec[1];
+                rows = (st == 0 && m > row0) ? min((uint32_t)MT, m - row0) : 0u;
+            } else {
+                rows = a.R > row0 ? min((uint32_t)MT, a.R - row0) : 0u;
+            }
+        }
+        uint32_t acc[MT][W];
+#pragma unroll
+        for (int r = 0; r < MT; ++r)
+#pragma unroll
+            for (int w = 0; w < W; ++w) acc[r][w] = 0;
+
+        const uint8_t *enc_base = a.data + ((uint64_t)g * K) * a.pitch + (uint64_t)col * VB;
+        for (uint32_t c0 = 0; c0 < K; c0 += a.JC) {
+            const uint32_t nj = min(a.JC, K - c0);
+            if (!enc_once) {
+                __syncthreads();
+                mac_expand<MT, DEC>(a, s_ent, gfirst, DEC ? ng : 1u, c0, nj, row0);
+                __syncthreads();
+            }
+            if (rows == 0) continue;
+            const uint8_t *ent0 = s_ent + (gs * a.JC) * L::ENTRY;
+            auto share_ptr = [&](uint32_t jj) -> const uint8_t * {
+                if constexpr (DEC) {
+                    return *reinterpret_cast<const uint8_t *const *>(ent0 + jj * L::ENTRY) + (uint64_t)col * VB;
+                } else {
+                    return enc_base + (uint64_t)(c0 + jj) * a.pitch;
+                }
+            };
+            Gran<VEC> x[PD];
+#pragma unroll
+            for (int u = 0; u < PD; ++u)
+                if ((uint32_t)u < nj) x[u] = load_gran<VEC>(share_ptr(u), col, a.B);
+            for (uint32_t jb = 0; jb < nj; jb += PD) {
+#pragma unroll
+                for (int u = 0; u < PD; ++u) {
+                    const uint32_t jj = jb + u;
+                    if (jj < nj) {
+                        const Gran<VEC> cur = x[u];
+                        if (jj + PD < nj) x[u] = load_gran<VEC>(share_ptr(jj + PD), col, a.B);
+                        uint32_t t[L::TBL_DW];
+                        const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + jj * L::ENTRY + 16);
+#pragma unroll
+                        for (int i = 0; i < L::TBL_DW / 4; ++i) {
+                            const uint4 q = tv[i];
+                            t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+                        }
+#pragma unroll
+                        for (int w = 0; w < W; ++w) {
+                            const uint32_t xv = cur.d[w];
+                            const uint32_t s0 = xv & 0x07070707u;
+                            const uint32_t s1 = (xv >> 3) & 0x07070707u;
+                            const uint32_t s2 = (xv >> 6) & 0x03030303u;
+#pragma unroll
+                            for (int r = 0; r < MT; ++r) acc[r][w] ^= perm_mul(t + 5 * r, s0, s1, s2);
+                        }
+                    }
+                }
+            }
+        }
+        if (rows) {
+            const uint64_t obase = ((uint64_t)g * a.R + row0) * a.pitch + (uint64_t)col * VB;
+#pragma unroll
+            for (int r = 0; r < MT; ++r)
+                if ((uint32_t)r < rows) store_gran<VEC>(a.out + obase + (uint64_t)r * a.pitch, acc[r], col, a.B);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// host-side launch helpers
+// ---------------------------------------------------------------------------------------------------
+static int pick_vec(size_t pitch, std::initializer_list<const void *> ptrs)
+{
+    for (int v : {16, 8, 4}) {
+        bool ok = (pitch % v) == 0;
+        for (const void *p : ptrs) ok = ok && (reinterpret_cast<uintptr_t>(p) % v) == 0;
+        if (ok) return v;
+    }
+    return 1;
+}
+
+static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
+
+template <int VEC, int MT, bool DEC>
+static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
+{
+    using L = MacLayout<MT>;
+    const size_t lds = (size_t)a.gmax * a.JC * L::ENTRY;
+    uint32_t want = (a.total + kBlock - 1) / kBlock;
+    uint32_t cap = (uint32_t)std::max(1, di.cus) * 8u / (uint32_t)std::max(1, tiles);
+    const uint32_t gx = std::max(1u, std::min(want, std::max(cap, 1u)));
+    hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC>), dim3(gx, tiles), dim3(kBlock), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <bool DEC>
+static int dispatch_mac(const DeviceInfo &di, int vec, int mt, MacArgs a, int tiles, hipStream_t s)
+{
+#define KFEC_MT_CASES(V)                                                     \
+    switch (mt) {                                                            \
+    case 1: return run_mac<V, 1, DEC>(di, a, tiles, s);                      \
+    case 2: return run_mac<V, 2, DEC>(di, a, tiles, s);                      \
+    case 3: return run_mac<V, 3, DEC>(di, a, tiles, s);                      \
+    case 4: return run_mac<V, 4, DEC>(di, a, tiles, s);                      \
+    default: return run_mac<V, 8, DEC>(di, a, tiles, s);                     \
+    }
+    switch (vec) {
+    case 16: KFEC_MT_CASES(16)
+    case 8: KFEC_MT_CASES(8)
+    case 4: KFEC_MT_CASES(4)
+    default: KFEC_MT_CASES(1)
+    }
+#undef KFEC_MT_CASES
+}
+
+static int entry_bytes(int mt)
+{
+    switch (mt) {
+    case 1: return MacLayout<1>::ENTRY;
+    case 2: return MacLayout<2>::ENTRY;
+    case 3: return MacLayout<3>::ENTRY;
+    case 4: return MacLayout<4>::ENTRY;
+    default: return MacLayout<8>::ENTRY;
+    }
+}
+
+static constexpr size_t kLdsBudget = 32 * 1024;
+static constexpr size_t kMaxItemsPerLaunch = 0x7FFFFFFFu;
+
+// split G into launches whose item count fits 32-bit indexing
+template <typename F>
+static int for_group_ranges(size_t G, size_t cols, F &&f)
+{
+    const size_t gmax_launch = std::max<size_t>(1, kMaxItemsPerLaunch / std::max<size_t>(cols, 1));
+    for (size_t g0 = 0; g0 < G; g0 += gmax_launch) {
+        const int rc = f(g0, std::min(gmax_launch, G - g0));
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, size_t B, size_t pitch,
+                  const void *d_data, void *d_parity, hipStream_t s)
+{
+    const int R = N - K;
+    if (R == 0 || G == 0 || B == 0) return 0;
+    const int vec = pick_vec(pitch, {d_data, d_parity});
+    const int vb = vec >= 4 ? vec : 4;
+    const size_t cols = (B + vb - 1) / vb;
+    const int mt = pick_mt(R);
+    const int tiles = (R + mt - 1) / mt;
+    const size_t ent = entry_bytes(mt);
+    const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / ent));
+    return for_group_ranges(G, cols, [&](size_t g0, size_t gn) {
+        MacArgs a{};
+        a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
+        a.parity = nullptr;
+        a.out = static_cast<uint8_t *>(d_parity) + g0 * R * pitch;
+        a.enc = d_enc;
+        a.rec = nullptr;
+        a.pitch = pitch;
+        a.total = (uint32_t)(gn * cols);
+        a.cols = (uint32_t)cols;
+        a.G = (uint32_t)gn;
+        a.K = K; a.R = R; a.B = (uint32_t)B;
+        a.rec_stride = 0;
+        a.JC = JC;
+        a.gmax = 1;
+        return dispatch_mac<false>(di, vec, mt, a, tiles, s);
+    });
+}
+
+int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, size_t B, size_t pitch,
+                  const void *d_data, const void *d_parity, const uint64_t *d_present, void *d_out,
+                  uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s)
+{
+    const int R = N - K;
+    if (G == 0) return 0;
+    uint8_t *rec = static_cast<uint8_t *>(d_workspace);
+    const size_t rs = record_stride(K, R);
+    PrepArgs p{};
+    p.present = d_present;
+    p.enc = d_enc;
+    p.rec = rec;
+    p.out_idx = d_out_idx;
+    p.status = d_status;
+    p.G = G;
+    p.K = K; p.N = N; p.R = R;
+    p.rec_stride = (uint32_t)rs;
+    const int mmax = std::min(K, R);
+    if (mmax <= 8) {
+        const size_t lds = 768 + (size_t)R * K;
+        const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((G + kBlock - 1) / kBlock,
+                                                                                (size_t)std::max(di.cus, 1) * 4));
+        if (mmax <= 4) hipLaunchKernelGGL((decode_prep_small<4>), dim3(blocks), dim3(kBlock), lds, s, p);
+        else hipLaunchKernelGGL((decode_prep_small<8>), dim3(blocks), dim3(kBlock), lds, s, p);
+    } else {
+        const size_t lds = 768 + 4 * 256 + (((size_t)R * K + 15) & ~size_t(15)) + (size_t)mmax * 2 * mmax;
+        const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>(G, (size_t)std::max(di.cus, 1) * 16));
+        hipLaunchKernelGGL(decode_prep_wave, dim3(blocks), dim3(64), lds, s, p, mmax);
+    }
+    if (hipGetLastError() != hipSuccess) return -3;
+    if (R == 0 || B == 0) return 0;
+
+    const int vec = pick_vec(pitch, {d_data, d_parity, d_out});
+    const int vb = vec >= 4 ? vec : 4;
+    const size_t cols = (B + vb - 1) / vb;
+    const int mt = pick_mt(R);
+    const int tiles = (R + mt - 1) / mt;
+    const size_t ent = entry_bytes(mt);
+    return for_group_ranges(G, cols, [&](size_t g0, size_t gn) {
+        const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kBlock - 1) / cols + 2);
+        const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
+        MacArgs a{};
+        a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
+        a.parity = static_cast<const uint8_t *>(d_parity) + g0 * R * pitch;
+        a.out = static_cast<uint8_t *>(d_out) + g0 * R * pitch;
+        a.enc = d_enc;
+        a.rec = rec + g0 * rs;
+        a.pitch = pitch;
+        a.total = (uint32_t)(gn * cols);
+        a.cols = (uint32_t)cols;
+        a.G = (uint32_t)gn;
+        a.K = K; a.R = R; a.B = (uint32_t)B;
+        a.rec_stride = (uint32_t)rs;
+        a.JC = JC;
+        a.gmax = gmax;
+        return dispatch_mac<true>(di, vec, mt, a, tiles, s);
+    });
+}
+
+// ---------------------------------------------------------------------------------------------------
+// synthetic inputs / checks; the CPU definitions are in oracle/rs_oracle.c
+// ---------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) synth_kernel(uint64_t seed, uint32_t N, uint64_t g0, uint64_t G, uint32_t s0,
+                                                       uint32_t ns, uint32_t B, uint64_t pitch, uint8_t *out)
+{
+    const uint64_t Wd = (B + 7) / 8;
+    const uint64_t total = G * ns * Wd;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t w = i % Wd, q = i / Wd;
+        const uint64_t s = q % ns, gl = q / ns;
+        const uint64_t v = splitmix64(seed ^ (((g0 + gl) * N + s0 + s) * Wd + w));
+        uint8_t *dst = out + (gl * ns + s) * pitch + w * 8;
+        if (w * 8 + 8 <= B && (reinterpret_cast<uintptr_t>(dst) & 7) == 0) {
+            *reinterpret_cast<uint64_t *>(dst) = v;
+        } else {
+            for (uint32_t k = 0; k < 8 && w * 8 + k < B; ++k) dst[k] = (uint8_t)(v >> (8 * k));
+        }
+    }
+}
+
+int launch_synth(uint64_t seed, int N, size_t g0, size_t G, size_t s0, size_t ns, size_t B, size_t pitch,
+                 void *d_out, hipStream_t s)
+{
+    if (G == 0 || ns == 0 || B == 0) return 0;
+    hipLaunchKernelGGL(synth_kernel, dim3(4096), dim3(kBlock), 0, s, seed, (uint32_t)N, (uint64_t)g0, (uint64_t)G,
+                       (uint32_t)s0, (uint32_t)ns, (uint32_t)B, (uint64_t)pitch, static_cast<uint8_t *>(d_out));
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+__global__ void __launch_bounds__(kBlock) erasure_kernel(uint64_t seed, uint32_t N, uint64_t g0, uint64_t G, uint32_t pool,
+                                                         uint32_t count_max, int random_count, uint64_t *present)
+{
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const uint64_t gg = g0 + g;
+    uint32_t cnt = count_max;
+    if (random_count) cnt = 1 + (uint32_t)(splitmix64(seed ^ ~gg) % count_max);
+    uint64_t m[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m[q] = bits_below((int)N, q);
+    uint8_t perm[256];
+    for (int i = 0; i < 256; ++i) perm[i] = (uint8_t)i;
+    for (uint32_t t = 0; t < cnt && t < pool; ++t) {
+        const uint64_t r = splitmix64(seed ^ (gg * 0x100u + t));
+        const uint32_t k = t + (uint32_t)(r % (uint64_t)(pool - t));
+        const uint8_t tmp = perm[t];
+        perm[t] = perm[k];
+        perm[k] = tmp;
+        m[perm[t] >> 6] &= ~(1ull << (perm[t] & 63));
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) present[g * 4 + q] = m[q];
+}
+
+int launch_erasure_masks(uint64_t seed, int N, size_t g0, size_t G, size_t pool, size_t count_max, int random_count,
+                         uint64_t *d_present, hipStream_t s)
+{
+    if (G == 0) return 0;
+    hipLaunchKernelGGL(erasure_kernel, dim3((uint32_t)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, seed,
+                       (uint32_t)N, (uint64_t)g0, (uint64_t)G, (uint32_t)pool, (uint32_t)std::max<size_t>(count_max, 1),
+                       random_count, d_present);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+__global__ void __launch_bounds__(kBlock) verify_kernel(uint32_t K, uint32_t R, uint64_t G, uint32_t B, uint64_t pitch,
+                                                        const uint8_t *data, const uint8_t *out, const uint8_t *out_idx,
+                                                        unsigned long long *mismatch)
+{
+    const uint64_t cols = (B + 3) / 4;
+    const uint64_t total = G * R * cols;
+    unsigned long long bad = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = i % cols, slot = i / cols;  // slot = g * R + t
+        const uint32_t idx = out_idx[slot];
+        if (idx == 0xFF) continue;
+        const uint64_t g = slot / R;
+        const uint8_t *o = out + slot * pitch + c * 4;
+        const uint8_t *d = data + (g * K + idx) * pitch + c * 4;
+        bool diff = false;
+        for (uint32_t b = 0; b < 4 && c * 4 + b < B; ++b) diff |= (o[b] != d[b]);
+        bad += diff;
+    }
+    if (bad) atomicAdd(mismatch, bad);
+}
+
+int launch_verify(int K, int N, size_t G, size_t B, size_t pitch, const void *d_data, const void *d_out,
+                  const uint8_t *d_out_idx, uint64_t *d_mismatch, hipStream_t s)
+{
+    const int R = N - K;
+    if (G == 0 || R == 0 || B == 0) return 0;
+    hipLaunchKernelGGL(verify_kernel, dim3(4096), dim3(kBlock), 0, s, (uint32_t)K, (uint32_t)R, (uint64_t)G,
+                       (uint32_t)B, (uint64_t)pitch, static_cast<const uint8_t *>(d_data),
+                       static_cast<const uint8_t *>(d_out), d_out_idx,
+                       reinterpret_cast<unsigned long long *>(d_mismatch));
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace kfec

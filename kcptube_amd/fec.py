@@ -1,0 +1,258 @@
+"""Python host mirror of kcptube's ``fecpp::fec_code`` on top of libkfec.so (include/kfec.h).
+
+``FecCode`` keeps the reference class's interface (/root/reference/src/3rd_party/fecpp.hpp:36-81):
+same names (including the ``reset_martix`` spelling), same argument meaning, same error behaviour --
+``ValueError`` where the reference throws ``std::invalid_argument`` and empty containers where it
+returns ``{}``.  Every byte is computed by the gfx950 HIP kernels; there is no CPU compute path, and a
+missing library or GPU raises ``KfecUnavailable`` instead of falling back.
+
+The batched methods take device-resident ``torch.uint8`` tensors laid out ``[G][shards][pitch]`` and run
+asynchronously on the current (or given) HIP stream -- the GPU path of the project.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libkfec.so")
+HEADER = os.path.join(os.path.dirname(PKG), "include", "kfec.h")
+
+KFEC_OK, KFEC_EMPTY, KFEC_EINVAL, KFEC_ENODEV, KFEC_EHIP, KFEC_ENOMEM, KFEC_ESINGULAR = 0, 1, -1, -2, -3, -4, -5
+GROUP_OK, GROUP_EMPTY, GROUP_SINGULAR = 0, 1, 2
+_ERRNAMES = {KFEC_EINVAL: "EINVAL", KFEC_ENODEV: "ENODEV", KFEC_EHIP: "EHIP", KFEC_ENOMEM: "ENOMEM",
+             KFEC_ESINGULAR: "ESINGULAR"}
+
+
+class KfecUnavailable(RuntimeError):
+    """libkfec.so is not built or no gfx950 GPU is usable: the coder never falls back to the CPU."""
+
+
+class KfecError(RuntimeError):
+    pass
+
+
+_lib = None
+_u8p = C.POINTER(C.c_uint8)
+_szp = C.POINTER(C.c_size_t)
+_vp = C.c_void_p
+
+
+def header_functions() -> list[str]:
+    """Names of every function include/kfec.h declares."""
+    with open(HEADER) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(kfec_[a-z_0-9]+)\s*\(", txt, re.M)))
+
+
+def load_library():
+    """ctypes handle of libkfec.so with prototypes set.  Raises KfecUnavailable if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise KfecUnavailable(f"{LIB_PATH} is not built (run __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    sz = C.c_size_t
+    proto = {
+        "kfec_create": (C.c_int, [sz, sz, C.POINTER(_vp)]),
+        "kfec_reset": (C.c_int, [_vp, sz, sz]),
+        "kfec_destroy": (None, [_vp]),
+        "kfec_get_K": (sz, [_vp]),
+        "kfec_get_N": (sz, [_vp]),
+        "kfec_enc_matrix": (C.c_int, [_vp, _u8p]),
+        "kfec_encode": (C.c_int, [_vp, _u8p, sz, sz, _u8p]),
+        "kfec_decode": (C.c_int, [_vp, _szp, C.POINTER(_u8p), sz, sz, _szp, _u8p, _szp]),
+        "kfec_encode_batch": (C.c_int, [_vp, sz, sz, sz, _vp, _vp, _vp]),
+        "kfec_decode_workspace_size": (sz, [_vp, sz]),
+        "kfec_decode_batch": (C.c_int, [_vp, sz, sz, sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "kfec_synth": (C.c_int, [_vp, C.c_uint64, sz, sz, sz, sz, sz, sz, _vp, _vp]),
+        "kfec_erasure_masks": (C.c_int, [_vp, C.c_uint64, sz, sz, sz, sz, C.c_int, _vp, _vp]),
+        "kfec_verify_recovered": (C.c_int, [_vp, sz, sz, sz, _vp, _vp, _vp, _vp, _vp]),
+        "kfec_version": (C.c_char_p, []),
+        "kfec_device": (C.c_int, [_vp]),
+    }
+    for name, (res, args) in proto.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str) -> int:
+    if rc == KFEC_ENODEV:
+        raise KfecUnavailable(f"{what}: no usable gfx950 device (the coder has no CPU fallback)")
+    if rc < 0:
+        raise KfecError(f"{what} failed: {_ERRNAMES.get(rc, rc)}")
+    return rc
+
+
+def _stream_handle(stream) -> int | None:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def _dptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+class FecCode:
+    """fecpp::fec_code on the GPU.  ``FecCode()`` is the reference's default-constructed K = N = 0 coder;
+    ``FecCode(K, N)`` / ``reset_martix(K, N)`` validate 1 <= K <= N <= 256 like fecpp.cpp:431,439."""
+
+    def __init__(self, K: int | None = None, N: int | None = None):
+        self._lib = load_library()
+        self._ctx = _vp()
+        self.K = 0
+        self.N = 0
+        if K is None and N is None:  # fec_code(): K = N = 0, usable only after reset_martix
+            return
+        self.reset_martix(int(K or 0), int(N or 0))
+
+    @classmethod
+    def create(cls, K: int, N: int) -> "FecCode":
+        """fec_code(K, N): throws (ValueError) on a K/N violation, including K = N = 0."""
+        c = cls()
+        c.reset_martix(K, N)
+        return c
+
+    def reset_martix(self, K: int, N: int) -> None:
+        if K <= 0 or N <= 0 or K > 256 or N > 256 or K > N:
+            raise ValueError("fec_code: violated 1 <= K <= N <= 256")
+        if self._ctx.value:
+            rc = self._lib.kfec_reset(self._ctx, K, N)
+        else:
+            rc = self._lib.kfec_create(K, N, C.byref(self._ctx))
+        if rc == KFEC_EINVAL:
+            raise ValueError("fec_code: violated 1 <= K <= N <= 256")
+        _check(rc, "kfec_create")
+        self.K, self.N = K, N
+
+    def __del__(self):
+        try:
+            if self._ctx and self._ctx.value:
+                self._lib.kfec_destroy(self._ctx)
+                self._ctx = _vp()
+        except Exception:
+            pass
+
+    def get_K(self) -> int:
+        return self.K
+
+    def get_N(self) -> int:
+        return self.N
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def enc_matrix(self):
+        import numpy as np
+        self._need_ctx()
+        out = np.zeros((self.N, self.K), np.uint8)
+        _check(self._lib.kfec_enc_matrix(self._ctx, out.ctypes.data_as(_u8p)), "kfec_enc_matrix")
+        return out
+
+    def _need_ctx(self):
+        if not self._ctx.value:
+            raise KfecError("fec_code has K = N = 0 (default-constructed); call reset_martix first")
+
+    # ---- fec_code::encode / fec_code::decode ------------------------------------------------------
+    def encode(self, input: bytes | None, data_length: int | None = None, block_size: int = 0) -> list[bytes]:
+        """Parity blocks of the first K blocks of ``input`` (fecpp.cpp:495-513); [] where it returns {}."""
+        self._need_ctx()
+        if input is None:
+            return []
+        buf = bytes(input)
+        dl = len(buf) if data_length is None else int(data_length)
+        R = self.N - self.K
+        if block_size <= 0 or (dl // block_size) % self.K != 0 or dl < self.K * block_size:
+            return []
+        src = (C.c_uint8 * max(len(buf), 1)).from_buffer_copy(buf if buf else b"\0")
+        out = (C.c_uint8 * max(R * block_size, 1))()
+        rc = _check(self._lib.kfec_encode(self._ctx, src, dl, block_size, out), "kfec_encode")
+        if rc == KFEC_EMPTY:
+            return []
+        raw = bytes(out)
+        return [raw[r * block_size:(r + 1) * block_size] for r in range(R)]
+
+    def decode(self, shares: dict, share_size: int) -> dict:
+        """Missing data shards {index: bytes} from >= K shares (fecpp.cpp:518-587); {} where it returns {}."""
+        self._need_ctx()
+        ids = sorted(int(i) for i in shares)
+        n = len(ids)
+        if n < self.K:
+            return {}
+        bufs = [(C.c_uint8 * max(share_size, 1)).from_buffer_copy(bytes(shares[i])[:share_size].ljust(max(share_size, 1), b"\0"))
+                for i in ids]
+        ida = (C.c_size_t * max(n, 1))(*ids)
+        pa = (_u8p * max(n, 1))(*[C.cast(b, _u8p) for b in bufs])
+        out = (C.c_uint8 * max(self.K * share_size, 1))()
+        oids = (C.c_size_t * max(self.K, 1))()
+        nout = C.c_size_t(0)
+        rc = self._lib.kfec_decode(self._ctx, ida, pa, n, share_size, oids, out, C.byref(nout))
+        if rc == KFEC_ESINGULAR:
+            raise ValueError("singlar matrix")
+        rc = _check(rc, "kfec_decode")
+        if rc == KFEC_EMPTY:
+            return {}
+        raw = bytes(out)
+        return {int(oids[t]): raw[t * share_size:(t + 1) * share_size] for t in range(nout.value)}
+
+    # ---- batched device-resident path ---------------------------------------------------------------
+    def encode_batch(self, data, parity, B: int | None = None, stream=None) -> None:
+        """data: uint8 cuda tensor [G][K][pitch]; parity: [G][N-K][pitch] (written)."""
+        self._need_ctx()
+        G, k, pitch = data.shape
+        assert k == self.K and data.is_contiguous() and parity.is_contiguous()
+        B = pitch if B is None else B
+        _check(self._lib.kfec_encode_batch(self._ctx, G, B, pitch, _dptr(data), _dptr(parity),
+                                           _stream_handle(stream)), "kfec_encode_batch")
+
+    def decode_workspace(self, G: int, device=None):
+        import torch
+        n = self._lib.kfec_decode_workspace_size(self._ctx, G)
+        return torch.empty(max(n, 16), dtype=torch.uint8, device=device or "cuda")
+
+    def decode_batch(self, data, parity, present, out, out_idx, status, workspace, B: int | None = None,
+                     stream=None) -> None:
+        """present: int64 [G][4] bitmasks; out: [G][R][pitch]; out_idx: uint8 [G][R]; status: uint8 [G]."""
+        self._need_ctx()
+        G, k, pitch = data.shape
+        assert k == self.K and present.shape == (G, 4)
+        B = pitch if B is None else B
+        _check(self._lib.kfec_decode_batch(self._ctx, G, B, pitch, _dptr(data), _dptr(parity), _dptr(present),
+                                           _dptr(out), _dptr(out_idx), _dptr(status), _dptr(workspace),
+                                           _stream_handle(stream)), "kfec_decode_batch")
+
+    def synth(self, out, seed: int, g0: int = 0, s0: int = 0, B: int | None = None, stream=None) -> None:
+        """Fill out[G][ns][pitch] with SURVEY 8(d) counter bytes for groups g0.., slots s0.."""
+        self._need_ctx()
+        G, ns, pitch = out.shape
+        B = pitch if B is None else B
+        _check(self._lib.kfec_synth(self._ctx, seed, g0, G, s0, ns, B, pitch, _dptr(out), _stream_handle(stream)),
+               "kfec_synth")
+
+    def erasure_masks(self, present, seed: int, pool: int, count_max: int, random_count: bool = False,
+                      g0: int = 0, stream=None) -> None:
+        self._need_ctx()
+        G = present.shape[0]
+        _check(self._lib.kfec_erasure_masks(self._ctx, seed, g0, G, pool, count_max, int(random_count),
+                                            _dptr(present), _stream_handle(stream)), "kfec_erasure_masks")
+
+    def verify_recovered(self, data, out, out_idx, mismatch, B: int | None = None, stream=None) -> None:
+        self._need_ctx()
+        G, _, pitch = data.shape
+        B = pitch if B is None else B
+        _check(self._lib.kfec_verify_recovered(self._ctx, G, B, pitch, _dptr(data), _dptr(out), _dptr(out_idx),
+                                               _dptr(mismatch), _stream_handle(stream)), "kfec_verify_recovered")
+
+
+def version() -> str:
+    return load_library().kfec_version().decode()
