@@ -48,6 +48,17 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def build_variant(name: str, defines: dict[str, int]) -> str:
+    """Timing/ablation variant of the library (tools/ab.py): kcptube_amd/variants/libkfec_<name>.so."""
+    out_dir = os.path.join(PKG, "variants")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, f"libkfec_{name}.so")
+    cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+           "-o", out] + [f"-D{k}={v}" for k, v in defines.items()] + [os.path.join(CSRC, s) for s in SOURCES]
+    subprocess.check_call(cmd, cwd=CSRC)
+    return out
+
+
 def build_compat_test(force: bool = False) -> str:
     """C++ program exercising include/fecpp_compat.hpp against libkfec.so (run by the GPU tests)."""
     src = os.path.join(ROOT, "tests", "cpp", "compat_test.cpp")

@@ -24,12 +24,28 @@
 #include "kfec_internal.hpp"
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 
 namespace kfec {
 
 __constant__ GfTables c_gf = make_gf_tables();
 
 static constexpr int kBlock = 256;
+
+// build-time tuning knobs (tools/ab.py builds variants; the shipped library uses the defaults)
+#ifndef KFEC_PD
+#define KFEC_PD 4
+#endif
+#ifndef KFEC_ABLATE
+#define KFEC_ABLATE 0
+#endif
+#ifndef KFEC_MINW
+#define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the flattened kernel
+#endif
+#ifndef KFEC_NTSTORE
+#define KFEC_NTSTORE 1  // nontemporal output stores in the flattened kernel (+2.5% encode, measured)
+#endif
 
 // ---------------------------------------------------------------------------------------------------
 // small device helpers
@@ -456,7 +472,12 @@ template <int VEC>
 __device__ __forceinline__ void store_gran(uint8_t *p, const uint32_t *d, uint32_t col, uint32_t B)
 {
     if constexpr (VEC == 16) {
+#if KFEC_NTSTORE
+        typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u32x4_t{d[0], d[1], d[2], d[3]}, reinterpret_cast<u32x4_t *>(p));
+#else
         *reinterpret_cast<uint4 *>(p) = make_uint4(d[0], d[1], d[2], d[3]);
+#endif
     } else if constexpr (VEC == 8) {
         *reinterpret_cast<uint2 *>(p) = make_uint2(d[0], d[1]);
     } else if constexpr (VEC == 4) {
@@ -469,11 +490,22 @@ __device__ __forceinline__ void store_gran(uint8_t *p, const uint32_t *d, uint32
     }
 }
 
-// z ^= c * x for 4 bytes, c given by its 5 permute tables (kfec_gf.hpp gf_perm_tables)
-__device__ __forceinline__ uint32_t perm_mul(const uint32_t *t, uint32_t s0, uint32_t s1, uint32_t s2)
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor_b32 otherwise
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
-    return __builtin_amdgcn_perm(t[1], t[0], s0) ^ __builtin_amdgcn_perm(t[3], t[2], s1) ^
-           __builtin_amdgcn_perm(t[4], t[4], s2);
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// acc ^ c * x for 4 bytes, c given by its 5 permute tables (kfec_gf.hpp gf_perm_tables):
+// three v_perm_b32 lookups (bits 0-2, 3-5, 6-7 of every byte) and two XORs
+__device__ __forceinline__ uint32_t perm_mac(uint32_t acc, const uint32_t *t, uint32_t s0, uint32_t s1, uint32_t s2)
+{
+    const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], s0);
+    const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], s1);
+    const uint32_t p2 = __builtin_amdgcn_perm(t[4], t[4], s2);
+    return xor3(acc, p0, p1) ^ p2;
 }
 
 template <int MT>
@@ -518,11 +550,11 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
 }
 
 template <int VEC, int MT, bool DEC>
-__global__ void __launch_bounds__(kBlock) mac_kernel(MacArgs a)
+__global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
 {
     using L = MacLayout<MT>;
     constexpr int W = Gran<VEC>::W;
-    constexpr int PD = 4;  // shards in flight per lane
+    constexpr int PD = KFEC_PD;  // shards in flight per lane
     constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
 
@@ -601,8 +633,14 @@ __global__ void __launch_bounds__(kBlock) mac_kernel(MacArgs a)
                             const uint32_t s0 = xv & 0x07070707u;
                             const uint32_t s1 = (xv >> 3) & 0x07070707u;
                             const uint32_t s2 = (xv >> 6) & 0x03030303u;
+#if KFEC_ABLATE == 1  // timing-only build: memory traffic of the real kernel, XOR instead of the GF MAC
 #pragma unroll
-                            for (int r = 0; r < MT; ++r) acc[r][w] ^= perm_mul(t + 5 * r, s0, s1, s2);
+                            for (int r = 0; r < MT; ++r) acc[r][w] ^= xv ^ t[5 * r];
+                            (void)s0; (void)s1; (void)s2;
+#else
+#pragma unroll
+                            for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+#endif
                         }
                     }
                 }
@@ -614,6 +652,270 @@ __global__ void __launch_bounds__(kBlock) mac_kernel(MacArgs a)
             for (int r = 0; r < MT; ++r)
                 if ((uint32_t)r < rows) store_gran<VEC>(a.out + obase + (uint64_t)r * a.pitch, acc[r], col, a.B);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// (A4/A5/A8/A11) group-tile perm-MAC kernel: the primary path for shards up to 8 KiB.
+// One workgroup owns one shard group at a time.  It stages the group's K selected shards (or a chunk of
+// JS of them) into LDS with linear, coalesced 16-B loads -- a whole group of 20 x 1440 B is 225 complete
+// 128-B lines, so no line is fetched twice, unlike per-lane strided column reads whose 1-KiB wave
+// chunks straddle shard boundaries -- then every lane computes one 8-byte column of the MT output rows
+// from LDS.  The coefficient tables of the chunk are expanded into LDS once per group (decode) or once
+// per kernel (encode) and read back with broadcast ds_read_b128.
+// ---------------------------------------------------------------------------------------------------
+struct LdsArgs {
+    const uint8_t *data;    // [G][K][pitch]
+    const uint8_t *parity;  // [G][R][pitch]
+    uint8_t *out;           // encode: parity, decode: recovered [G][R][pitch]
+    const uint8_t *enc;     // N x K (encode)
+    const uint8_t *rec;     // per-group records (decode)
+    uint64_t pitch;
+    uint32_t G, K, R, B;
+    uint32_t rec_stride;
+    uint32_t JS;            // shards staged per chunk
+    uint32_t Bs;            // LDS row stride of a staged shard (multiple of 16, >= B)
+    uint32_t cols;          // 8-byte columns = ceil(B / 8)
+    uint64_t bs_inv;        // ceil(2^32 / Bs): o / Bs for staged offsets o < 2^16 without a divide
+    uint32_t tbl_all;       // encode: tables of all K shards stay in LDS for the whole kernel
+};
+
+template <int MT>
+struct TileLayout {
+    static constexpr int T4 = (MT + 3) / 4 * 4;
+    static constexpr int TBL = MT * 16 + T4 * 4;  // per shard: [MT][t0..t3] then t4[MT] (padded to 16 B)
+};
+
+// expand coefficient tables of shards [c0, c0+nj) for rows [row0, row0+MT) of group g into LDS
+template <int MT, bool DEC>
+__device__ __forceinline__ void tile_expand(const LdsArgs &a, uint8_t *s_tbl, uint32_t g, uint32_t c0, uint32_t nj,
+                                            uint32_t row0, uint32_t m)
+{
+    using L = TileLayout<MT>;
+    for (uint32_t e = threadIdx.x; e < nj * MT; e += blockDim.x) {
+        const uint32_t r = e % MT, jj = e / MT, j = c0 + jj, u = row0 + r;
+        uint32_t c = 0;
+        if constexpr (DEC) {
+            if (u < m) c = a.rec[(uint64_t)g * a.rec_stride + 4 + a.K + u * a.K + j];
+        } else {
+            if (u < a.R) c = a.enc[(uint64_t)(a.K + u) * a.K + j];
+        }
+        uint32_t t[5];
+        gf_perm_tables(c, t);
+        uint8_t *base = s_tbl + jj * L::TBL;
+        *reinterpret_cast<uint4 *>(base + r * 16) = make_uint4(t[0], t[1], t[2], t[3]);
+        reinterpret_cast<uint32_t *>(base + MT * 16)[r] = t[4];
+    }
+}
+
+template <int SV>
+__device__ __forceinline__ void stage_copy(uint8_t *dst, const uint8_t *src)
+{
+    if constexpr (SV == 16) *reinterpret_cast<uint4 *>(dst) = *reinterpret_cast<const uint4 *>(src);
+    else if constexpr (SV == 8) *reinterpret_cast<uint2 *>(dst) = *reinterpret_cast<const uint2 *>(src);
+    else if constexpr (SV == 4) *reinterpret_cast<uint32_t *>(dst) = *reinterpret_cast<const uint32_t *>(src);
+    else *dst = *src;
+}
+
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+// One work unit = (group g, chunk of shards [c0, c0+nj)).  Stage a unit into an LDS buffer of JS rows of
+// Bs bytes.  SV == 16: LDS-DMA (global_load_lds_dwordx4): each wave-instruction fills 1 KiB of LDS
+// contiguously while every lane names its own 16-B source -- a gather of shard rows; asynchronous, no
+// VGPRs, completion awaited by the next s_waitcnt vmcnt(0) + barrier.  Other SV (pitch not 16-aligned):
+// synchronous register staging.
+template <int SV, bool DEC>
+__device__ __forceinline__ void tile_stage(const LdsArgs &a, uint8_t *buf, uint32_t g, uint32_t c0, uint32_t nj)
+{
+    const uint32_t K = a.K;
+    auto shard_src = [&](uint32_t jj) -> const uint8_t * {
+        if constexpr (DEC) {
+            const uint32_t sid = a.rec[(uint64_t)g * a.rec_stride + 4 + c0 + jj];
+            return (sid < K) ? a.data + ((uint64_t)g * K + sid) * a.pitch
+                             : a.parity + ((uint64_t)g * a.R + (sid - K)) * a.pitch;
+        } else {
+            return a.data + ((uint64_t)g * K + c0 + jj) * a.pitch;
+        }
+    };
+    if constexpr (SV == 16) {
+        const uint32_t bytes = nj * a.Bs;
+        const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+        for (uint32_t ch = wave; ch * 1024 < bytes; ch += nw) {
+            const uint32_t o = ch * 1024 + lane * 16;
+            const uint32_t jj = (uint32_t)(((uint64_t)o * a.bs_inv) >> 32), off = o - jj * a.Bs;  // o / Bs
+            if (o < bytes) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the builtin exists only in the device pass of this single-source file
+                __builtin_amdgcn_global_load_lds(shard_src(jj) + off,
+                                                 (__attribute__((address_space(3))) void *)(buf + ch * 1024), 16, 0, 0);
+#endif
+            }
+        }
+    } else {
+        const uint32_t gps = a.Bs / SV;  // granules per staged row (rows padded to 16 B)
+        const uint32_t total = nj * gps;
+        constexpr int NB = 8;
+        for (uint32_t base = threadIdx.x; base < total; base += NB * blockDim.x) {
+            uint8_t v[NB][SV];
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                const uint32_t gi = base + k * blockDim.x;
+                if (gi < total) {
+                    const uint32_t jj = gi / gps, off = (gi - jj * gps) * SV;
+                    if (off < a.B) {
+                        const uint8_t *src = shard_src(jj) + off;
+                        if constexpr (SV == 8) *reinterpret_cast<uint2 *>(v[k]) = *reinterpret_cast<const uint2 *>(src);
+                        else if constexpr (SV == 4) *reinterpret_cast<uint32_t *>(v[k]) = *reinterpret_cast<const uint32_t *>(src);
+                        else v[k][0] = *src;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                const uint32_t gi = base + k * blockDim.x;
+                if (gi < total) {
+                    const uint32_t jj = gi / gps, off = (gi - jj * gps) * SV;
+                    uint8_t *dst = buf + jj * a.Bs + off;
+                    if constexpr (SV == 8) *reinterpret_cast<uint2 *>(dst) = *reinterpret_cast<uint2 *>(v[k]);
+                    else if constexpr (SV == 4) *reinterpret_cast<uint32_t *>(dst) = *reinterpret_cast<uint32_t *>(v[k]);
+                    else *dst = v[k][0];
+                }
+            }
+        }
+    }
+}
+
+// acc[r] ^= coef(r, jj) * x over one 8-byte column, tables at tb (TileLayout)
+template <int MT>
+__device__ __forceinline__ void tile_mac(u32x2_t (&acc)[MT], u32x2_t x, const uint8_t *tb)
+{
+    using L = TileLayout<MT>;
+    uint32_t t4[L::T4];
+#pragma unroll
+    for (int q = 0; q < L::T4 / 4; ++q) {
+        const uint4 v = reinterpret_cast<const uint4 *>(tb + MT * 16)[q];
+        t4[4 * q] = v.x; t4[4 * q + 1] = v.y; t4[4 * q + 2] = v.z; t4[4 * q + 3] = v.w;
+    }
+    uint32_t s0[2], s1[2], s2[2];
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+        s0[w] = x[w] & 0x07070707u;
+        s1[w] = (x[w] >> 3) & 0x07070707u;
+        s2[w] = (x[w] >> 6) & 0x03030303u;
+    }
+#pragma unroll
+    for (int r = 0; r < MT; ++r) {
+        const uint4 v = reinterpret_cast<const uint4 *>(tb)[r];
+        const uint32_t t[5] = {v.x, v.y, v.z, v.w, t4[r]};
+#if KFEC_ABLATE == 1
+        acc[r][0] ^= x[0] ^ t[0];
+        acc[r][1] ^= x[1] ^ t[4];
+#else
+#pragma unroll
+        for (int w = 0; w < 2; ++w) acc[r][w] = perm_mac(acc[r][w], t, s0[w], s1[w], s2[w]);
+#endif
+    }
+}
+
+// Persistent workgroup walking its (group, chunk) units through a 2-deep LDS ring: the DMA of unit u+1
+// is in flight while unit u is computed.  Tables (and, for encode with few shards, the whole table set)
+// live beside the ring.
+template <int MT, bool DEC, int SV>
+__global__ void __launch_bounds__(256) mac_tile_kernel(LdsArgs a)
+{
+    using L = TileLayout<MT>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t K = a.K, JS = a.JS, row0 = blockIdx.y * MT;
+    const uint32_t nch = (K + JS - 1) / JS;  // chunks per group
+    // LDS carve-up as integer offsets from smem: selecting between two pointers at run time makes hipcc
+    // lose the LDS address space and emit flat loads for the whole compute loop
+    const uint32_t ring_sz = JS * a.Bs, tbl0 = 2 * ring_sz, tring_sz = JS * L::TBL;
+    uint8_t *tbl_base = smem + tbl0;
+    // encode tables for all K shards fit once (enc_all) or are expanded per unit into a 2-deep ring
+    const bool enc_all = !DEC && a.tbl_all;
+
+    // rows of this workgroup's tile for group g; 0 = nothing to do for g
+    auto rows_of = [&](uint32_t g) -> uint32_t {
+        if constexpr (DEC) {
+            const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
+            const uint32_t st = rec[0], m = rec[1];
+            return (st == 0 && m > row0) ? min((uint32_t)MT, m - row0) : 0u;
+        } else {
+            return a.R > row0 ? min((uint32_t)MT, a.R - row0) : 0u;
+        }
+    };
+    auto m_of = [&](uint32_t g) -> uint32_t {
+        if constexpr (DEC) return a.rec[(uint64_t)g * a.rec_stride + 1];
+        else return 0u;
+    };
+    // first group at or after g with work for this tile
+    auto next_group = [&](uint32_t g) -> uint32_t {
+        while (g < a.G && rows_of(g) == 0) g += gridDim.x;
+        return g;
+    };
+
+    if (enc_all) tile_expand<MT, false>(a, tbl_base, 0, 0, K, row0, 0);
+
+    uint32_t g = next_group(blockIdx.x), c = 0;
+    if (g >= a.G) return;
+    // prologue: unit (g, 0) into slot 0
+    if (!enc_all) tile_expand<MT, DEC>(a, smem + tbl0, g, 0, min(JS, K), row0, m_of(g));
+    tile_stage<SV, DEC>(a, smem, g, 0, min(JS, K));
+    uint32_t slot = 0, rows = rows_of(g);
+    u32x2_t acc[MT];
+#pragma unroll
+    for (int r = 0; r < MT; ++r) acc[r] = u32x2_t{0u, 0u};
+    const uint32_t col = threadIdx.x;
+    while (true) {
+        // the unit after (g, c)
+        uint32_t gn = g, cn = c + 1;
+        if (cn == nch) {
+            cn = 0;
+            gn = next_group(g + gridDim.x);
+        }
+        if constexpr (SV == 16) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // unit (g, c) has landed in ring[slot]; everyone is done with ring[slot ^ 1]
+        if (gn < a.G) {
+            const uint32_t njn = min(JS, K - cn * JS);
+            if (!enc_all) tile_expand<MT, DEC>(a, smem + tbl0 + (slot ^ 1) * tring_sz, gn, cn * JS, njn, row0, m_of(gn));
+            tile_stage<SV, DEC>(a, smem + (slot ^ 1) * ring_sz, gn, cn * JS, njn);
+        }
+        const uint32_t nj = min(JS, K - c * JS);
+        const uint32_t tb_off = enc_all ? tbl0 + c * JS * L::TBL : tbl0 + slot * tring_sz;
+        if (col < a.cols) {
+            const uint8_t *tb = smem + tb_off;
+            const uint8_t *xs = smem + slot * ring_sz + col * 8;
+            for (uint32_t jj = 0; jj < nj; ++jj)
+                tile_mac<MT>(acc, *reinterpret_cast<const u32x2_t *>(xs + jj * a.Bs), tb + jj * L::TBL);
+        }
+        if (c + 1 == nch) {  // group finished: store its rows
+            if (col < a.cols) {
+                const uint64_t obase = ((uint64_t)g * a.R + row0) * a.pitch + (uint64_t)col * 8;
+#pragma unroll
+                for (int r = 0; r < MT; ++r) {
+                    if ((uint32_t)r < rows) {
+                        uint8_t *o = a.out + obase + (uint64_t)r * a.pitch;
+                        if constexpr (SV >= 8) {
+                            *reinterpret_cast<u32x2_t *>(o) = acc[r];
+                        } else if constexpr (SV == 4) {
+                            // pitch is only 4-aligned: the second dword may lie past the slot's pitch
+                            *reinterpret_cast<uint32_t *>(o) = acc[r][0];
+                            if (col * 8 + 4 < a.B) *reinterpret_cast<uint32_t *>(o + 4) = acc[r][1];
+                        } else {
+#pragma unroll
+                            for (int b = 0; b < 8; ++b)
+                                if (col * 8 + b < a.B) o[b] = (uint8_t)(acc[r][b >> 2] >> (8 * (b & 3)));
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < MT; ++r) acc[r] = u32x2_t{0u, 0u};
+            if (gn >= a.G) break;
+            rows = rows_of(gn);
+        }
+        g = gn;
+        c = cn;
+        slot ^= 1;
     }
 }
 
@@ -630,6 +932,15 @@ static int pick_vec(size_t pitch, std::initializer_list<const void *> ptrs)
     return 1;
 }
 
+// resident 256-thread blocks per CU for a kernel (occupancy API, capped at 8: MI355X_MICROARCH.md
+// "Residency": the API can over-report by one for SGPR-heavy kernels; ours stay below 80 SGPRs)
+static int resident_blocks(const void *kernel, size_t lds)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, kBlock, lds) != hipSuccess || n <= 0) n = 1;
+    return std::min(n, 8);
+}
+
 static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
 
 template <int VEC, int MT, bool DEC>
@@ -637,8 +948,11 @@ static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
 {
     using L = MacLayout<MT>;
     const size_t lds = (size_t)a.gmax * a.JC * L::ENTRY;
-    uint32_t want = (a.total + kBlock - 1) / kBlock;
-    uint32_t cap = (uint32_t)std::max(1, di.cus) * 8u / (uint32_t)std::max(1, tiles);
+    // persistent grid sized to what is resident at once: a grid one block per CU larger than that
+    // leaves a tail in which a single block per CU runs alone (measured: +45% kernel time)
+    const uint32_t want = (a.total + kBlock - 1) / kBlock;
+    const uint32_t cap = (uint32_t)(std::max(1, di.cus) * resident_blocks((const void *)mac_kernel<VEC, MT, DEC>, lds))
+                         / (uint32_t)std::max(1, tiles);
     const uint32_t gx = std::max(1u, std::min(want, std::max(cap, 1u)));
     hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC>), dim3(gx, tiles), dim3(kBlock), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
@@ -676,6 +990,69 @@ static int entry_bytes(int mt)
 }
 
 static constexpr size_t kLdsBudget = 32 * 1024;
+static constexpr size_t kTileLdsBudget = 31 * 1024;  // 5 workgroups per CU (160 KiB of LDS)
+
+// group-tile kernel for shards up to 2 KiB (one 8-byte column per lane of a 256-lane workgroup) and
+// < 2^32 groups; larger shards take the flattened kernel
+// Measured slower than the flattened kernel on MI355X once the GF math is in (DESIGN.md "kernel
+// architecture"), so it is opt-in: KFEC_KERNEL=tile.
+static bool use_tile_path(size_t G, size_t B)
+{
+    static const bool on = [] {
+        const char *e = getenv("KFEC_KERNEL");
+        return e && std::string(e) == "tile";
+    }();
+    return on && B <= 2048 && G < 0xFFFFFFFFull;
+}
+
+template <int MT, bool DEC, int SV>
+static int run_tile(const DeviceInfo &di, LdsArgs a, int tiles, hipStream_t s)
+{
+    using L = TileLayout<MT>;
+    a.Bs = (a.B + 15) & ~15u;
+    a.cols = (a.B + 7) / 8;
+    a.bs_inv = ((1ull << 32) + a.Bs - 1) / a.Bs;
+    // 2-deep ring of JS-shard chunks (+ their tables) within the per-workgroup LDS budget; encode keeps
+    // all K shards' tables resident when they are small
+    const size_t all_tbl = (size_t)a.K * L::TBL;
+    a.tbl_all = (!DEC && all_tbl <= 4096) ? 1u : 0u;
+    const size_t per_row = 2 * (size_t)a.Bs + (a.tbl_all ? 0 : 2 * (size_t)L::TBL);
+    const size_t budget = kTileLdsBudget - (a.tbl_all ? all_tbl : 0);
+    const size_t nch = std::max<size_t>(1, (a.K * per_row + budget - 1) / budget);
+    a.JS = (uint32_t)((a.K + nch - 1) / nch);
+    const size_t lds = (size_t)a.JS * per_row + (a.tbl_all ? all_tbl : 0);
+    const uint32_t threads = 256;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)mac_tile_kernel<MT, DEC, SV>, threads, lds) !=
+            hipSuccess || occ <= 0)
+        occ = 1;
+    const uint32_t cap = (uint32_t)std::max(1, di.cus * std::min(occ, 8) / std::max(1, tiles));
+    const uint32_t gx = std::max(1u, std::min<uint32_t>(a.G, cap));
+    hipLaunchKernelGGL((mac_tile_kernel<MT, DEC, SV>), dim3(gx, tiles), dim3(threads), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <bool DEC>
+static int dispatch_tile(const DeviceInfo &di, int sv, LdsArgs a, hipStream_t g_stream)
+{
+    const int mt = a.R <= 4 ? std::max<int>(a.R, 1) : 8;
+    const int tiles = ((int)a.R + mt - 1) / mt;
+#define KFEC_TILE_MT(SV)                                                           \
+    switch (mt) {                                                                  \
+    case 1: return run_tile<1, DEC, SV>(di, a, tiles, g_stream);                   \
+    case 2: return run_tile<2, DEC, SV>(di, a, tiles, g_stream);                   \
+    case 3: return run_tile<3, DEC, SV>(di, a, tiles, g_stream);                   \
+    case 4: return run_tile<4, DEC, SV>(di, a, tiles, g_stream);                   \
+    default: return run_tile<8, DEC, SV>(di, a, tiles, g_stream);                  \
+    }
+    switch (sv) {
+    case 16: KFEC_TILE_MT(16)
+    case 8: KFEC_TILE_MT(8)
+    case 4: KFEC_TILE_MT(4)
+    default: KFEC_TILE_MT(1)
+    }
+#undef KFEC_TILE_MT
+}
 static constexpr size_t kMaxItemsPerLaunch = 0x7FFFFFFFu;
 
 // split G into launches whose item count fits 32-bit indexing
@@ -695,6 +1072,15 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
 {
     const int R = N - K;
     if (R == 0 || G == 0 || B == 0) return 0;
+    if (use_tile_path(G, B)) {
+        LdsArgs a{};
+        a.data = static_cast<const uint8_t *>(d_data);
+        a.out = static_cast<uint8_t *>(d_parity);
+        a.enc = d_enc;
+        a.pitch = pitch;
+        a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
+        return dispatch_tile<false>(di, pick_vec(pitch, {d_data, d_parity}), a, s);
+    }
     const int vec = pick_vec(pitch, {d_data, d_parity});
     const int vb = vec >= 4 ? vec : 4;
     const size_t cols = (B + vb - 1) / vb;
@@ -741,8 +1127,10 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     const int mmax = std::min(K, R);
     if (mmax <= 8) {
         const size_t lds = 768 + (size_t)R * K;
+        // one thread per group: the per-group work is a chain of dependent LDS lookups, so latency is hidden
+        // by having many groups in flight, not by looping
         const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((G + kBlock - 1) / kBlock,
-                                                                                (size_t)std::max(di.cus, 1) * 4));
+                                                                                (size_t)std::max(di.cus, 1) * 64));
         if (mmax <= 4) hipLaunchKernelGGL((decode_prep_small<4>), dim3(blocks), dim3(kBlock), lds, s, p);
         else hipLaunchKernelGGL((decode_prep_small<8>), dim3(blocks), dim3(kBlock), lds, s, p);
     } else {
@@ -752,6 +1140,18 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     }
     if (hipGetLastError() != hipSuccess) return -3;
     if (R == 0 || B == 0) return 0;
+    if (use_tile_path(G, B)) {
+        LdsArgs a{};
+        a.data = static_cast<const uint8_t *>(d_data);
+        a.parity = static_cast<const uint8_t *>(d_parity);
+        a.out = static_cast<uint8_t *>(d_out);
+        a.enc = d_enc;
+        a.rec = rec;
+        a.pitch = pitch;
+        a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
+        a.rec_stride = (uint32_t)rs;
+        return dispatch_tile<true>(di, pick_vec(pitch, {d_data, d_parity, d_out}), a, s);
+    }
 
     const int vec = pick_vec(pitch, {d_data, d_parity, d_out});
     const int vb = vec >= 4 ? vec : 4;

@@ -16,7 +16,7 @@ import os
 import re
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libkfec.so")
+LIB_PATH = os.environ.get("KFEC_LIB") or os.path.join(PKG, "libkfec.so")
 HEADER = os.path.join(os.path.dirname(PKG), "include", "kfec.h")
 
 KFEC_OK, KFEC_EMPTY, KFEC_EINVAL, KFEC_ENODEV, KFEC_EHIP, KFEC_ENOMEM, KFEC_ESINGULAR = 0, 1, -1, -2, -3, -4, -5

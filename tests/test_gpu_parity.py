@@ -201,6 +201,11 @@ CASES = [
     (5, 5, 32, 32, 10, 0, "R=0"),
     (128, 256, 48, 48, 3, 100, "R=128, m up to 100"),
     (255, 256, 40, 40, 6, 1, "K=255"),
+    (5, 8, 9000, 9000, 7, 3, "B > 8 KiB -> flattened kernel, V=8"),
+    (3, 5, 8193, 8208, 5, None, "B > 8 KiB, pitch > B -> flattened kernel, V=16"),
+    (4, 7, 2047, 2047, 5, 3, "largest tile-kernel B, bytewise staging"),
+    (6, 9, 2048, 2048, 5, 3, "largest tile-kernel B, LDS-DMA staging"),
+    (6, 9, 2049, 2064, 5, 3, "smallest flattened-kernel B"),
 ]
 
 

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Time encode / decode of one library build (KFEC_LIB env) on fec=K:R groups; prints one JSON line."""
+import json, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from kcptube_amd import FecCode
+
+K, N, B, G = (int(x) for x in (sys.argv[1:5] if len(sys.argv) > 4 else (20, 23, 1440, 1 << 20)))
+iters = int(os.environ.get("AB_ITERS", "10"))
+R = N - K
+dev = torch.device("cuda:0")
+c = FecCode(K, N)
+data = torch.empty((G, K, B), dtype=torch.uint8, device=dev)
+par = torch.empty((G, R, B), dtype=torch.uint8, device=dev)
+masks = torch.empty((G, 4), dtype=torch.int64, device=dev)
+out = torch.empty((G, R, B), dtype=torch.uint8, device=dev)
+idx = torch.empty((G, R), dtype=torch.uint8, device=dev)
+st = torch.empty((G,), dtype=torch.uint8, device=dev)
+ws = c.decode_workspace(G)
+c.synth(data, 1)
+c.erasure_masks(masks, 1, K, min(R, K))
+s = torch.cuda.current_stream()
+e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+enc, dec = [], []
+for i in range(iters + 2):
+    e[0].record(s); c.encode_batch(data, par); e[1].record(s)
+    c.decode_batch(data, par, masks, out, idx, st, ws); e[2].record(s)
+    torch.cuda.synchronize()
+    if i >= 2:
+        enc.append(e[0].elapsed_time(e[1])); dec.append(e[1].elapsed_time(e[2]))
+enc.sort(); dec.sort()
+eb = G * (K + R) * B
+db = G * (K + min(R, K)) * B
+print(json.dumps({"lib": os.path.basename(os.environ.get("KFEC_LIB", "libkfec.so")), "enc_ms": enc[len(enc)//2],
+                  "dec_ms": dec[len(dec)//2], "enc_GBps": round(eb / enc[len(enc)//2] / 1e6, 1),
+                  "dec_GBps": round(db / dec[len(dec)//2] / 1e6, 1)}), flush=True)
