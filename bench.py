@@ -52,7 +52,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(K, N, B, pool, erase, rnd, target_cpu_s):
+def cpu_baseline(K, N, B, pool, erase, rnd, target_cpu_s, decode_only=False):
     """Reference coder on the host cores, bounded sample.  Test infrastructure (oracle/), used here
     only for the reported CPU baseline -- never for the GPU number."""
     import oracle as orc
@@ -61,7 +61,8 @@ def cpu_baseline(K, N, B, pool, erase, rnd, target_cpu_s):
     if orc.RefCoder.available():
         ref = orc.RefCoder()
         kind = "reference"
-        run = lambda passes: ref.bench_roundtrip(K, N, B, G, pool, erase, rnd, threads, passes, 0x5EED0001)[:2]
+        run = lambda passes: ref.bench_roundtrip(K, N, B, G, pool, erase, rnd, threads, passes, 0x5EED0001,
+                                                 decode_only)[:2]
     else:
         o = orc.Oracle()
         kind = "port"
@@ -79,7 +80,7 @@ def cpu_baseline(K, N, B, pool, erase, rnd, target_cpu_s):
                     break
     except OSError:
         pass
-    what = "encode + decode" if K else ""
+    what = "decode-only" if decode_only else "encode + decode"
     return {"value": round(bps / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
             "sample": f"{G} distinct groups x {passes} passes of fec={K}:{N-K} B={B} {what} "
                       f"({'random 1-%d of all %d' % (erase, N) if rnd else '%d data' % erase} shards erased), "
@@ -96,8 +97,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU; local % count only matters for a multi-rank rehearsal on a smaller box
+    local_dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
 
     from kcptube_amd import FecCode
 
@@ -218,7 +221,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            result["cpu_baseline"] = cpu_baseline(K, N, B, pool, erase, rnd, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(K, N, B, pool, erase, rnd, args.cpu_seconds,
+                                                  decode_only=not do_enc)
         except Exception as e:  # the GPU number stands on its own
             result["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

@@ -192,7 +192,7 @@ class RefCoder:
             lib.ref_decode.restype = C.c_long
             lib.ref_bench_roundtrip.argtypes = [C.c_size_t] * 6 + [C.c_int, C.c_size_t, C.c_size_t,
                                                                   C.c_uint64, C.POINTER(C.c_double),
-                                                                  _szp]
+                                                                  _szp, C.c_int]
             lib.ref_bench_roundtrip.restype = C.c_double
             RefCoder._lib = lib
         self.lib = RefCoder._lib
@@ -224,9 +224,11 @@ class RefCoder:
             raise ValueError("singular matrix")
         return {int(oids[t]): out[t * share_size:(t + 1) * share_size].tobytes() for t in range(m)}
 
-    def bench_roundtrip(self, K, N, B, G, pool, erase_max, random_count, threads, passes, seed):
+    def bench_roundtrip(self, K, N, B, G, pool, erase_max, random_count, threads, passes, seed,
+                        decode_only=False):
+        """payload bytes/s of (encode +) decode over G groups, the reference coder on `threads` cores"""
         secs = C.c_double(0)
         rec = C.c_size_t(0)
         bps = self.lib.ref_bench_roundtrip(K, N, B, G, pool, erase_max, int(random_count), threads,
-                                           passes, seed, C.byref(secs), C.byref(rec))
+                                           passes, seed, C.byref(secs), C.byref(rec), int(decode_only))
         return bps, secs.value, rec.value

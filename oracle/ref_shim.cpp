@@ -108,7 +108,7 @@ long ref_decode(size_t K, size_t N, const size_t *ids, const uint8_t *const *ptr
 // Returns payload bytes/s = G * passes * K * B / wall seconds.
 double ref_bench_roundtrip(size_t K, size_t N, size_t B, size_t G, size_t pool, size_t erase_max,
                            int random_count, size_t threads, size_t passes, uint64_t seed,
-                           double *seconds_out, size_t *recovered_out)
+                           double *seconds_out, size_t *recovered_out, int decode_only)
 {
     fecpp::fec_code warm(K, N);
     (void)warm;
@@ -123,6 +123,15 @@ double ref_bench_roundtrip(size_t K, size_t N, size_t B, size_t G, size_t pool, 
                 for (size_t k = 0; k < 8 && w * 8 + k < B; ++k) dst[w * 8 + k] = (uint8_t)(v >> (8 * k));
             }
         }
+    // decode-only runs read parity encoded before the timed region
+    std::vector<uint8_t> parity;
+    if (decode_only) {
+        parity.resize(G * (N - K) * B);
+        for (size_t g = 0; g < G; ++g) {
+            auto red = warm.encode(data.data() + g * K * B, K * B, B);
+            for (size_t r = 0; r < N - K; ++r) std::memcpy(parity.data() + (g * (N - K) + r) * B, red[r].get(), B);
+        }
+    }
     std::vector<size_t> recovered(threads, 0);
     auto worker = [&](size_t t) {
         fecpp::fec_code c(K, N);
@@ -131,7 +140,11 @@ double ref_bench_roundtrip(size_t K, size_t N, size_t B, size_t G, size_t pool, 
         for (size_t p = 0; p < passes; ++p)
             for (size_t g = a; g < b; ++g) {
                 const uint8_t *d = data.data() + g * K * B;
-                auto red = c.encode(d, K * B, B);
+                std::vector<std::unique_ptr<uint8_t[]>> red;
+                if (!decode_only) red = c.encode(d, K * B, B);
+                auto par_of = [&](size_t r) -> const uint8_t * {
+                    return decode_only ? parity.data() + (g * (N - K) + r) * B : red[r].get();
+                };
                 // erasure draw: same definition as orc_erasure_mask / the HIP generator
                 size_t cnt = erase_max;
                 if (random_count) cnt = 1 + (size_t)(smix(seed ^ ~(uint64_t)g) % erase_max);
@@ -147,7 +160,7 @@ double ref_bench_roundtrip(size_t K, size_t N, size_t B, size_t G, size_t pool, 
                 }
                 std::map<size_t, const uint8_t *> shares;
                 for (size_t s = 0; s < N; ++s)
-                    if (present[s]) shares[s] = s < K ? d + s * B : red[s - K].get();
+                    if (present[s]) shares[s] = s < K ? d + s * B : par_of(s - K);
                 auto res = c.decode(shares, B);
                 rec += res.size();
             }

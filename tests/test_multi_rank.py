@@ -1,0 +1,96 @@
+"""CPU tests of the multi-GPU path: world_size-2 gloo processes partition the group space exactly as
+bench.py's ranks do, compute their share (here with the oracle, since no GPU is present), and the
+combined result equals the single-rank result -- the property the N-GPU bench relies on (no group
+lost or duplicated, no data-path collective)."""
+from __future__ import annotations
+
+import hashlib
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from kcptube_amd.partition import combine_digests, group_range
+
+
+def test_group_range_covers_exactly():
+    for total in (0, 1, 7, 1 << 20, 8 << 20):
+        for world in (1, 2, 3, 4, 8):
+            spans = [group_range(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c and a <= b
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        group_range(10, 2, 2)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, total, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import Oracle
+    o = Oracle()
+    K, N, B, seed = 10, 13, 64, 0x5EED0003
+    g0, g1 = group_range(total, world, rank)
+    data = o.synth(seed, N, B, g0, g1 - g0, 0, K)
+    par = o.encode_batch(K, N, data, B)
+    masks = o.erasure_masks(seed, g1 - g0, N, N, 3, random_max=3, g0=g0)
+    out, idx, st = o.decode_batch(K, N, data, par, masks, B)
+    out[idx == 0xFF] = 0
+    dig = hashlib.sha256(par.tobytes() + out.tobytes()).hexdigest()
+    digs = [None] * world
+    dist.all_gather_object(digs, dig)
+    import torch
+    t = torch.tensor([float(g1 - g0)])
+    dist.all_reduce(t)
+    if rank == 0:
+        with open(os.path.join(out_dir, "res.txt"), "w") as f:
+            f.write(combine_digests(digs) + " " + str(int(t.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_partition_matches_single_rank(tmp_path, oracle):
+    total = 37
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, total, str(tmp_path)), nprocs=2, join=True)
+    combined, n = open(tmp_path / "res.txt").read().split()
+    assert int(n) == total
+    # single-rank reference: same per-range digests computed in one process
+    K, N, B, seed = 10, 13, 64, 0x5EED0003
+    digs = []
+    for r in range(2):
+        g0, g1 = group_range(total, 2, r)
+        data = oracle.synth(seed, N, B, g0, g1 - g0, 0, K)
+        par = oracle.encode_batch(K, N, data, B)
+        masks = oracle.erasure_masks(seed, g1 - g0, N, N, 3, random_max=3, g0=g0)
+        out, idx, st = oracle.decode_batch(K, N, data, par, masks, B)
+        out[idx == 0xFF] = 0
+        digs.append(hashlib.sha256(par.tobytes() + out.tobytes()).hexdigest())
+    assert combined == combine_digests(digs)
+    # and the partition is a partition: the whole range in one go gives the same parity bytes
+    data = oracle.synth(seed, N, B, 0, total, 0, K)
+    par_all = oracle.encode_batch(K, N, data, B)
+    g0, g1 = group_range(total, 2, 1)
+    par_1 = oracle.encode_batch(K, N, oracle.synth(seed, N, B, g0, g1 - g0, 0, K), B)
+    np.testing.assert_array_equal(par_all[g0:g1], par_1)
+
+
+def test_bench_rank_offsets_are_disjoint():
+    """bench.py gives rank r the groups [r*G, (r+1)*G) (weak scaling): disjoint and contiguous."""
+    G = 1 << 20
+    spans = [(r * G, (r + 1) * G) for r in range(8)]
+    for (a, b), (c, d) in zip(spans, spans[1:]):
+        assert b == c

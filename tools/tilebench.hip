@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(NT) kA(const uint8_t* __restrict__ d, uint8_t*
 
 // B: tile with register prefetch of the next group (issue-early / write-late), W=2 columns, NT threads
 template <int NT, bool GF, int LPT>
-__global__ void __launch_bounds__(NT) kB(const uint8_t* __restrict__ d, uint8_t* __restrict__ par, unsigned G, const uint8_t* enc) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 5))) kB(const uint8_t* __restrict__ d, uint8_t* __restrict__ par, unsigned G, const uint8_t* enc) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s[];
   uint32_t* tb = (uint32_t*)(s + K * B);
   for (int e = threadIdx.x; e < K * R; e += NT) {
@@ -69,18 +69,22 @@ __global__ void __launch_bounds__(NT) kB(const uint8_t* __restrict__ d, uint8_t*
   static_assert(LPT * NT >= nv, "prefetch covers the group");
   uint4 pf[LPT];
   unsigned g = blockIdx.x;
-  auto load = [&](unsigned gg) {
-    const uint4* src = (const uint4*)(d + (size_t)gg * K * B);
+  {
+    const uint4* src = (const uint4*)(d + (size_t)g * K * B);
 #pragma unroll
-    for (int k = 0; k < LPT; ++k) { unsigned i = threadIdx.x + k * NT; if (i < nv && gg < G) pf[k] = src[i]; }
-  };
-  load(g);
+    for (int k = 0; k < LPT; ++k) { const unsigned i = threadIdx.x + k * NT; if (i < nv && g < G) pf[k] = src[i]; }
+  }
   for (; g < G; g += gridDim.x) {
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < LPT; ++k) { unsigned i = threadIdx.x + k * NT; if (i < nv) ((uint4*)s)[i] = pf[k]; }
+    for (int k = 0; k < LPT; ++k) { const unsigned i = threadIdx.x + k * NT; if (i < nv) ((uint4*)s)[i] = pf[k]; }
     __syncthreads();
-    load(g + gridDim.x);
+    const unsigned gn = g + gridDim.x;
+    if (gn < G) {
+      const uint4* src = (const uint4*)(d + (size_t)gn * K * B);
+#pragma unroll
+      for (int k = 0; k < LPT; ++k) { const unsigned i = threadIdx.x + k * NT; if (i < nv) pf[k] = src[i]; }
+    }
     const unsigned c = threadIdx.x;
     if (c < cols) {
       uint32_t acc[R][2] = {};
