@@ -111,6 +111,10 @@ int kfec_erasure_masks(const kfec_ctx *ctx, uint64_t seed, size_t g0, size_t G, 
 int kfec_verify_recovered(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, const void *d_data,
                           const void *d_out, const uint8_t *d_out_idx, uint64_t *d_mismatch, void *stream);
 
+/* Non-zero if a bounded spin of the persistent stream-engine kernel ever timed out on the current device
+ * (bit 0: loader, bit 1: consumer).  Never expected; the engine exits instead of hanging the GPU. */
+uint32_t kfec_debug_flags(void);
+
 /* Library version string and the device the context runs on (-1 if none). */
 const char *kfec_version(void);
 int kfec_device(const kfec_ctx *ctx);

@@ -78,7 +78,9 @@ inline int set_dev(const kfec_ctx *c) { return hipSetDevice(c->di.device) == hip
 
 extern "C" {
 
-const char *kfec_version(void) { return "kfec 0.1 (gfx950 perm-MAC)"; }
+const char *kfec_version(void) { return "kfec 0.2 (gfx950 perm-MAC, LDS-DMA stream engine)"; }
+
+uint32_t kfec_debug_flags(void) { return kfec::engine_error_word(); }
 
 int kfec_device(const kfec_ctx *ctx) { return ctx ? ctx->di.device : -1; }
 

@@ -9,9 +9,11 @@ namespace kfec {
 // Per-group decode record written by the prep kernels and read by the MAC kernel (group-major, so the
 // few records a workgroup needs per iteration are a couple of contiguous cache lines):
 //   [0] status (KFEC_GROUP_*), [1] m = missing data shards, [2..3] 0,
-//   [4, 4+K)            src[j]    share id used as column j of the selected K x K system,
-//   [4+K, 4+K+R*K)      coef[u][j] row u (u < m) of the inverse decode matrix for missing shard u.
-inline size_t record_stride(size_t K, size_t R) { return (4 + K + R * K + 15) & ~size_t(15); }
+//   [4, 4+K4)              src[j]     share id used as column j of the selected K x K system,
+//   [4+K4, 4+K4+R*K4)      coef[u][j] row u (u < m) of the inverse decode matrix for missing shard u,
+// with K4 = K rounded up to 4 so that the prep kernel writes whole dwords.
+inline size_t rec_k4(size_t K) { return (K + 3) & ~size_t(3); }
+inline size_t record_stride(size_t K, size_t R) { return (4 + rec_k4(K) + R * rec_k4(K) + 15) & ~size_t(15); }
 
 struct DeviceInfo {
     int device = -1;
@@ -31,5 +33,7 @@ int launch_erasure_masks(uint64_t seed, int N, size_t g0, size_t G, size_t pool,
                          int random_count, uint64_t *d_present, hipStream_t s);
 int launch_verify(int K, int N, size_t G, size_t B, size_t pitch, const void *d_data, const void *d_out,
                   const uint8_t *d_out_idx, uint64_t *d_mismatch, hipStream_t s);
+
+uint32_t engine_error_word();
 
 }  // namespace kfec

@@ -31,6 +31,26 @@ namespace kfec {
 
 __constant__ GfTables c_gf = make_gf_tables();
 
+// set by the stream engine if a bounded spin ever times out (read by kfec_engine_error)
+__device__ uint32_t g_engine_err;
+
+static uint32_t *g_err_word()
+{
+    static uint32_t *p[64] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    dev &= 63;
+    if (!p[dev]) (void)hipGetSymbolAddress(reinterpret_cast<void **>(&p[dev]), HIP_SYMBOL(g_engine_err));
+    return p[dev];
+}
+
+uint32_t engine_error_word()
+{
+    uint32_t v = 0;
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_engine_err), sizeof(v));
+    return v;
+}
+
 static constexpr int kBlock = 256;
 
 // build-time tuning knobs (tools/ab.py builds variants; the shipped library uses the defaults)
@@ -39,6 +59,9 @@ static constexpr int kBlock = 256;
 #endif
 #ifndef KFEC_ABLATE
 #define KFEC_ABLATE 0
+#endif
+#ifndef KFEC_VEC32
+#define KFEC_VEC32 1  // 32-byte lane granules in the flattened kernel (2 KiB per wave-instruction pair)
 #endif
 #ifndef KFEC_MINW
 #define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the flattened kernel
@@ -256,47 +279,58 @@ __global__ void __launch_bounds__(kBlock) decode_prep_small(PrepArgs a)
         for (int u = 0; u < MAXM; ++u)
 #pragma unroll
             for (int t = 0; t < MAXM; ++t) lS[u][t] = Iv[u][t] ? s_log[Iv[u][t]] : 0x1FFu;
-        uint8_t *src = rec + 4, *coef = rec + 4 + K;
-        for (int j = 0; j < K; ++j) {
-            const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
-            if (miss) {
-                // rank of j among the missing ids
-                int t = 0;
+        // columns in groups of 4 so that src and every coefficient row are written as whole dwords
+        const int K4 = (K + 3) & ~3;
+        uint32_t *srcw = reinterpret_cast<uint32_t *>(rec + 4);
+        uint32_t *coefw = reinterpret_cast<uint32_t *>(rec + 4 + K4);
+        for (int j0 = 0; j0 < K4; j0 += 4) {
+            uint32_t sw = 0, cw[MAXM];
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    t += (q < (j >> 6)) ? __popcll(dm[q]) : (q == (j >> 6) ? __popcll(dm[q] & ((1ull << (j & 63)) - 1ull)) : 0);
-                int pt = 0;
+            for (int u = 0; u < MAXM; ++u) cw[u] = 0;
 #pragma unroll
-                for (int tt = 0; tt < MAXM; ++tt) pt = (tt == t) ? P[tt] : pt;
-                src[j] = (uint8_t)pt;
+            for (int b = 0; b < 4; ++b) {
+                const int j = j0 + b;
+                if (j >= K) break;
+                const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
+                if (miss) {
+                    int t = 0;  // rank of j among the missing ids
 #pragma unroll
-                for (int u = 0; u < MAXM; ++u) {
-                    if (u < m) {
+                    for (int q = 0; q < 4; ++q)
+                        t += (q < (j >> 6)) ? __popcll(dm[q])
+                                            : (q == (j >> 6) ? __popcll(dm[q] & ((1ull << (j & 63)) - 1ull)) : 0);
+                    uint32_t pt = 0;
+#pragma unroll
+                    for (int tt = 0; tt < MAXM; ++tt) pt = (tt == t) ? (uint32_t)P[tt] : pt;
+                    sw |= pt << (8 * b);
+#pragma unroll
+                    for (int u = 0; u < MAXM; ++u) {
                         uint32_t v = 0;
 #pragma unroll
                         for (int tt = 0; tt < MAXM; ++tt) v = (tt == t) ? Iv[u][tt] : v;
-                        coef[u * K + j] = (uint8_t)v;
+                        cw[u] |= v << (8 * b);
                     }
-                }
-            } else {
-                src[j] = (uint8_t)j;
-                uint32_t le[MAXM];
+                } else {
+                    sw |= (uint32_t)j << (8 * b);
+                    uint32_t le[MAXM];
 #pragma unroll
-                for (int t = 0; t < MAXM; ++t) {
-                    const uint32_t e = (t < m) ? s_E[(P[t] - K) * K + j] : 0u;
-                    le[t] = e ? s_log[e] : 0x1FFu;
-                }
+                    for (int t = 0; t < MAXM; ++t) {
+                        const uint32_t e = (t < m) ? s_E[(P[t] - K) * K + j] : 0u;
+                        le[t] = e ? s_log[e] : 0x1FFu;
+                    }
 #pragma unroll
-                for (int u = 0; u < MAXM; ++u) {
-                    if (u < m) {
+                    for (int u = 0; u < MAXM; ++u) {
                         uint32_t v = 0;
 #pragma unroll
                         for (int t = 0; t < MAXM; ++t)
                             if (t < m && lS[u][t] != 0x1FFu && le[t] != 0x1FFu) v ^= s_exp[lS[u][t] + le[t]];
-                        coef[u * K + j] = (uint8_t)v;
+                        cw[u] |= v << (8 * b);
                     }
                 }
             }
+            srcw[j0 >> 2] = sw;
+#pragma unroll
+            for (int u = 0; u < MAXM; ++u)
+                if (u < m) coefw[u * (K4 >> 2) + (j0 >> 2)] = cw[u];
         }
 #pragma unroll
         for (int t = 0; t < MAXM; ++t)
@@ -394,7 +428,8 @@ __global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
             __syncthreads();
             continue;
         }
-        uint8_t *src = rec + 4, *coef = rec + 4 + K;
+        const int K4 = (K + 3) & ~3;
+        uint8_t *src = rec + 4, *coef = rec + 4 + K4;
         for (int j = lane; j < K; j += 64) {
             const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
             src[j] = miss ? s_P[s_rank[j]] : (uint8_t)j;
@@ -408,7 +443,7 @@ __global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
             } else {
                 for (int t = 0; t < m; ++t) v ^= gmul(s_exp, s_log, s_A[u * W2 + m + t], s_E[(s_P[t] - K) * K + j]);
             }
-            coef[u * K + j] = (uint8_t)v;
+            coef[u * K4 + j] = (uint8_t)v;
         }
         for (int t = lane; t < R; t += 64) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
         if (lane == 0) {
@@ -431,8 +466,9 @@ struct MacArgs {
     const uint8_t *enc;     // N x K encoding matrix (encode)
     const uint8_t *rec;     // per-group records (decode)
     uint64_t pitch;
-    uint32_t total;         // G * cols work items
+    uint32_t total;         // G * cpad work items
     uint32_t cols;          // granules per shard
+    uint32_t cpad;          // items per group (>= cols; lanes with col >= cols idle)
     uint32_t G, K, R, B;
     uint32_t rec_stride;
     uint32_t JC;            // shards per LDS chunk
@@ -449,7 +485,11 @@ template <int VEC>
 __device__ __forceinline__ Gran<VEC> load_gran(const uint8_t *p, uint32_t col, uint32_t B)
 {
     Gran<VEC> v;
-    if constexpr (VEC == 16) {
+    if constexpr (VEC == 32) {
+        const uint4 x = reinterpret_cast<const uint4 *>(p)[0], y = reinterpret_cast<const uint4 *>(p)[1];
+        v.d[0] = x.x; v.d[1] = x.y; v.d[2] = x.z; v.d[3] = x.w;
+        v.d[4] = y.x; v.d[5] = y.y; v.d[6] = y.z; v.d[7] = y.w;
+    } else if constexpr (VEC == 16) {
         const uint4 x = *reinterpret_cast<const uint4 *>(p);
         v.d[0] = x.x; v.d[1] = x.y; v.d[2] = x.z; v.d[3] = x.w;
     } else if constexpr (VEC == 8) {
@@ -471,7 +511,10 @@ __device__ __forceinline__ Gran<VEC> load_gran(const uint8_t *p, uint32_t col, u
 template <int VEC>
 __device__ __forceinline__ void store_gran(uint8_t *p, const uint32_t *d, uint32_t col, uint32_t B)
 {
-    if constexpr (VEC == 16) {
+    if constexpr (VEC == 32) {
+        store_gran<16>(p, d, col, B);
+        store_gran<16>(p + 16, d + 4, col, B);
+    } else if constexpr (VEC == 16) {
 #if KFEC_NTSTORE
         typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
         __builtin_nontemporal_store(u32x4_t{d[0], d[1], d[2], d[3]}, reinterpret_cast<u32x4_t *>(p));
@@ -528,10 +571,11 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
         uint8_t *ent = s_ent + (gs * a.JC + jj) * L::ENTRY;
         uint32_t c = 0;
         if constexpr (DEC) {
+            const uint32_t K4 = (a.K + 3) & ~3u;
             const uint32_t g = gfirst + gs;
             const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
             const uint32_t st = rec[0], m = rec[1];
-            if (st == 0 && u < m) c = rec[4 + a.K + u * a.K + j];
+            if (st == 0 && u < m) c = rec[4 + K4 + u * K4 + j];
             if (r == 0) {
                 const uint32_t src = rec[4 + j];
                 const uint8_t *p = (src < a.K) ? a.data + ((uint64_t)g * a.K + src) * a.pitch
@@ -554,12 +598,12 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
 {
     using L = MacLayout<MT>;
     constexpr int W = Gran<VEC>::W;
-    constexpr int PD = KFEC_PD;  // shards in flight per lane
+    constexpr int PD = VEC >= 32 ? KFEC_PD / 2 : KFEC_PD;  // shards in flight per lane (~64 B per lane)
     constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
 
     const uint32_t row0 = blockIdx.y * MT;
-    const uint32_t K = a.K, cols = a.cols;
+    const uint32_t K = a.K, cols = a.cpad;
     const bool enc_once = !DEC && K <= a.JC;
     if (enc_once) {
         mac_expand<MT, false>(a, s_ent, 0, 1, 0, K, row0);
@@ -568,9 +612,9 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
     const uint32_t stride = gridDim.x * kBlock;
     for (uint32_t base = blockIdx.x * kBlock; base < a.total; base += stride) {
         const uint32_t item = base + threadIdx.x;
-        const bool in = item < a.total;
-        const uint32_t g = in ? item / cols : 0;
-        const uint32_t col = in ? item - g * cols : 0;
+        const uint32_t g = item < a.total ? item / cols : 0;
+        const uint32_t col = item < a.total ? item - g * cols : 0;
+        const bool in = item < a.total && col < a.cols;
         const uint32_t gfirst = base / cols;
         const uint32_t glast = min(base + kBlock - 1, a.total - 1) / cols;
         const uint32_t ng = glast - gfirst + 1;
@@ -696,7 +740,7 @@ __device__ __forceinline__ void tile_expand(const LdsArgs &a, uint8_t *s_tbl, ui
         const uint32_t r = e % MT, jj = e / MT, j = c0 + jj, u = row0 + r;
         uint32_t c = 0;
         if constexpr (DEC) {
-            if (u < m) c = a.rec[(uint64_t)g * a.rec_stride + 4 + a.K + u * a.K + j];
+            if (u < m) c = a.rec[(uint64_t)g * a.rec_stride + 4 + ((a.K + 3) & ~3u) * (1 + u) + j];
         } else {
             if (u < a.R) c = a.enc[(uint64_t)(a.K + u) * a.K + j];
         }
@@ -816,6 +860,33 @@ __device__ __forceinline__ void tile_mac(u32x2_t (&acc)[MT], u32x2_t x, const ui
     }
 }
 
+// as tile_mac, with the shard's tables already in registers (TileLayout order)
+template <int MT>
+__device__ __forceinline__ void tile_mac_regs(u32x2_t (&acc)[MT], u32x2_t x, const uint4 *tv)
+{
+    using L = TileLayout<MT>;
+    const uint32_t *t4 = reinterpret_cast<const uint32_t *>(tv + MT);
+    uint32_t s0[2], s1[2], s2[2];
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+        s0[w] = x[w] & 0x07070707u;
+        s1[w] = (x[w] >> 3) & 0x07070707u;
+        s2[w] = (x[w] >> 6) & 0x03030303u;
+    }
+#pragma unroll
+    for (int r = 0; r < MT; ++r) {
+        const uint32_t t[5] = {tv[r].x, tv[r].y, tv[r].z, tv[r].w, t4[r]};
+#if KFEC_ABLATE == 1
+        acc[r][0] ^= x[0] ^ t[0];
+        acc[r][1] ^= x[1] ^ t[4];
+#else
+#pragma unroll
+        for (int w = 0; w < 2; ++w) acc[r][w] = perm_mac(acc[r][w], t, s0[w], s1[w], s2[w]);
+#endif
+    }
+    (void)sizeof(L);
+}
+
 // Persistent workgroup walking its (group, chunk) units through a 2-deep LDS ring: the DMA of unit u+1
 // is in flight while unit u is computed.  Tables (and, for encode with few shards, the whole table set)
 // live beside the ring.
@@ -920,10 +991,226 @@ __global__ void __launch_bounds__(256) mac_tile_kernel(LdsArgs a)
 }
 
 // ---------------------------------------------------------------------------------------------------
+// (A4/A5/A8/A11) stream engine: one persistent workgroup per CU, role-split waves.
+//   loader waves (kEngNL) gather whole groups (or chunks of JS shards) into a kEngS-slot LDS ring with
+//     LDS-DMA (global_load_lds_dwordx4, per-lane 16-B sources, 1 KiB of LDS per wave-instruction).
+//     A group of 20 x 1440 B is 225 complete 128-B lines, so no line is fetched twice.  Each loader owns
+//     units u = w, w + NL, ...: waits for the slot to be free, issues all its DMAs, waits vmcnt(0),
+//     publishes the slot.  Several units are in flight per CU at any time.
+//   consumer teams (2 x kEngTW waves) take alternate groups; each lane owns one 8-byte column and
+//     accumulates its MT output rows over the group's chunks, then stores them (non-temporal).
+//   Hand-off: LDS counters filled[s] (fill generation) and consumed[s] (consumer waves done), workgroup-
+//   scope release/acquire.  Every spin is bounded: on timeout the wave sets a flag and leaves, so a bug
+//   can never hang the GPU (outputs would then fail verification).
+// ---------------------------------------------------------------------------------------------------
+static constexpr int kEngS = 5;     // ring slots
+static constexpr int kEngNL = 3;    // loader waves
+static constexpr int kEngTW = 4;    // waves per consumer team (256 lanes: one 8-byte column each)
+static constexpr int kEngThreads = (kEngNL + 2 * kEngTW) * 64;
+static constexpr uint32_t kSpinMax = 1u << 22;
+
+struct StreamArgs {
+    const uint8_t *data, *parity;
+    uint8_t *out;
+    const uint8_t *enc, *rec;
+    uint32_t *err;          // device word: set non-zero if a spin timed out
+    uint64_t pitch;
+    uint32_t G, K, R, B;
+    uint32_t rec_stride;
+    uint32_t JS, nch;       // shards per unit, units per group
+    uint32_t Bs;            // LDS row stride (B rounded up to 16)
+    uint32_t slot_bytes;    // JS * Bs rounded up to 1 KiB
+    uint32_t cols;          // 8-byte columns = ceil(B / 8)
+    uint64_t bs_inv;        // ceil(2^32 / Bs)
+};
+
+__device__ __forceinline__ uint32_t lds_load_acq(uint32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// wait until *p >= target; false on timeout
+__device__ __forceinline__ bool spin_ge(uint32_t *p, uint32_t target)
+{
+    for (uint32_t i = 0; i < kSpinMax; ++i) {
+        if (lds_load_acq(p) >= target) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+
+template <int MT, bool DEC>
+__global__ void __launch_bounds__(kEngThreads) mac_stream_kernel(StreamArgs a)
+{
+    using L = TileLayout<MT>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t K = a.K, JS = a.JS, nch = a.nch;
+    // LDS: [S slots][tables: encode K*TBL once | decode S*JS*TBL][filled[S], consumed[S]]
+    const uint32_t tbl0 = kEngS * a.slot_bytes;
+    const uint32_t tbl_bytes = DEC ? kEngS * JS * L::TBL : K * L::TBL;
+    uint32_t *filled = reinterpret_cast<uint32_t *>(smem + tbl0 + tbl_bytes);
+    uint32_t *consumed = filled + kEngS;
+
+    if (threadIdx.x < kEngS) {
+        filled[threadIdx.x] = 0;
+        consumed[threadIdx.x] = 0;
+    }
+    if constexpr (!DEC) {  // encode tables of all K shards, once
+        for (uint32_t e = threadIdx.x; e < K * MT; e += blockDim.x) {
+            const uint32_t r = e % MT, j = e / MT;
+            const uint32_t cf = (r < a.R) ? a.enc[(uint64_t)(K + r) * K + j] : 0u;
+            uint32_t t[5];
+            gf_perm_tables(cf, t);
+            uint8_t *tb = smem + tbl0 + j * L::TBL;
+            *reinterpret_cast<uint4 *>(tb + r * 16) = make_uint4(t[0], t[1], t[2], t[3]);
+            reinterpret_cast<uint32_t *>(tb + MT * 16)[r] = t[4];
+        }
+    }
+    __syncthreads();
+
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t my_groups = a.G > blockIdx.x ? (a.G - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+    const uint32_t n_units = my_groups * nch;
+
+    if (wave < kEngNL) {
+        // ---------------- loader ----------------
+        for (uint32_t u = wave; u < n_units; u += kEngNL) {
+            const uint32_t k = u / nch, c = u - k * nch, g = blockIdx.x + k * gridDim.x;
+            const uint32_t s = u % kEngS, f = u / kEngS;
+            if (!spin_ge(&consumed[s], kEngTW * f)) {
+                if (lane == 0) atomicOr(a.err, 1u);
+                return;
+            }
+            const uint32_t c0 = c * JS, nj = min(JS, K - c0);
+            uint8_t *slot = smem + s * a.slot_bytes;
+            bool work = true;
+            const uint8_t *rec = nullptr;
+            if constexpr (DEC) {
+                rec = a.rec + (uint64_t)g * a.rec_stride;
+                const uint32_t st = rec[0], m = rec[1];
+                work = (st == 0 && m > 0);
+                if (work) {
+                    uint8_t *tb = smem + tbl0 + s * JS * L::TBL;
+                    for (uint32_t e = lane; e < nj * MT; e += 64) {
+                        const uint32_t r = e % MT, jj = e / MT;
+                        const uint32_t cf = (r < m) ? rec[4 + ((K + 3) & ~3u) * (1 + r) + c0 + jj] : 0u;
+                        uint32_t t[5];
+                        gf_perm_tables(cf, t);
+                        *reinterpret_cast<uint4 *>(tb + jj * L::TBL + r * 16) = make_uint4(t[0], t[1], t[2], t[3]);
+                        reinterpret_cast<uint32_t *>(tb + jj * L::TBL + MT * 16)[r] = t[4];
+                    }
+                }
+            }
+            if (work) {
+                // shard base addresses of this unit, one per lane (nj <= 64 is not required: lanes
+                // beyond 64 shards fall back to a direct lookup), fetched with one coalesced load
+                uint64_t my_base = 0;
+                if constexpr (DEC) {
+                    if (lane < nj) {
+                        const uint32_t sid = rec[4 + c0 + lane];
+                        my_base = reinterpret_cast<uint64_t>((sid < K) ? a.data + ((uint64_t)g * K + sid) * a.pitch
+                                                                       : a.parity + ((uint64_t)g * a.R + (sid - K)) * a.pitch);
+                    }
+                }
+                const uint32_t bytes = nj * a.Bs;
+                for (uint32_t ch = 0; ch * 1024 < bytes; ++ch) {
+                    const uint32_t o = ch * 1024 + lane * 16;
+                    const uint32_t jj = (uint32_t)(((uint64_t)min(o, bytes - 1) * a.bs_inv) >> 32), off = o - jj * a.Bs;
+                    const uint8_t *src;
+                    if constexpr (DEC) {
+                        if (nj <= 64) {
+                            src = reinterpret_cast<const uint8_t *>(__shfl(my_base, (int)jj));
+                        } else {
+                            const uint32_t sid = rec[4 + c0 + jj];
+                            src = (sid < K) ? a.data + ((uint64_t)g * K + sid) * a.pitch
+                                            : a.parity + ((uint64_t)g * a.R + (sid - K)) * a.pitch;
+                        }
+                    } else {
+                        src = a.data + ((uint64_t)g * K + c0 + jj) * a.pitch;
+                    }
+                    if (o < bytes) {
+#if defined(__HIP_DEVICE_COMPILE__)
+                        __builtin_amdgcn_global_load_lds(src + off, (__attribute__((address_space(3))) void *)(slot + ch * 1024),
+                                                         16, 0, 0);
+#endif
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(&filled[s], f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return;
+    }
+    // ---------------- consumer ----------------
+    const uint32_t team = (wave - kEngNL) / kEngTW, tw = (wave - kEngNL) % kEngTW;
+    const uint32_t col = tw * 64 + lane;
+    for (uint32_t k = team; k < my_groups; k += 2) {
+        const uint32_t g = blockIdx.x + k * gridDim.x;
+        uint32_t rows;
+        if constexpr (DEC) {
+            const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
+            const uint32_t st = rec[0], m = rec[1];
+            rows = (st == 0) ? min((uint32_t)MT, m) : 0u;
+        } else {
+            rows = min((uint32_t)MT, a.R);
+        }
+        u32x2_t acc[MT];
+#pragma unroll
+        for (int r = 0; r < MT; ++r) acc[r] = u32x2_t{0u, 0u};
+        for (uint32_t c = 0; c < nch; ++c) {
+            const uint32_t u = k * nch + c, s = u % kEngS, f = u / kEngS;
+            if (!spin_ge(&filled[s], f + 1)) {
+                if (lane == 0) atomicOr(a.err, 2u);
+                return;
+            }
+            const uint32_t c0 = c * JS, nj = min(JS, K - c0);
+            if (rows && col < a.cols) {
+                const uint8_t *xs = smem + s * a.slot_bytes + col * 8;
+                const uint8_t *tb = DEC ? smem + tbl0 + s * JS * L::TBL : smem + tbl0 + c0 * L::TBL;
+                // software pipeline: shard jj+1's data and tables are read while shard jj is computed
+                // (2 waves per SIMD cannot hide LDS latency by themselves)
+                u32x2_t xn = *reinterpret_cast<const u32x2_t *>(xs);
+                uint4 tn[L::TBL / 16];
+#pragma unroll
+                for (int q = 0; q < L::TBL / 16; ++q) tn[q] = reinterpret_cast<const uint4 *>(tb)[q];
+                for (uint32_t jj = 0; jj < nj; ++jj) {
+                    const u32x2_t x = xn;
+                    uint4 tc[L::TBL / 16];
+#pragma unroll
+                    for (int q = 0; q < L::TBL / 16; ++q) tc[q] = tn[q];
+                    if (jj + 1 < nj) {
+                        xn = *reinterpret_cast<const u32x2_t *>(xs + (jj + 1) * a.Bs);
+#pragma unroll
+                        for (int q = 0; q < L::TBL / 16; ++q)
+                            tn[q] = reinterpret_cast<const uint4 *>(tb + (jj + 1) * L::TBL)[q];
+                    }
+                    tile_mac_regs<MT>(acc, x, tc);
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_fetch_add(&consumed[s], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (rows && col < a.cols) {
+            uint8_t *o = a.out + ((uint64_t)g * a.R) * a.pitch + (uint64_t)col * 8;
+#pragma unroll
+            for (int r = 0; r < MT; ++r)
+                if ((uint32_t)r < rows) __builtin_nontemporal_store(acc[r], reinterpret_cast<u32x2_t *>(o + (uint64_t)r * a.pitch));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
 // host-side launch helpers
 // ---------------------------------------------------------------------------------------------------
 static int pick_vec(size_t pitch, std::initializer_list<const void *> ptrs)
 {
+#if KFEC_VEC32
+    {
+        bool ok = (pitch % 32) == 0;
+        for (const void *p : ptrs) ok = ok && (reinterpret_cast<uintptr_t>(p) % 16) == 0;
+        if (ok) return 32;
+    }
+#endif
     for (int v : {16, 8, 4}) {
         bool ok = (pitch % v) == 0;
         for (const void *p : ptrs) ok = ok && (reinterpret_cast<uintptr_t>(p) % v) == 0;
@@ -942,6 +1229,17 @@ static int resident_blocks(const void *kernel, size_t lds)
 }
 
 static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
+
+// KFEC_PAD=1: pad a group's items to whole waves, so one wave-instruction reads a whole shard row and
+// both halves of every 128-B line that straddles two shards are read by consecutive instructions
+static size_t pad_cols(size_t cols)
+{
+    static const bool on = [] {
+        const char *e = getenv("KFEC_PAD");
+        return e && std::string(e) == "1";
+    }();
+    return on ? (cols + 63) / 64 * 64 : cols;
+}
 
 template <int VEC, int MT, bool DEC>
 static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
@@ -970,6 +1268,9 @@ static int dispatch_mac(const DeviceInfo &di, int vec, int mt, MacArgs a, int ti
     default: return run_mac<V, 8, DEC>(di, a, tiles, s);                     \
     }
     switch (vec) {
+#if KFEC_VEC32
+    case 32: KFEC_MT_CASES(32)
+#endif
     case 16: KFEC_MT_CASES(16)
     case 8: KFEC_MT_CASES(8)
     case 4: KFEC_MT_CASES(4)
@@ -1032,11 +1333,89 @@ static int run_tile(const DeviceInfo &di, LdsArgs a, int tiles, hipStream_t s)
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// ---- stream engine launch ----
+static constexpr size_t kEngLdsMax = 160 * 1024 - 1024;
+
+struct EngPlan {
+    bool ok = false;
+    uint32_t JS = 0, nch = 0, Bs = 0, slot_bytes = 0;
+    size_t lds = 0;
+};
+
+static EngPlan plan_stream(uint32_t K, uint32_t R, uint32_t B, int mt, bool dec)
+{
+    EngPlan p;
+    if (B == 0 || B > 2048 || R == 0 || R > (uint32_t)mt) return p;
+    const uint32_t tbl = (uint32_t)(mt * 16 + (mt + 3) / 4 * 16);
+    p.Bs = (B + 15) & ~15u;
+    const size_t enc_tbl = dec ? 0 : (size_t)K * tbl;
+    if (enc_tbl + 64 >= kEngLdsMax) return p;
+    for (uint32_t js = std::min<uint32_t>(K, (32 * 1024) / p.Bs); js >= 1; --js) {
+        const uint32_t slot = ((js * p.Bs + 1023) / 1024) * 1024;
+        const size_t lds = (size_t)kEngS * (slot + (dec ? (size_t)js * tbl : 0)) + enc_tbl + 64;
+        if (lds <= kEngLdsMax) {
+            p.ok = true;
+            p.JS = js;
+            p.nch = (K + js - 1) / js;
+            p.slot_bytes = slot;
+            p.lds = lds;
+            return p;
+        }
+    }
+    return p;
+}
+
+template <int MT, bool DEC>
+static int run_stream(const DeviceInfo &di, StreamArgs a, const EngPlan &p, hipStream_t s)
+{
+    static bool attr_set = false;  // per instantiation: allow > 64 KiB of dynamic LDS
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void *)mac_stream_kernel<MT, DEC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kEngLdsMax) != hipSuccess)
+            return -3;
+        attr_set = true;
+    }
+    a.JS = p.JS;
+    a.nch = p.nch;
+    a.Bs = p.Bs;
+    a.slot_bytes = p.slot_bytes;
+    a.cols = (a.B + 7) / 8;
+    a.bs_inv = ((1ull << 32) + a.Bs - 1) / a.Bs;
+    const uint32_t gx = std::max(1u, std::min<uint32_t>(a.G, (uint32_t)std::max(1, di.cus)));
+    hipLaunchKernelGGL((mac_stream_kernel<MT, DEC>), dim3(gx), dim3(kEngThreads), p.lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <bool DEC>
+static int dispatch_stream(const DeviceInfo &di, StreamArgs a, const EngPlan &p, int mt, hipStream_t s)
+{
+    switch (mt) {
+    case 1: return run_stream<1, DEC>(di, a, p, s);
+    case 2: return run_stream<2, DEC>(di, a, p, s);
+    case 3: return run_stream<3, DEC>(di, a, p, s);
+    case 4: return run_stream<4, DEC>(di, a, p, s);
+    default: return run_stream<8, DEC>(di, a, p, s);
+    }
+}
+
+// the stream engine serves layouts with 16-B aligned slots, B <= 2 KiB and R <= 8 (one row tile).
+// Measured slower than the flattened kernel (its LDS ring holds ~3 groups in flight per CU, the
+// flattened kernel's VGPRs ~4x that), so it is opt-in: KFEC_KERNEL=engine.
+static bool stream_enabled()
+{
+    static const bool on = [] {
+        const char *e = getenv("KFEC_KERNEL");
+        return e && std::string(e) == "engine";
+    }();
+    return on;
+}
+
 template <bool DEC>
 static int dispatch_tile(const DeviceInfo &di, int sv, LdsArgs a, hipStream_t g_stream)
 {
     const int mt = a.R <= 4 ? std::max<int>(a.R, 1) : 8;
     const int tiles = ((int)a.R + mt - 1) / mt;
+    if (sv > 16) sv = 16;
 #define KFEC_TILE_MT(SV)                                                           \
     switch (mt) {                                                                  \
     case 1: return run_tile<1, DEC, SV>(di, a, tiles, g_stream);                   \
@@ -1081,14 +1460,28 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
         return dispatch_tile<false>(di, pick_vec(pitch, {d_data, d_parity}), a, s);
     }
+    if (stream_enabled() && G < 0xFFFFFFFFull && pick_vec(pitch, {d_data, d_parity}) >= 16) {
+        const int mt = pick_mt(R);
+        const EngPlan p = plan_stream(K, R, (uint32_t)B, mt, false);
+        if (p.ok) {
+            StreamArgs a{};
+            a.data = static_cast<const uint8_t *>(d_data);
+            a.out = static_cast<uint8_t *>(d_parity);
+            a.enc = d_enc;
+            a.err = g_err_word();
+            a.pitch = pitch;
+            a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
+            return dispatch_stream<false>(di, a, p, mt, s);
+        }
+    }
     const int vec = pick_vec(pitch, {d_data, d_parity});
     const int vb = vec >= 4 ? vec : 4;
-    const size_t cols = (B + vb - 1) / vb;
+    const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
     const int mt = pick_mt(R);
     const int tiles = (R + mt - 1) / mt;
     const size_t ent = entry_bytes(mt);
     const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / ent));
-    return for_group_ranges(G, cols, [&](size_t g0, size_t gn) {
+    return for_group_ranges(G, cpad, [&](size_t g0, size_t gn) {
         MacArgs a{};
         a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
         a.parity = nullptr;
@@ -1096,8 +1489,9 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.enc = d_enc;
         a.rec = nullptr;
         a.pitch = pitch;
-        a.total = (uint32_t)(gn * cols);
+        a.total = (uint32_t)(gn * cpad);
         a.cols = (uint32_t)cols;
+        a.cpad = (uint32_t)cpad;
         a.G = (uint32_t)gn;
         a.K = K; a.R = R; a.B = (uint32_t)B;
         a.rec_stride = 0;
@@ -1152,15 +1546,32 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.rec_stride = (uint32_t)rs;
         return dispatch_tile<true>(di, pick_vec(pitch, {d_data, d_parity, d_out}), a, s);
     }
+    if (stream_enabled() && G < 0xFFFFFFFFull && pick_vec(pitch, {d_data, d_parity, d_out}) >= 16) {
+        const int mt = pick_mt(R);
+        const EngPlan p = plan_stream(K, R, (uint32_t)B, mt, true);
+        if (p.ok) {
+            StreamArgs a{};
+            a.data = static_cast<const uint8_t *>(d_data);
+            a.parity = static_cast<const uint8_t *>(d_parity);
+            a.out = static_cast<uint8_t *>(d_out);
+            a.enc = d_enc;
+            a.rec = rec;
+            a.err = g_err_word();
+            a.pitch = pitch;
+            a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
+            a.rec_stride = (uint32_t)rs;
+            return dispatch_stream<true>(di, a, p, mt, s);
+        }
+    }
 
     const int vec = pick_vec(pitch, {d_data, d_parity, d_out});
     const int vb = vec >= 4 ? vec : 4;
-    const size_t cols = (B + vb - 1) / vb;
+    const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
     const int mt = pick_mt(R);
     const int tiles = (R + mt - 1) / mt;
     const size_t ent = entry_bytes(mt);
-    return for_group_ranges(G, cols, [&](size_t g0, size_t gn) {
-        const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kBlock - 1) / cols + 2);
+    return for_group_ranges(G, cpad, [&](size_t g0, size_t gn) {
+        const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kBlock - 1) / cpad + 2);
         const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
         MacArgs a{};
         a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
@@ -1169,8 +1580,9 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.enc = d_enc;
         a.rec = rec + g0 * rs;
         a.pitch = pitch;
-        a.total = (uint32_t)(gn * cols);
+        a.total = (uint32_t)(gn * cpad);
         a.cols = (uint32_t)cols;
+        a.cpad = (uint32_t)cpad;
         a.G = (uint32_t)gn;
         a.K = K; a.R = R; a.B = (uint32_t)B;
         a.rec_stride = (uint32_t)rs;

@@ -71,6 +71,7 @@ def load_library():
         "kfec_erasure_masks": (C.c_int, [_vp, C.c_uint64, sz, sz, sz, sz, C.c_int, _vp, _vp]),
         "kfec_verify_recovered": (C.c_int, [_vp, sz, sz, sz, _vp, _vp, _vp, _vp, _vp]),
         "kfec_version": (C.c_char_p, []),
+        "kfec_debug_flags": (C.c_uint32, []),
         "kfec_device": (C.c_int, [_vp]),
     }
     for name, (res, args) in proto.items():
@@ -252,6 +253,11 @@ class FecCode:
         B = pitch if B is None else B
         _check(self._lib.kfec_verify_recovered(self._ctx, G, B, pitch, _dptr(data), _dptr(out), _dptr(out_idx),
                                                _dptr(mismatch), _stream_handle(stream)), "kfec_verify_recovered")
+
+
+def debug_flags() -> int:
+    """kfec_debug_flags(): non-zero if the stream engine's bounded spins ever timed out."""
+    return int(load_library().kfec_debug_flags())
 
 
 def version() -> str:

@@ -338,3 +338,10 @@ def test_compat_header_program(dev):
     r = subprocess.run([COMPAT_TEST], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "COMPAT OK" in r.stdout
+
+
+def test_engine_never_timed_out(dev):
+    """The stream engine's bounded spins never expired during the whole GPU test session."""
+    from kcptube_amd.fec import debug_flags
+    torch.cuda.synchronize()
+    assert debug_flags() == 0

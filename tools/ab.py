@@ -8,10 +8,14 @@ if "--" in args:
 rounds = int(args[0]); libs = args[1:]
 here = os.path.dirname(os.path.abspath(__file__))
 for r in range(rounds):
-    for lib in libs:
+    for spec in libs:
+        lib, _, kv = spec.partition(":")  # lib.so[:KEY=VAL,KEY=VAL]
         env = dict(os.environ, KFEC_LIB=os.path.abspath(lib))
+        for item in filter(None, kv.split(",")):
+            k, v = item.split("=", 1)
+            env[k] = v
         p = subprocess.run([sys.executable, os.path.join(here, "ab_one.py")] + shape, env=env,
                            capture_output=True, text=True, timeout=600)
-        print(p.stdout.strip() or p.stderr[-2000:], flush=True)
+        print(spec.split("/")[-1], p.stdout.strip() or p.stderr[-2000:], flush=True)
         if p.returncode != 0:
             sys.exit(p.returncode)
