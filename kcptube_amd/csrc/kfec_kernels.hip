@@ -63,6 +63,9 @@ static constexpr int kBlock = 256;
 #ifndef KFEC_VEC32
 #define KFEC_VEC32 1  // 32-byte lane granules in the flattened kernel (2 KiB per wave-instruction pair)
 #endif
+#ifndef KFEC_ROT
+#define KFEC_ROT 0  // rotate odd waves' shard order by half a chunk (line-sharing in L2, see mac_kernel)
+#endif
 #ifndef KFEC_MINW
 #define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the flattened kernel
 #endif
@@ -646,11 +649,20 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
             }
             if (rows == 0) continue;
             const uint8_t *ent0 = s_ent + (gs * a.JC) * L::ENTRY;
+            // odd waves walk the chunk's shards rotated by nj/2: a 128-B line shared by two neighbouring
+            // waves (or by the tail of one shard and the head of the next) is then requested ~nj/2
+            // iterations apart, after the first request has filled the L2, instead of as a second miss
+            const uint32_t rot = (KFEC_ROT && ((threadIdx.x >> 6) & 1u)) ? nj / 2 : 0u;
+            auto sj = [&](uint32_t jj) -> uint32_t {
+                const uint32_t j = jj + rot;
+                return j >= nj ? j - nj : j;
+            };
             auto share_ptr = [&](uint32_t jj) -> const uint8_t * {
+                const uint32_t j = sj(jj);
                 if constexpr (DEC) {
-                    return *reinterpret_cast<const uint8_t *const *>(ent0 + jj * L::ENTRY) + (uint64_t)col * VB;
+                    return *reinterpret_cast<const uint8_t *const *>(ent0 + j * L::ENTRY) + (uint64_t)col * VB;
                 } else {
-                    return enc_base + (uint64_t)(c0 + jj) * a.pitch;
+                    return enc_base + (uint64_t)(c0 + j) * a.pitch;
                 }
             };
             Gran<VEC> x[PD];
@@ -665,7 +677,7 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
                         const Gran<VEC> cur = x[u];
                         if (jj + PD < nj) x[u] = load_gran<VEC>(share_ptr(jj + PD), col, a.B);
                         uint32_t t[L::TBL_DW];
-                        const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + jj * L::ENTRY + 16);
+                        const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + sj(jj) * L::ENTRY + 16);
 #pragma unroll
                         for (int i = 0; i < L::TBL_DW / 4; ++i) {
                             const uint4 q = tv[i];
@@ -987,6 +999,213 @@ __global__ void __launch_bounds__(256) mac_tile_kernel(LdsArgs a)
         g = gn;
         c = cn;
         slot ^= 1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// (A4/A5/A8/A11) wave-tile kernel: the primary path for 16-B aligned layouts, B <= 2 KiB, R <= 8.
+// One workgroup = one wave, persistent over its groups.  A group is streamed in chunks of JS shards
+// (20 x 1440 B -> chunks of 8, 8, 4 shards = 90, 90, 45 whole 128-B lines): every wave-instruction
+// loads 1 KiB of consecutive bytes, so each line is requested exactly once (per-lane column loads make
+// the L2 fetch the lines that straddle two shards twice: +12% DRAM reads, measured).  The chunk lands
+// in VGPRs (up to 12 x 16 B per lane), is written to the wave's private LDS tile, and the next chunk's
+// loads are issued before the current one is computed, so ~12 chunks (~135 KiB) are in flight per CU.
+// Each lane computes 16-byte columns l and l + 64 of the MT output rows from LDS.  No barriers: the
+// only LDS hazards are inside one wave (s_waitcnt lgkmcnt + wave barrier).
+// ---------------------------------------------------------------------------------------------------
+static constexpr int kWtLoads = 12;  // max 16-B loads per lane per chunk (12 KiB chunks)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs
+
+struct WtArgs {
+    const uint8_t *data, *parity;
+    uint8_t *out;
+    const uint8_t *enc, *rec;
+    uint64_t pitch;
+    uint32_t G, K, R, B;
+    uint32_t rec_stride;
+    uint32_t JS, nch;       // shards per chunk, chunks per group
+    uint32_t Bs;            // staged row stride in LDS (B rounded up to 16)
+    uint32_t cols;          // 16-B columns = ceil(B / 16) (<= 128)
+    uint64_t bs_inv;        // ceil(2^32 / Bs)
+};
+
+// issue the loads of chunk c of group g into pf; `base` = this lane's shard base address for g (lane j
+// holds shard j's), shuffled to the lanes that need it
+template <bool DEC>
+__device__ __forceinline__ void wt_issue(const WtArgs &a, u32x4_t (&pf)[kWtLoads], uint32_t g, uint32_t c, uint64_t base)
+{
+    const uint32_t K = a.K, lane = threadIdx.x;
+    const uint32_t c0 = c * a.JS, nj = min(a.JS, K - c0), bytes = nj * a.Bs;
+#pragma unroll
+    for (int i = 0; i < kWtLoads; ++i) {
+        const uint32_t o = i * 1024 + lane * 16;
+        const uint32_t oc = min(o, bytes - 1);
+        const uint32_t jj = (uint32_t)(((uint64_t)oc * a.bs_inv) >> 32), off = oc - jj * a.Bs;
+        uint64_t sb;
+        if (K <= 64) {
+            sb = __shfl(base, (int)(c0 + jj));
+        } else {
+            uint32_t sid = c0 + jj;
+            if constexpr (DEC) sid = a.rec[(uint64_t)g * a.rec_stride + 4 + c0 + jj];
+            sb = reinterpret_cast<uint64_t>((sid < K) ? a.data + ((uint64_t)g * K + sid) * a.pitch
+                                                      : a.parity + ((uint64_t)g * a.R + (sid - K)) * a.pitch);
+        }
+        if (o < bytes) pf[i] = *reinterpret_cast<const u32x4_t *>(reinterpret_cast<const uint8_t *>(sb) + off);
+    }
+}
+
+template <int MT, bool DEC>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) mac_wave_kernel(WtArgs a)
+{
+    using L = TileLayout<MT>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t K = a.K, JS = a.JS, nch = a.nch, lane = threadIdx.x;
+    uint8_t *tile = smem;                              // JS rows of Bs bytes
+    uint8_t *tbl = smem + ((JS * a.Bs + 15) & ~15u);   // K x TBL coefficient tables
+    const uint32_t K4 = (K + 3) & ~3u;
+
+    auto rows_of = [&](uint32_t g) -> uint32_t {
+        if constexpr (DEC) {
+            const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
+            return rec[0] == 0 ? min((uint32_t)MT, (uint32_t)rec[1]) : 0u;
+        } else {
+            return min((uint32_t)MT, a.R);
+        }
+    };
+    auto next_group = [&](uint32_t g) -> uint32_t {
+        if constexpr (DEC)
+            while (g < a.G && rows_of(g) == 0) g += gridDim.x;
+        return g;
+    };
+    // shard base addresses of group g, lane j holds shard j's (decode: the selected share)
+    auto shard_base = [&](uint32_t g) -> uint64_t {
+        uint64_t p = 0;
+        if (lane < K) {
+            uint32_t sid = lane;
+            if constexpr (DEC) sid = a.rec[(uint64_t)g * a.rec_stride + 4 + lane];
+            p = reinterpret_cast<uint64_t>((sid < K) ? a.data + ((uint64_t)g * K + sid) * a.pitch
+                                                     : a.parity + ((uint64_t)g * a.R + (sid - K)) * a.pitch);
+        }
+        return p;
+    };
+    u32x4_t pf[kWtLoads];
+    auto expand = [&](uint32_t g) {
+        uint32_t m = a.R;
+        const uint8_t *rec = nullptr;
+        if constexpr (DEC) {
+            rec = a.rec + (uint64_t)g * a.rec_stride;
+            m = rec[1];
+        }
+        for (uint32_t e = lane; e < K * MT; e += 64) {
+            const uint32_t r = e % MT, j = e / MT;
+            uint32_t cf = 0;
+            if constexpr (DEC) {
+                if (r < m) cf = rec[4 + K4 * (1 + r) + j];
+            } else {
+                if (r < a.R) cf = a.enc[(uint64_t)(K + r) * K + j];
+            }
+            uint32_t t[5];
+            gf_perm_tables(cf, t);
+            *reinterpret_cast<uint4 *>(tbl + j * L::TBL + r * 16) = make_uint4(t[0], t[1], t[2], t[3]);
+            reinterpret_cast<uint32_t *>(tbl + j * L::TBL + MT * 16)[r] = t[4];
+        }
+    };
+
+    uint32_t g = next_group(blockIdx.x);
+    if (g >= a.G) return;
+    if constexpr (!DEC) expand(0);
+    uint64_t base = shard_base(g);
+    wt_issue<DEC>(a, pf, g, 0, base);
+    uint32_t c = 0, rows = rows_of(g);
+    uint32_t accw[2][MT][4];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int r = 0; r < MT; ++r)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) accw[p][r][w] = 0;
+    bool need_tables = DEC;
+    while (true) {
+        // the chunk in pf has landed (the compiler waits on first use): stage it into the LDS tile
+        const uint32_t c0 = c * JS, nj = min(JS, K - c0), bytes = nj * a.Bs;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous chunk's tile reads are done
+#pragma unroll
+        for (int i = 0; i < kWtLoads; ++i) {
+            const uint32_t o = i * 1024 + lane * 16;
+            if (o < bytes) *reinterpret_cast<u32x4_t *>(tile + o) = pf[i];
+        }
+        if (need_tables) {
+            expand(g);
+            need_tables = false;
+        }
+        // next unit, and its loads, before computing this one
+        uint32_t gn = g, cn = c + 1;
+        if (cn == nch) {
+            cn = 0;
+            gn = next_group(g + gridDim.x);
+        }
+        uint64_t nbase = base;
+        if (gn < a.G) {
+            if (gn != g) nbase = shard_base(gn);
+            wt_issue<DEC>(a, pf, gn, cn, nbase);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        // compute chunk (g, c) from the tile
+        for (uint32_t jj = 0; jj < nj; ++jj) {
+            const uint8_t *tb = tbl + (c0 + jj) * L::TBL;
+            uint4 tv[L::TBL / 16];
+#pragma unroll
+            for (int q = 0; q < L::TBL / 16; ++q) tv[q] = reinterpret_cast<const uint4 *>(tb)[q];
+            const uint32_t *t4 = reinterpret_cast<const uint32_t *>(tv + MT);
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const uint32_t col = lane + 64 * p;
+                if (p == 1 && col >= a.cols) break;
+                const uint4 xv = *reinterpret_cast<const uint4 *>(tile + jj * a.Bs + col * 16);
+                const uint32_t x[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t s0 = x[w] & 0x07070707u, s1 = (x[w] >> 3) & 0x07070707u, s2 = (x[w] >> 6) & 0x03030303u;
+#pragma unroll
+                    for (int r = 0; r < MT; ++r) {
+                        const uint32_t t[5] = {tv[r].x, tv[r].y, tv[r].z, tv[r].w, t4[r]};
+#if KFEC_ABLATE == 1
+                        accw[p][r][w] ^= x[w] ^ t[0];
+                        (void)s0; (void)s1; (void)s2;
+#else
+                        accw[p][r][w] = perm_mac(accw[p][r][w], t, s0, s1, s2);
+#endif
+                    }
+                }
+            }
+        }
+        if (c + 1 == nch) {  // group done: store its rows, 16 B per lane and column
+            const uint64_t obase = (uint64_t)g * a.R * a.pitch;
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const uint32_t col = lane + 64 * p;
+                if (col < a.cols) {
+#pragma unroll
+                    for (int r = 0; r < MT; ++r)
+                        if ((uint32_t)r < rows) {
+                            __builtin_nontemporal_store(u32x4_t{accw[p][r][0], accw[p][r][1], accw[p][r][2], accw[p][r][3]},
+                                                        reinterpret_cast<u32x4_t *>(a.out + obase + (uint64_t)r * a.pitch + col * 16));
+                        }
+                }
+#pragma unroll
+                for (int r = 0; r < MT; ++r)
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) accw[p][r][w] = 0;
+            }
+            if (gn >= a.G) break;
+            rows = rows_of(gn);
+            need_tables = DEC;
+        }
+        g = gn;
+        c = cn;
+        base = nbase;
     }
 }
 
@@ -1333,6 +1552,75 @@ static int run_tile(const DeviceInfo &di, LdsArgs a, int tiles, hipStream_t s)
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// ---- wave-tile launch ----
+static constexpr size_t kWtLdsMax = 13 * 1024;  // 12 waves (workgroups) per CU fit in 160 KiB
+
+struct WtPlan {
+    bool ok = false;
+    uint32_t JS = 0, nch = 0, Bs = 0;
+    size_t lds = 0;
+};
+
+static WtPlan plan_wave(uint32_t K, uint32_t R, uint32_t B, int mt)
+{
+    WtPlan p;
+    if (B == 0 || B > 2048 || R == 0 || R > (uint32_t)mt) return p;
+    const uint32_t tbl = (uint32_t)(mt * 16 + (mt + 3) / 4 * 16);
+    p.Bs = (B + 15) & ~15u;
+    const uint32_t cap = (uint32_t)std::min<size_t>(K, (size_t)kWtLoads * 1024 / p.Bs);
+    if (cap == 0) return p;
+    // prefer chunks that are whole 128-B lines (e.g. 8 x 1440 B = 90 lines), else the largest
+    uint32_t js = cap;
+    for (uint32_t j = cap; j >= 1; --j)
+        if ((j * p.Bs) % 128 == 0 && 2 * j >= cap) {
+            js = j;
+            break;
+        }
+    p.JS = js;
+    p.nch = (K + js - 1) / js;
+    p.lds = ((size_t)js * p.Bs + 15) / 16 * 16 + (size_t)K * tbl;
+    p.ok = p.lds <= 64 * 1024;
+    return p;
+}
+
+template <int MT, bool DEC>
+static int run_wave(const DeviceInfo &di, WtArgs a, const WtPlan &p, hipStream_t s)
+{
+    a.JS = p.JS;
+    a.nch = p.nch;
+    a.Bs = p.Bs;
+    a.cols = (a.B + 15) / 16;
+    a.bs_inv = ((1ull << 32) + a.Bs - 1) / a.Bs;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)mac_wave_kernel<MT, DEC>, 64, p.lds) !=
+            hipSuccess || occ <= 0)
+        occ = 1;
+    const uint32_t gx = std::max(1u, std::min<uint32_t>(a.G, (uint32_t)std::max(1, di.cus * std::min(occ, 32))));
+    hipLaunchKernelGGL((mac_wave_kernel<MT, DEC>), dim3(gx), dim3(64), p.lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <bool DEC>
+static int dispatch_wave(const DeviceInfo &di, WtArgs a, const WtPlan &p, int mt, hipStream_t s)
+{
+    switch (mt) {
+    case 1: return run_wave<1, DEC>(di, a, p, s);
+    case 2: return run_wave<2, DEC>(di, a, p, s);
+    case 3: return run_wave<3, DEC>(di, a, p, s);
+    case 4: return run_wave<4, DEC>(di, a, p, s);
+    default: return run_wave<8, DEC>(di, a, p, s);
+    }
+}
+
+static bool wave_enabled()
+{
+    static const bool on = [] {
+        const char *e = getenv("KFEC_KERNEL");
+        return e && std::string(e) == "wave";
+    }();
+    return on;
+}
+
 // ---- stream engine launch ----
 static constexpr size_t kEngLdsMax = 160 * 1024 - 1024;
 
@@ -1460,6 +1748,19 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
         return dispatch_tile<false>(di, pick_vec(pitch, {d_data, d_parity}), a, s);
     }
+    if (wave_enabled() && G < 0xFFFFFFFFull && pick_vec(pitch, {d_data, d_parity}) >= 16) {
+        const int mt = pick_mt(R);
+        const WtPlan p = plan_wave(K, R, (uint32_t)B, mt);
+        if (p.ok) {
+            WtArgs a{};
+            a.data = static_cast<const uint8_t *>(d_data);
+            a.out = static_cast<uint8_t *>(d_parity);
+            a.enc = d_enc;
+            a.pitch = pitch;
+            a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
+            return dispatch_wave<false>(di, a, p, mt, s);
+        }
+    }
     if (stream_enabled() && G < 0xFFFFFFFFull && pick_vec(pitch, {d_data, d_parity}) >= 16) {
         const int mt = pick_mt(R);
         const EngPlan p = plan_stream(K, R, (uint32_t)B, mt, false);
@@ -1545,6 +1846,22 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
         a.rec_stride = (uint32_t)rs;
         return dispatch_tile<true>(di, pick_vec(pitch, {d_data, d_parity, d_out}), a, s);
+    }
+    if (wave_enabled() && G < 0xFFFFFFFFull && pick_vec(pitch, {d_data, d_parity, d_out}) >= 16) {
+        const int mt = pick_mt(R);
+        const WtPlan p = plan_wave(K, R, (uint32_t)B, mt);
+        if (p.ok) {
+            WtArgs a{};
+            a.data = static_cast<const uint8_t *>(d_data);
+            a.parity = static_cast<const uint8_t *>(d_parity);
+            a.out = static_cast<uint8_t *>(d_out);
+            a.enc = d_enc;
+            a.rec = rec;
+            a.pitch = pitch;
+            a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
+            a.rec_stride = (uint32_t)rs;
+            return dispatch_wave<true>(di, a, p, mt, s);
+        }
     }
     if (stream_enabled() && G < 0xFFFFFFFFull && pick_vec(pitch, {d_data, d_parity, d_out}) >= 16) {
         const int mt = pick_mt(R);
