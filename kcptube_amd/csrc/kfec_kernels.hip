@@ -63,9 +63,6 @@ static constexpr int kBlock = 256;
 #ifndef KFEC_VEC32
 #define KFEC_VEC32 1  // 32-byte lane granules in the flattened kernel (2 KiB per wave-instruction pair)
 #endif
-#ifndef KFEC_ROT
-#define KFEC_ROT 0  // rotate odd waves' shard order by half a chunk (line-sharing in L2, see mac_kernel)
-#endif
 #ifndef KFEC_MINW
 #define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the flattened kernel
 #endif
@@ -105,6 +102,24 @@ __device__ __forceinline__ uint64_t bits_below(int n, int q)
 {
     const int v = n - 64 * q;
     return v <= 0 ? 0ull : (v >= 64 ? ~0ull : ((1ull << v) - 1ull));
+}
+
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor_b32 otherwise
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// acc ^ c * x for 4 bytes, c given by its 5 permute tables (kfec_gf.hpp gf_perm_tables):
+// three v_perm_b32 lookups (bits 0-2, 3-5, 6-7 of every byte) and two XORs
+__device__ __forceinline__ uint32_t perm_mac(uint32_t acc, const uint32_t *t, uint32_t s0, uint32_t s1, uint32_t s2)
+{
+    const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], s0);
+    const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], s1);
+    const uint32_t p2 = __builtin_amdgcn_perm(t[4], t[4], s2);
+    return xor3(acc, p0, p1) ^ p2;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -343,18 +358,32 @@ __global__ void __launch_bounds__(kBlock) decode_prep_small(PrepArgs a)
     }
 }
 
-// General m (up to min(K, R) <= 128): one wave per group, lanes over matrix elements.
+// General m (up to min(K, R) <= 128): one wave per group.  All row arithmetic uses the perm MAC on
+// packed dwords (4 bytes per op), not per-byte log/antilog lookups:
+//   Gauss-Jordan on A = [S | I] (m rows of W4 dwords): per pivot c, lanes build the permute tables of
+//   1/piv and of every row's factor A[r][c]; then lanes over (row, dword) items do A[r] ^= f_r * A[c].
+//   coef = Sinv * E_P: lanes over (u, dword) items accumulate Sinv[u][t] * E[P_t] in LDS, one t at a time.
+__device__ __forceinline__ uint32_t pm_apply(uint32_t acc, const uint32_t *t, uint32_t x)
+{
+    return perm_mac(acc, t, x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u);
+}
+
 __global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int K = a.K, N = a.N, R = a.R;
+    const int K = a.K, N = a.N, R = a.R, lane = threadIdx.x;
+    const int K4 = (K + 3) & ~3, W4 = (2 * MMAX + 3) / 4;  // augmented row: 2m bytes -> W4 dwords
     uint8_t *s_exp = smem, *s_log = smem + 512;
-    uint8_t *s_M = smem + 768, *s_P = s_M + 256, *s_rank = s_P + 256, *s_f = s_rank + 256;  // 4 x 256
-    uint8_t *s_E = s_f + 256;                                                              // R x K
-    uint8_t *s_A = s_E + ((R * K + 15) & ~15);                                             // MMAX x 2*MMAX
-    const int lane = threadIdx.x;
+    uint8_t *s_M = smem + 768, *s_P = s_M + 256, *s_rank = s_P + 256;   // 3 x 256 bytes
+    uint32_t *s_T = reinterpret_cast<uint32_t *>(smem + 1536);          // 128 coefficient tables x 5 dwords
+    uint8_t *s_E = smem + 1536 + 128 * 20;                               // parity rows R x K4 (zero padded)
+    uint32_t *s_A = reinterpret_cast<uint32_t *>(s_E + R * K4);          // MMAX rows x W4 dwords
+    uint32_t *s_C = s_A + MMAX * W4;                                     // MMAX rows x K4/4 dwords
     stage_gf(s_exp, s_log);
-    for (int i = lane; i < R * K; i += 64) s_E[i] = a.enc[K * K + i];
+    for (int i = lane; i < R * K4; i += 64) {
+        const int r = i / K4, j = i - r * K4;
+        s_E[i] = j < K ? a.enc[(K + r) * K + j] : 0;
+    }
     __syncthreads();
 
     for (uint64_t g = blockIdx.x; g < a.G; g += gridDim.x) {
@@ -375,21 +404,19 @@ __global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
                 a.status[g] = 1;
             }
             for (int t = lane; t < R; t += 64) a.out_idx[g * R + t] = 0xFF;
-            __syncthreads();
             continue;
         }
-        // missing data ids ascending, and their ranks
+        // missing data ids ascending (and their ranks), highest present ids descending
         int base = 0;
         for (int q = 0; q < 4; ++q) {
             const bool f = (dm[q] >> lane) & 1ull;
-            const uint64_t below = __popcll(dm[q] & ((1ull << lane) - 1ull));
+            const int below = __popcll(dm[q] & ((1ull << lane) - 1ull));
             if (f) {
                 s_M[base + below] = (uint8_t)(q * 64 + lane);
                 s_rank[q * 64 + lane] = (uint8_t)(base + below);
             }
             base += __popcll(dm[q]);
         }
-        // highest present ids, descending
         base = 0;
         for (int q = 3; q >= 0; --q) {
             const bool f = (w[q] >> lane) & 1ull;
@@ -398,26 +425,44 @@ __global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
             base += __popcll(w[q]);
         }
         __syncthreads();
-        const int W2 = 2 * m;
-        for (int e = lane; e < m * W2; e += 64) {
-            const int t = e / W2, c = e - t * W2;
-            s_A[t * W2 + c] = (c < m) ? s_E[(s_P[t] - K) * K + s_M[c]] : (uint8_t)((c - m) == t);
+        const int w4 = (2 * m + 3) / 4;  // dwords per augmented row for this m
+        // A = [S | I]: S[t][u] = enc[P_t][M_u]
+        for (int e = lane; e < m * w4; e += 64) {
+            const int t = e / w4, d = e - t * w4;
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int col = 4 * d + b;
+                uint32_t x = 0;
+                if (col < m) x = s_E[(s_P[t] - K) * K4 + s_M[col]];
+                else if (col < 2 * m) x = (col - m == t);
+                v |= x << (8 * b);
+            }
+            s_A[t * W4 + d] = v;
         }
         __syncthreads();
         bool singular = false;
         for (int c = 0; c < m; ++c) {
-            const uint32_t piv = s_A[c * W2 + c];
+            const uint32_t piv = reinterpret_cast<const uint8_t *>(s_A + c * W4)[c];
             singular |= (piv == 0);
-            const uint32_t inv = ginv(s_exp, s_log, piv);
+            // normalize the pivot row (every lane builds the tables of 1/piv itself)
+            {
+                uint32_t ti[5];
+                gf_perm_tables(ginv(s_exp, s_log, piv), ti);
+                for (int d = lane; d < w4; d += 64) s_A[c * W4 + d] = pm_apply(0u, ti, s_A[c * W4 + d]);
+            }
+            // tables of each row's factor A[r][c] (0 for the pivot row itself)
+            for (int r = lane; r < m; r += 64) {
+                uint32_t tr[5];
+                gf_perm_tables(r == c ? 0u : reinterpret_cast<const uint8_t *>(s_A + r * W4)[c], tr);
+#pragma unroll
+                for (int i = 0; i < 5; ++i) s_T[r * 5 + i] = tr[i];
+            }
             __syncthreads();
-            for (int col = lane; col < W2; col += 64) s_A[c * W2 + col] = (uint8_t)gmul(s_exp, s_log, s_A[c * W2 + col], inv);
-            for (int r = lane; r < m; r += 64) s_f[r] = s_A[r * W2 + c];
-            __syncthreads();
-            for (int e = lane; e < m * W2; e += 64) {
-                const int r = e / W2, col = e - r * W2;
+            for (int e = lane; e < m * w4; e += 64) {
+                const int r = e / w4, d = e - r * w4;
                 if (r == c) continue;
-                const uint32_t f = s_f[r];
-                if (f) s_A[e] ^= (uint8_t)gmul(s_exp, s_log, f, s_A[c * W2 + col]);
+                s_A[r * W4 + d] = pm_apply(s_A[r * W4 + d], s_T + r * 5, s_A[c * W4 + d]);
             }
             __syncthreads();
         }
@@ -428,25 +473,53 @@ __global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
                 a.status[g] = 2;
             }
             for (int t = lane; t < R; t += 64) a.out_idx[g * R + t] = 0xFF;
-            __syncthreads();
             continue;
         }
-        const int K4 = (K + 3) & ~3;
-        uint8_t *src = rec + 4, *coef = rec + 4 + K4;
-        for (int j = lane; j < K; j += 64) {
-            const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
-            src[j] = miss ? s_P[s_rank[j]] : (uint8_t)j;
-        }
-        for (int e = lane; e < m * K; e += 64) {
-            const int u = e / K, j = e - u * K;
-            const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
-            uint32_t v = 0;
-            if (miss) {
-                v = s_A[u * W2 + m + s_rank[j]];
-            } else {
-                for (int t = 0; t < m; ++t) v ^= gmul(s_exp, s_log, s_A[u * W2 + m + t], s_E[(s_P[t] - K) * K + j]);
+        // coef[u][k] = XOR_t Sinv[u][t] * E[P_t][k] for present k; Sinv[u][t] on column M_t
+        const int kd = K4 / 4;
+        for (int e = lane; e < m * kd; e += 64) s_C[e] = 0;
+        for (int t = 0; t < m; ++t) {
+            __syncthreads();
+            for (int u = lane; u < m; u += 64) {
+                uint32_t tt[5];
+                gf_perm_tables(reinterpret_cast<const uint8_t *>(s_A + u * W4)[m + t], tt);
+#pragma unroll
+                for (int i = 0; i < 5; ++i) s_T[u * 5 + i] = tt[i];
             }
-            coef[u * K4 + j] = (uint8_t)v;
+            __syncthreads();
+            const uint32_t *erow = reinterpret_cast<const uint32_t *>(s_E + (s_P[t] - K) * K4);
+            for (int e = lane; e < m * kd; e += 64) {
+                const int u = e / kd, d = e - u * kd;
+                s_C[e] = pm_apply(s_C[e], s_T + u * 5, erow[d]);
+            }
+        }
+        __syncthreads();
+        // missing columns carry Sinv[u][rank] instead; write the record as whole dwords
+        uint32_t *srcw = reinterpret_cast<uint32_t *>(rec + 4);
+        uint32_t *coefw = reinterpret_cast<uint32_t *>(rec + 4 + K4);
+        for (int d = lane; d < kd; d += 64) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int j = 4 * d + b;
+                if (j >= K) break;
+                const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
+                v |= (uint32_t)(miss ? s_P[s_rank[j]] : j) << (8 * b);
+            }
+            srcw[d] = v;
+        }
+        for (int e = lane; e < m * kd; e += 64) {
+            const int u = e / kd, d = e - u * kd;
+            uint32_t v = s_C[e];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int j = 4 * d + b;
+                if (j < K && ((dm[j >> 6] >> (j & 63)) & 1ull)) {
+                    const uint32_t sv = reinterpret_cast<const uint8_t *>(s_A + u * W4)[m + s_rank[j]];
+                    v = (v & ~(0xFFu << (8 * b))) | (sv << (8 * b));
+                }
+            }
+            coefw[u * kd + d] = v;
         }
         for (int t = lane; t < R; t += 64) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
         if (lane == 0) {
@@ -476,6 +549,7 @@ struct MacArgs {
     uint32_t rec_stride;
     uint32_t JC;            // shards per LDS chunk
     uint32_t gmax;          // group slots per chunk
+    uint32_t order;         // shard visiting order: bit 0 interleave (see mac_kernel), bits 8.. odd-wave lag
 };
 
 template <int VEC>
@@ -534,24 +608,6 @@ __device__ __forceinline__ void store_gran(uint8_t *p, const uint32_t *d, uint32
         for (int b = 0; b < 4; ++b)
             if (b0 + b < B) p[b] = (uint8_t)(d[0] >> (8 * b));
     }
-}
-
-// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor_b32 otherwise
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
-{
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-
-// acc ^ c * x for 4 bytes, c given by its 5 permute tables (kfec_gf.hpp gf_perm_tables):
-// three v_perm_b32 lookups (bits 0-2, 3-5, 6-7 of every byte) and two XORs
-__device__ __forceinline__ uint32_t perm_mac(uint32_t acc, const uint32_t *t, uint32_t s0, uint32_t s1, uint32_t s2)
-{
-    const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], s0);
-    const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], s1);
-    const uint32_t p2 = __builtin_amdgcn_perm(t[4], t[4], s2);
-    return xor3(acc, p0, p1) ^ p2;
 }
 
 template <int MT>
@@ -649,13 +705,22 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
             }
             if (rows == 0) continue;
             const uint8_t *ent0 = s_ent + (gs * a.JC) * L::ENTRY;
-            // odd waves walk the chunk's shards rotated by nj/2: a 128-B line shared by two neighbouring
-            // waves (or by the tail of one shard and the head of the next) is then requested ~nj/2
-            // iterations apart, after the first request has filled the L2, instead of as a second miss
-            const uint32_t rot = (KFEC_ROT && ((threadIdx.x >> 6) & 1u)) ? nj / 2 : 0u;
+            // Shard visiting order.  A 128-B line straddling shards j and j+1 (3 of every 4 boundaries at
+            // B = 1440) is requested twice; the L2 does not merge a request with an in-flight miss of the
+            // same line, so both go to DRAM when j and j+1 are issued back to back.  Interleaving (order
+            // bit 0) visits each block of 2*PD shards odd-first ([1,3,..,0,2,..]): neighbours are then >= PD
+            // positions apart, i.e. the second request is issued after the first has landed and hits L2.
+            // Bits 8.. lag odd waves by that many positions (lines split between two waves).
+            const uint32_t lag = ((threadIdx.x >> 6) & 1u) ? (a.order >> 8) % nj : 0u;
+            const uint32_t nblk = (a.order & 1u) ? nj & ~(2u * PD - 1u) : 0u;
             auto sj = [&](uint32_t jj) -> uint32_t {
-                const uint32_t j = jj + rot;
-                return j >= nj ? j - nj : j;
+                uint32_t p = jj + lag;
+                p = p >= nj ? p - nj : p;
+                if (p < nblk) {
+                    const uint32_t q = p & (2u * PD - 1u);
+                    p = (p - q) + (q < (uint32_t)PD ? 2u * q + 1u : 2u * (q - PD));
+                }
+                return p;
             };
             auto share_ptr = [&](uint32_t jj) -> const uint8_t * {
                 const uint32_t j = sj(jj);
@@ -1440,11 +1505,25 @@ static int pick_vec(size_t pitch, std::initializer_list<const void *> ptrs)
 
 // resident 256-thread blocks per CU for a kernel (occupancy API, capped at 8: MI355X_MICROARCH.md
 // "Residency": the API can over-report by one for SGPR-heavy kernels; ours stay below 80 SGPRs)
+static int env_int(const char *name, int dflt)
+{
+    const char *e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+
+// shard visiting order of mac_kernel (MacArgs::order); KFEC_ORDER overrides for experiments
+static uint32_t mac_order()
+{
+    static const uint32_t o = (uint32_t)env_int("KFEC_ORDER", 0);
+    return o;
+}
+
 static int resident_blocks(const void *kernel, size_t lds)
 {
+    static const int cap = std::max(1, std::min(8, env_int("KFEC_BLOCKS", 8)));
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, kBlock, lds) != hipSuccess || n <= 0) n = 1;
-    return std::min(n, 8);
+    return std::min(n, cap);
 }
 
 static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
@@ -1468,8 +1547,12 @@ static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
     // persistent grid sized to what is resident at once: a grid one block per CU larger than that
     // leaves a tail in which a single block per CU runs alone (measured: +45% kernel time)
     const uint32_t want = (a.total + kBlock - 1) / kBlock;
-    const uint32_t cap = (uint32_t)(std::max(1, di.cus) * resident_blocks((const void *)mac_kernel<VEC, MT, DEC>, lds))
-                         / (uint32_t)std::max(1, tiles);
+    uint32_t cap = (uint32_t)(std::max(1, di.cus) * resident_blocks((const void *)mac_kernel<VEC, MT, DEC>, lds))
+                   / (uint32_t)std::max(1, tiles);
+    // with several row tiles, keep gridDim.x a multiple of the 8 XCDs: workgroups (x, y) and (x, y') then
+    // share an XCD (dispatch is round-robin over XCDs in linear block order), so the tiles' re-reads of
+    // the same shard bytes hit that XCD's L2
+    if (tiles > 1 && cap >= 8) cap &= ~7u;
     const uint32_t gx = std::max(1u, std::min(want, std::max(cap, 1u)));
     hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC>), dim3(gx, tiles), dim3(kBlock), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
@@ -1798,6 +1881,7 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.rec_stride = 0;
         a.JC = JC;
         a.gmax = 1;
+        a.order = mac_order();
         return dispatch_mac<false>(di, vec, mt, a, tiles, s);
     });
 }
@@ -1829,8 +1913,20 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         if (mmax <= 4) hipLaunchKernelGGL((decode_prep_small<4>), dim3(blocks), dim3(kBlock), lds, s, p);
         else hipLaunchKernelGGL((decode_prep_small<8>), dim3(blocks), dim3(kBlock), lds, s, p);
     } else {
-        const size_t lds = 768 + 4 * 256 + (((size_t)R * K + 15) & ~size_t(15)) + (size_t)mmax * 2 * mmax;
-        const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>(G, (size_t)std::max(di.cus, 1) * 16));
+        const size_t K4 = (K + 3) & ~size_t(3), W4 = (2 * (size_t)mmax + 3) / 4;
+        const size_t lds = 1536 + 128 * 20 + (size_t)R * K4 + (size_t)mmax * W4 * 4 + (size_t)mmax * K4;
+        static bool attr = false;  // up to ~67 KB for R = K = 128
+        if (!attr) {
+            if (hipFuncSetAttribute((const void *)decode_prep_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    96 * 1024) != hipSuccess)
+                return -3;
+            attr = true;
+        }
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)decode_prep_wave, 64, lds) != hipSuccess ||
+            occ <= 0)
+            occ = 1;
+        const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>(G, (size_t)std::max(di.cus, 1) * occ));
         hipLaunchKernelGGL(decode_prep_wave, dim3(blocks), dim3(64), lds, s, p, mmax);
     }
     if (hipGetLastError() != hipSuccess) return -3;
@@ -1905,6 +2001,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.rec_stride = (uint32_t)rs;
         a.JC = JC;
         a.gmax = gmax;
+        a.order = mac_order();
         return dispatch_mac<true>(di, vec, mt, a, tiles, s);
     });
 }
