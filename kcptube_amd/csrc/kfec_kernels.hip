@@ -182,28 +182,30 @@ struct PrepArgs {
     uint32_t rec_stride;
 };
 
+// (no early return: the unrolled q index stays a constant, so w[] lives in registers, not scratch)
 __device__ __forceinline__ int pop_lowest(uint64_t (&w)[4])
 {
+    int res = -1;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        if (w[q]) {
-            const int b = __ffsll((unsigned long long)w[q]) - 1;
+        if (res < 0 && w[q]) {
+            res = q * 64 + __ffsll((unsigned long long)w[q]) - 1;
             w[q] &= w[q] - 1;
-            return q * 64 + b;
         }
-    return -1;
+    return res;
 }
 
 __device__ __forceinline__ int pop_highest(uint64_t (&w)[4])
 {
+    int res = -1;
 #pragma unroll
     for (int q = 3; q >= 0; --q)
-        if (w[q]) {
+        if (res < 0 && w[q]) {
             const int b = 63 - __clzll((unsigned long long)w[q]);
             w[q] &= ~(1ull << b);
-            return q * 64 + b;
+            res = q * 64 + b;
         }
-    return -1;
+    return res;
 }
 
 __device__ __forceinline__ void write_empty(const PrepArgs &a, uint64_t g, uint8_t st)
@@ -358,29 +360,175 @@ __global__ void __launch_bounds__(kBlock) decode_prep_small(PrepArgs a)
     }
 }
 
-// General m (up to min(K, R) <= 128): one wave per group.  All row arithmetic uses the perm MAC on
-// packed dwords (4 bytes per op), not per-byte log/antilog lookups:
-//   Gauss-Jordan on A = [S | I] (m rows of W4 dwords): per pivot c, lanes build the permute tables of
-//   1/piv and of every row's factor A[r][c]; then lanes over (row, dword) items do A[r] ^= f_r * A[c].
-//   coef = Sinv * E_P: lanes over (u, dword) items accumulate Sinv[u][t] * E[P_t] in LDS, one t at a time.
+// acc ^ c * x for the 4 bytes of x (c given by its permute tables)
 __device__ __forceinline__ uint32_t pm_apply(uint32_t acc, const uint32_t *t, uint32_t x)
 {
     return perm_mac(acc, t, x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u);
 }
 
-__global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
+// m <= MAXM <= 4 (fec=20:3, 10:3, ...): one thread per group, all GF arithmetic on packed bytes with the
+// perm MAC instead of log/antilog lookups.  A row of [S | I] is one dword each for S and I (MAXM <= 4
+// bytes); Gauss-Jordan normalises and eliminates whole rows with one perm MAC per dword; the coefficient
+// product runs over dwords of the parity rows with the MAXM^2 tables of Sinv held in VGPRs.
+template <int MAXM>
+__global__ void __launch_bounds__(kBlock) decode_prep_perm(PrepArgs a)
+{
+    static_assert(MAXM >= 1 && MAXM <= 4, "rows are packed into one dword");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *s_exp = smem, *s_log = smem + 512, *s_E = smem + 768;  // s_E: parity rows, R x K4 (zero padded)
+    stage_gf(s_exp, s_log);
+    const int K = a.K, N = a.N, R = a.R, K4 = (K + 3) & ~3, kd = K4 / 4;
+    for (int i = threadIdx.x; i < R * K4; i += blockDim.x) {
+        const int r = i / K4, j = i - r * K4;
+        s_E[i] = j < K ? a.enc[(K + r) * K + j] : 0;
+    }
+    __syncthreads();
+    const uint32_t *s_E32 = reinterpret_cast<const uint32_t *>(s_E);
+
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < a.G;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t w[4], dm[4];
+        int cnt = 0, m = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            w[q] = a.present[g * 4 + q] & bits_below(N, q);
+            dm[q] = ~w[q] & bits_below(K, q);
+            cnt += __popcll(w[q]);
+            m += __popcll(dm[q]);
+        }
+        if (cnt < K || m > MAXM) {
+            write_empty(a, g, 1);
+            continue;
+        }
+        uint8_t *rec = a.rec + g * a.rec_stride;
+        int M[MAXM], P[MAXM];
+        uint64_t dmw[4] = {dm[0], dm[1], dm[2], dm[3]};
+        uint64_t pw[4] = {w[0], w[1], w[2], w[3]};
+#pragma unroll
+        for (int t = 0; t < MAXM; ++t) {
+            M[t] = (t < m) ? pop_lowest(dmw) : 0;
+            P[t] = (t < m) ? pop_highest(pw) : K;
+        }
+        // A[t] = row t of S (byte u = S[t][u]); identity beyond m.  Iv[t] = row t of the inverse.
+        uint32_t A[MAXM], Iv[MAXM];
+#pragma unroll
+        for (int t = 0; t < MAXM; ++t) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int u = 0; u < MAXM; ++u) {
+                const uint32_t x = (t < m && u < m) ? s_E[(P[t] - K) * K4 + M[u]] : (uint32_t)(t == u);
+                v |= x << (8 * u);
+            }
+            A[t] = v;
+            Iv[t] = 1u << (8 * t);
+        }
+        bool singular = false;
+#pragma unroll
+        for (int c = 0; c < MAXM; ++c) {
+            if (c < m) {
+                const uint32_t piv = (A[c] >> (8 * c)) & 0xFFu;
+                singular |= (piv == 0);
+                uint32_t tb[5];
+                gf_perm_tables(ginv(s_exp, s_log, piv), tb);
+                A[c] = pm_apply(0u, tb, A[c]);
+                Iv[c] = pm_apply(0u, tb, Iv[c]);
+#pragma unroll
+                for (int r = 0; r < MAXM; ++r) {
+                    if (r == c || r >= m) continue;
+                    gf_perm_tables((A[r] >> (8 * c)) & 0xFFu, tb);
+                    A[r] = pm_apply(A[r], tb, A[c]);
+                    Iv[r] = pm_apply(Iv[r], tb, Iv[c]);
+                }
+            }
+        }
+        if (singular) {
+            write_empty(a, g, 2);
+            continue;
+        }
+        rec[0] = 0;
+        rec[1] = (uint8_t)m;
+        rec[2] = rec[3] = 0;
+        // tables of Sinv[u][t] (zero beyond m, so those terms vanish)
+        uint32_t T[MAXM][MAXM][5];
+#pragma unroll
+        for (int u = 0; u < MAXM; ++u)
+#pragma unroll
+            for (int t = 0; t < MAXM; ++t) gf_perm_tables((u < m && t < m) ? (Iv[u] >> (8 * t)) & 0xFFu : 0u, T[u][t]);
+        uint32_t *srcw = reinterpret_cast<uint32_t *>(rec + 4);
+        uint32_t *coefw = reinterpret_cast<uint32_t *>(rec + 4 + K4);
+        for (int d = 0; d < kd; ++d) {
+            uint32_t x[MAXM];
+#pragma unroll
+            for (int t = 0; t < MAXM; ++t) x[t] = (t < m) ? s_E32[(P[t] - K) * kd + d] : 0u;
+            uint32_t cw[MAXM];
+#pragma unroll
+            for (int u = 0; u < MAXM; ++u) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int t = 0; t < MAXM; ++t) v = pm_apply(v, T[u][t], x[t]);
+                cw[u] = v;
+            }
+            // columns of missing shards: source = the parity share P_rank, coefficient Sinv[u][rank]
+            uint32_t sw = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int j = 4 * d + b;
+                uint32_t src = (uint32_t)j;
+#pragma unroll
+                for (int t = 0; t < MAXM; ++t)
+                    if (t < m && M[t] == j) {
+                        src = (uint32_t)P[t];
+#pragma unroll
+                        for (int u = 0; u < MAXM; ++u)
+                            cw[u] = (cw[u] & ~(0xFFu << (8 * b))) | (((Iv[u] >> (8 * t)) & 0xFFu) << (8 * b));
+                    }
+                sw |= (j < K ? src : 0u) << (8 * b);
+            }
+            srcw[d] = sw;
+#pragma unroll
+            for (int u = 0; u < MAXM; ++u)
+                if (u < m) coefw[u * kd + d] = cw[u];
+        }
+#pragma unroll
+        for (int t = 0; t < MAXM; ++t)
+            if (t < R) a.out_idx[g * R + t] = (t < m) ? (uint8_t)M[t] : (uint8_t)0xFF;
+        for (int t = MAXM; t < R; ++t) a.out_idx[g * R + t] = 0xFF;
+        a.status[g] = 0;
+    }
+}
+
+// General m (up to min(K, R) <= 128): one 256-thread workgroup per group.  All row arithmetic uses the
+// perm MAC on packed dwords (4 bytes per op), not per-byte log/antilog lookups:
+//   Gauss-Jordan on A = [S | I] (m rows of W4 dwords), one phase per pivot c: threads build the permute
+//   tables of each row's factor (A[r][c] / piv, or 1 / piv for the pivot row) and copy the pivot row;
+//   then threads over (row, dword) items do A[r] ^= f_r * A[c] (A[c] = f_c * A[c] for the pivot row).
+//   coef = Sinv * E_P: each thread owns fixed (u, dword) items with accumulators in VGPRs; the tables of
+//   Sinv[u][t] are built kTC columns t at a time.
+constexpr int kPrepThreads = 256;
+constexpr int kPrepTC = 8;                       // Sinv columns per table batch
+constexpr int kPrepAcc = 32;                     // dwords per thread: K4/4 <= 64 over >= 2 threads per row
+
+__device__ __forceinline__ void store_tables(uint32_t *dst, uint32_t c)
+{
+    uint32_t t[5];
+    gf_perm_tables(c, t);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) dst[i] = t[i];
+}
+
+__global__ void __launch_bounds__(kPrepThreads) decode_prep_wave(PrepArgs a, int MMAX)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int K = a.K, N = a.N, R = a.R, lane = threadIdx.x;
-    const int K4 = (K + 3) & ~3, W4 = (2 * MMAX + 3) / 4;  // augmented row: 2m bytes -> W4 dwords
+    const int K = a.K, N = a.N, R = a.R, tid = threadIdx.x, lane = tid & 63;
+    const int K4 = (K + 3) & ~3, kd = K4 / 4, W4 = (2 * MMAX + 3) / 4;  // augmented row: 2m bytes
     uint8_t *s_exp = smem, *s_log = smem + 512;
-    uint8_t *s_M = smem + 768, *s_P = s_M + 256, *s_rank = s_P + 256;   // 3 x 256 bytes
-    uint32_t *s_T = reinterpret_cast<uint32_t *>(smem + 1536);          // 128 coefficient tables x 5 dwords
-    uint8_t *s_E = smem + 1536 + 128 * 20;                               // parity rows R x K4 (zero padded)
-    uint32_t *s_A = reinterpret_cast<uint32_t *>(s_E + R * K4);          // MMAX rows x W4 dwords
-    uint32_t *s_C = s_A + MMAX * W4;                                     // MMAX rows x K4/4 dwords
+    uint8_t *s_M = smem + 768, *s_P = s_M + 256, *s_rank = s_P + 256;  // 3 x 256 bytes
+    uint32_t *s_T = reinterpret_cast<uint32_t *>(smem + 1536);         // 128 * kPrepTC tables x 5 dwords
+    uint32_t *s_row = s_T + 128 * kPrepTC * 5;                          // copy of the pivot row (64 dwords)
+    uint8_t *s_E = reinterpret_cast<uint8_t *>(s_row + 64);             // parity rows R x K4 (zero padded)
+    uint32_t *s_A = reinterpret_cast<uint32_t *>(s_E + R * K4);         // MMAX rows x W4 dwords
     stage_gf(s_exp, s_log);
-    for (int i = lane; i < R * K4; i += 64) {
+    for (int i = tid; i < R * K4; i += kPrepThreads) {
         const int r = i / K4, j = i - r * K4;
         s_E[i] = j < K ? a.enc[(K + r) * K + j] : 0;
     }
@@ -398,36 +546,38 @@ __global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
         }
         uint8_t *rec = a.rec + g * a.rec_stride;
         if (cnt < K || m > MMAX) {
-            if (lane == 0) {
+            if (tid == 0) {
                 rec[0] = 1;
                 rec[1] = 0;
                 a.status[g] = 1;
             }
-            for (int t = lane; t < R; t += 64) a.out_idx[g * R + t] = 0xFF;
+            for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = 0xFF;
             continue;
         }
-        // missing data ids ascending (and their ranks), highest present ids descending
-        int base = 0;
-        for (int q = 0; q < 4; ++q) {
-            const bool f = (dm[q] >> lane) & 1ull;
-            const int below = __popcll(dm[q] & ((1ull << lane) - 1ull));
-            if (f) {
-                s_M[base + below] = (uint8_t)(q * 64 + lane);
-                s_rank[q * 64 + lane] = (uint8_t)(base + below);
+        // wave 0: missing data ids ascending (and their ranks), highest present ids descending
+        if (tid < 64) {
+            int base = 0;
+            for (int q = 0; q < 4; ++q) {
+                const bool f = (dm[q] >> lane) & 1ull;
+                const int below = __popcll(dm[q] & ((1ull << lane) - 1ull));
+                if (f) {
+                    s_M[base + below] = (uint8_t)(q * 64 + lane);
+                    s_rank[q * 64 + lane] = (uint8_t)(base + below);
+                }
+                base += __popcll(dm[q]);
             }
-            base += __popcll(dm[q]);
-        }
-        base = 0;
-        for (int q = 3; q >= 0; --q) {
-            const bool f = (w[q] >> lane) & 1ull;
-            const int above = __popcll(lane == 63 ? 0ull : (w[q] & ~((2ull << lane) - 1ull)));
-            if (f && base + above < m) s_P[base + above] = (uint8_t)(q * 64 + lane);
-            base += __popcll(w[q]);
+            base = 0;
+            for (int q = 3; q >= 0; --q) {
+                const bool f = (w[q] >> lane) & 1ull;
+                const int above = __popcll(lane == 63 ? 0ull : (w[q] & ~((2ull << lane) - 1ull)));
+                if (f && base + above < m) s_P[base + above] = (uint8_t)(q * 64 + lane);
+                base += __popcll(w[q]);
+            }
         }
         __syncthreads();
         const int w4 = (2 * m + 3) / 4;  // dwords per augmented row for this m
         // A = [S | I]: S[t][u] = enc[P_t][M_u]
-        for (int e = lane; e < m * w4; e += 64) {
+        for (int e = tid; e < m * w4; e += kPrepThreads) {
             const int t = e / w4, d = e - t * w4;
             uint32_t v = 0;
 #pragma unroll
@@ -445,59 +595,62 @@ __global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
         for (int c = 0; c < m; ++c) {
             const uint32_t piv = reinterpret_cast<const uint8_t *>(s_A + c * W4)[c];
             singular |= (piv == 0);
-            // normalize the pivot row (every lane builds the tables of 1/piv itself)
-            {
-                uint32_t ti[5];
-                gf_perm_tables(ginv(s_exp, s_log, piv), ti);
-                for (int d = lane; d < w4; d += 64) s_A[c * W4 + d] = pm_apply(0u, ti, s_A[c * W4 + d]);
+            const uint32_t inv = ginv(s_exp, s_log, piv);
+            for (int r = tid; r < m; r += kPrepThreads) {
+                const uint32_t f = r == c ? inv : gmul(s_exp, s_log, reinterpret_cast<const uint8_t *>(s_A + r * W4)[c], inv);
+                store_tables(s_T + r * 5, f);
             }
-            // tables of each row's factor A[r][c] (0 for the pivot row itself)
-            for (int r = lane; r < m; r += 64) {
-                uint32_t tr[5];
-                gf_perm_tables(r == c ? 0u : reinterpret_cast<const uint8_t *>(s_A + r * W4)[c], tr);
-#pragma unroll
-                for (int i = 0; i < 5; ++i) s_T[r * 5 + i] = tr[i];
-            }
+            for (int d = tid; d < w4; d += kPrepThreads) s_row[d] = s_A[c * W4 + d];
             __syncthreads();
-            for (int e = lane; e < m * w4; e += 64) {
+            for (int e = tid; e < m * w4; e += kPrepThreads) {
                 const int r = e / w4, d = e - r * w4;
-                if (r == c) continue;
-                s_A[r * W4 + d] = pm_apply(s_A[r * W4 + d], s_T + r * 5, s_A[c * W4 + d]);
+                s_A[r * W4 + d] = pm_apply(r == c ? 0u : s_A[r * W4 + d], s_T + r * 5, s_row[d]);
             }
             __syncthreads();
         }
         if (singular) {
-            if (lane == 0) {
+            if (tid == 0) {
                 rec[0] = 2;
                 rec[1] = 0;
                 a.status[g] = 2;
             }
-            for (int t = lane; t < R; t += 64) a.out_idx[g * R + t] = 0xFF;
+            for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = 0xFF;
             continue;
         }
-        // coef[u][k] = XOR_t Sinv[u][t] * E[P_t][k] for present k; Sinv[u][t] on column M_t
-        const int kd = K4 / 4;
-        for (int e = lane; e < m * kd; e += 64) s_C[e] = 0;
-        for (int t = 0; t < m; ++t) {
-            __syncthreads();
-            for (int u = lane; u < m; u += 64) {
-                uint32_t tt[5];
-                gf_perm_tables(reinterpret_cast<const uint8_t *>(s_A + u * W4)[m + t], tt);
+        // coef[u][k] = XOR_t Sinv[u][t] * E[P_t][k] for present k.  tpr threads per row u (power of two,
+        // m * tpr <= 256); thread (u, sub) owns dwords d = sub + tpr * i with accumulators in VGPRs, so the
+        // tables of Sinv[u][t] are read once per thread and t
+        const int tpr = m <= 32 ? 8 : (m <= 64 ? 4 : 2);
+        const int u = tid / tpr, sub = tid - u * tpr;
+        uint32_t acc[kPrepAcc];
 #pragma unroll
-                for (int i = 0; i < 5; ++i) s_T[u * 5 + i] = tt[i];
+        for (int i = 0; i < kPrepAcc; ++i) acc[i] = 0;
+        for (int t0 = 0; t0 < m; t0 += kPrepTC) {
+            const int tn = min(kPrepTC, m - t0);
+            for (int e = tid; e < m * tn; e += kPrepThreads) {
+                const int uu = e / tn, tt = e - uu * tn;
+                store_tables(s_T + (uu * kPrepTC + tt) * 5, reinterpret_cast<const uint8_t *>(s_A + uu * W4)[m + t0 + tt]);
             }
             __syncthreads();
-            const uint32_t *erow = reinterpret_cast<const uint32_t *>(s_E + (s_P[t] - K) * K4);
-            for (int e = lane; e < m * kd; e += 64) {
-                const int u = e / kd, d = e - u * kd;
-                s_C[e] = pm_apply(s_C[e], s_T + u * 5, erow[d]);
+            if (u < m) {
+                for (int tt = 0; tt < tn; ++tt) {
+                    uint32_t tb[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) tb[i] = s_T[(u * kPrepTC + tt) * 5 + i];
+                    const uint32_t *erow = reinterpret_cast<const uint32_t *>(s_E + (s_P[t0 + tt] - K) * K4);
+#pragma unroll
+                    for (int i = 0; i < kPrepAcc; ++i) {
+                        const int d = sub + tpr * i;
+                        if (d < kd) acc[i] = pm_apply(acc[i], tb, erow[d]);
+                    }
+                }
             }
+            __syncthreads();
         }
-        __syncthreads();
         // missing columns carry Sinv[u][rank] instead; write the record as whole dwords
         uint32_t *srcw = reinterpret_cast<uint32_t *>(rec + 4);
         uint32_t *coefw = reinterpret_cast<uint32_t *>(rec + 4 + K4);
-        for (int d = lane; d < kd; d += 64) {
+        for (int d = tid; d < kd; d += kPrepThreads) {
             uint32_t v = 0;
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
@@ -508,21 +661,26 @@ __global__ void __launch_bounds__(64) decode_prep_wave(PrepArgs a, int MMAX)
             }
             srcw[d] = v;
         }
-        for (int e = lane; e < m * kd; e += 64) {
-            const int u = e / kd, d = e - u * kd;
-            uint32_t v = s_C[e];
+        if (u < m) {
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int j = 4 * d + b;
-                if (j < K && ((dm[j >> 6] >> (j & 63)) & 1ull)) {
-                    const uint32_t sv = reinterpret_cast<const uint8_t *>(s_A + u * W4)[m + s_rank[j]];
-                    v = (v & ~(0xFFu << (8 * b))) | (sv << (8 * b));
+            for (int i = 0; i < kPrepAcc; ++i) {
+                const int d = sub + tpr * i;
+                if (d < kd) {
+                    uint32_t v = acc[i];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const int j = 4 * d + b;
+                        if (j < K && ((dm[j >> 6] >> (j & 63)) & 1ull)) {
+                            const uint32_t sv = reinterpret_cast<const uint8_t *>(s_A + u * W4)[m + s_rank[j]];
+                            v = (v & ~(0xFFu << (8 * b))) | (sv << (8 * b));
+                        }
+                    }
+                    coefw[u * kd + d] = v;
                 }
             }
-            coefw[u * kd + d] = v;
         }
-        for (int t = lane; t < R; t += 64) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
-        if (lane == 0) {
+        for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
+        if (tid == 0) {
             rec[0] = 0;
             rec[1] = (uint8_t)m;
             rec[2] = rec[3] = 0;
@@ -612,8 +770,10 @@ __device__ __forceinline__ void store_gran(uint8_t *p, const uint32_t *d, uint32
 
 template <int MT>
 struct MacLayout {
-    static constexpr int TBL_DW = ((5 * MT + 3) / 4) * 4;  // table dwords per (group, shard)
-    static constexpr int ENTRY = 16 + 4 * TBL_DW;          // + 8-byte share pointer, 8 pad
+    // per (group, shard): 8-byte share pointer + 8 pad, then t0..t3 of row r at 16 * r (one ds_read_b128),
+    // then t4 of every row (MT dwords, padded to 16 B)
+    static constexpr int T4OFF = 16 + 16 * MT;
+    static constexpr int ENTRY = T4OFF + ((4 * MT + 15) / 16) * 16;
 };
 
 // expand coefficients of shards [c0, c0+nj) for group slots [0, ng) into LDS entries
@@ -646,9 +806,8 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
         }
         uint32_t t[5];
         gf_perm_tables(c, t);
-        uint32_t *tp = reinterpret_cast<uint32_t *>(ent + 16) + 5 * r;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) tp[i] = t[i];
+        *reinterpret_cast<uint4 *>(ent + 16 + 16 * r) = make_uint4(t[0], t[1], t[2], t[3]);
+        reinterpret_cast<uint32_t *>(ent + L::T4OFF)[r] = t[4];
     }
 }
 
@@ -741,27 +900,28 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
                     if (jj < nj) {
                         const Gran<VEC> cur = x[u];
                         if (jj + PD < nj) x[u] = load_gran<VEC>(share_ptr(jj + PD), col, a.B);
-                        uint32_t t[L::TBL_DW];
-                        const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + sj(jj) * L::ENTRY + 16);
-#pragma unroll
-                        for (int i = 0; i < L::TBL_DW / 4; ++i) {
-                            const uint4 q = tv[i];
-                            t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
-                        }
+                        const uint8_t *ent = ent0 + sj(jj) * L::ENTRY;
+                        uint32_t s0[W], s1[W], s2[W];
 #pragma unroll
                         for (int w = 0; w < W; ++w) {
                             const uint32_t xv = cur.d[w];
-                            const uint32_t s0 = xv & 0x07070707u;
-                            const uint32_t s1 = (xv >> 3) & 0x07070707u;
-                            const uint32_t s2 = (xv >> 6) & 0x03030303u;
+                            s0[w] = xv & 0x07070707u;
+                            s1[w] = (xv >> 3) & 0x07070707u;
+                            s2[w] = (xv >> 6) & 0x03030303u;
+                        }
+#pragma unroll
+                        for (int r = 0; r < MT; ++r) {
+                            const uint4 q = *reinterpret_cast<const uint4 *>(ent + 16 + 16 * r);
+                            const uint32_t t[5] = {q.x, q.y, q.z, q.w,
+                                                   reinterpret_cast<const uint32_t *>(ent + L::T4OFF)[r]};
+#pragma unroll
+                            for (int w = 0; w < W; ++w) {
 #if KFEC_ABLATE == 1  // timing-only build: memory traffic of the real kernel, XOR instead of the GF MAC
-#pragma unroll
-                            for (int r = 0; r < MT; ++r) acc[r][w] ^= xv ^ t[5 * r];
-                            (void)s0; (void)s1; (void)s2;
+                                acc[r][w] ^= cur.d[w] ^ t[0];
 #else
-#pragma unroll
-                            for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+                                acc[r][w] = perm_mac(acc[r][w], t, s0[w], s1[w], s2[w]);
 #endif
+                            }
                         }
                     }
                 }
@@ -1528,6 +1688,21 @@ static int resident_blocks(const void *kernel, size_t lds)
 
 static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
 
+// (granule bytes, output rows per tile) of the flattened kernel.  Accumulators take MT * VEC/4 VGPRs;
+// keeping that at <= 64 lets a larger R use taller row tiles on narrower granules, so each input byte
+// is read by fewer tiles (200:55: 7 tiles of 8 rows -> 2 of 32).  KFEC_MT / KFEC_VEC override.
+static void mac_shape(int R, int vec_max, int &vec, int &mt)
+{
+    static const int mt_env = env_int("KFEC_MT", 0), vec_env = env_int("KFEC_VEC", 0);
+    if (R <= 4) mt = std::max(R, 1), vec = vec_max;
+    else if (R <= 8) mt = 8, vec = std::min(vec_max, 32);
+    else if (R <= 16) mt = 16, vec = std::min(vec_max, 16);
+    else mt = 32, vec = std::min(vec_max, 8);
+    if (mt_env == 1 || mt_env == 2 || mt_env == 3 || mt_env == 4 || mt_env == 8 || mt_env == 16 || mt_env == 32)
+        mt = mt_env;
+    if (vec_env > 0 && vec_env < vec && (vec_env & (vec_env - 1)) == 0) vec = vec_env;
+}
+
 // KFEC_PAD=1: pad a group's items to whole waves, so one wave-instruction reads a whole shard row and
 // both halves of every 128-B line that straddles two shards are read by consecutive instructions
 static size_t pad_cols(size_t cols)
@@ -1567,7 +1742,9 @@ static int dispatch_mac(const DeviceInfo &di, int vec, int mt, MacArgs a, int ti
     case 2: return run_mac<V, 2, DEC>(di, a, tiles, s);                      \
     case 3: return run_mac<V, 3, DEC>(di, a, tiles, s);                      \
     case 4: return run_mac<V, 4, DEC>(di, a, tiles, s);                      \
-    default: return run_mac<V, 8, DEC>(di, a, tiles, s);                     \
+    case 8: return run_mac<V, 8, DEC>(di, a, tiles, s);                      \
+    case 16: return run_mac<V, 16, DEC>(di, a, tiles, s);                    \
+    default: return run_mac<V, 32, DEC>(di, a, tiles, s);                    \
     }
     switch (vec) {
 #if KFEC_VEC32
@@ -1588,7 +1765,9 @@ static int entry_bytes(int mt)
     case 2: return MacLayout<2>::ENTRY;
     case 3: return MacLayout<3>::ENTRY;
     case 4: return MacLayout<4>::ENTRY;
-    default: return MacLayout<8>::ENTRY;
+    case 8: return MacLayout<8>::ENTRY;
+    case 16: return MacLayout<16>::ENTRY;
+    default: return MacLayout<32>::ENTRY;
     }
 }
 
@@ -1858,10 +2037,10 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
             return dispatch_stream<false>(di, a, p, mt, s);
         }
     }
-    const int vec = pick_vec(pitch, {d_data, d_parity});
+    int vec = 0, mt = 0;
+    mac_shape(R, pick_vec(pitch, {d_data, d_parity}), vec, mt);
     const int vb = vec >= 4 ? vec : 4;
     const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
-    const int mt = pick_mt(R);
     const int tiles = (R + mt - 1) / mt;
     const size_t ent = entry_bytes(mt);
     const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / ent));
@@ -1910,12 +2089,16 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         // by having many groups in flight, not by looping
         const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((G + kBlock - 1) / kBlock,
                                                                                 (size_t)std::max(di.cus, 1) * 64));
-        if (mmax <= 4) hipLaunchKernelGGL((decode_prep_small<4>), dim3(blocks), dim3(kBlock), lds, s, p);
+        const size_t lds4 = 768 + (size_t)R * (((size_t)K + 3) & ~size_t(3));
+        if (mmax == 1) hipLaunchKernelGGL((decode_prep_perm<1>), dim3(blocks), dim3(kBlock), lds4, s, p);
+        else if (mmax == 2) hipLaunchKernelGGL((decode_prep_perm<2>), dim3(blocks), dim3(kBlock), lds4, s, p);
+        else if (mmax == 3) hipLaunchKernelGGL((decode_prep_perm<3>), dim3(blocks), dim3(kBlock), lds4, s, p);
+        else if (mmax == 4) hipLaunchKernelGGL((decode_prep_perm<4>), dim3(blocks), dim3(kBlock), lds4, s, p);
         else hipLaunchKernelGGL((decode_prep_small<8>), dim3(blocks), dim3(kBlock), lds, s, p);
     } else {
         const size_t K4 = (K + 3) & ~size_t(3), W4 = (2 * (size_t)mmax + 3) / 4;
-        const size_t lds = 1536 + 128 * 20 + (size_t)R * K4 + (size_t)mmax * W4 * 4 + (size_t)mmax * K4;
-        static bool attr = false;  // up to ~67 KB for R = K = 128
+        const size_t lds = 1536 + 128 * kPrepTC * 20 + 256 + (size_t)R * K4 + (size_t)mmax * W4 * 4;
+        static bool attr = false;  // up to ~70 KB for R = K = 128
         if (!attr) {
             if (hipFuncSetAttribute((const void *)decode_prep_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     96 * 1024) != hipSuccess)
@@ -1923,11 +2106,11 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
             attr = true;
         }
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)decode_prep_wave, 64, lds) != hipSuccess ||
-            occ <= 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)decode_prep_wave, kPrepThreads, lds) !=
+                hipSuccess || occ <= 0)
             occ = 1;
         const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>(G, (size_t)std::max(di.cus, 1) * occ));
-        hipLaunchKernelGGL(decode_prep_wave, dim3(blocks), dim3(64), lds, s, p, mmax);
+        hipLaunchKernelGGL(decode_prep_wave, dim3(blocks), dim3(kPrepThreads), lds, s, p, mmax);
     }
     if (hipGetLastError() != hipSuccess) return -3;
     if (R == 0 || B == 0) return 0;
@@ -1977,10 +2160,10 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         }
     }
 
-    const int vec = pick_vec(pitch, {d_data, d_parity, d_out});
+    int vec = 0, mt = 0;
+    mac_shape(R, pick_vec(pitch, {d_data, d_parity, d_out}), vec, mt);
     const int vb = vec >= 4 ? vec : 4;
     const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
-    const int mt = pick_mt(R);
     const int tiles = (R + mt - 1) / mt;
     const size_t ent = entry_bytes(mt);
     return for_group_ranges(G, cpad, [&](size_t g0, size_t gn) {
