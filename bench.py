@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--config", default="20:3", choices=sorted(CONFIGS))
     p.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-seconds of the baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=16.0, help="target CPU-seconds of the baseline sample")
     return p.parse_args()
 
 
@@ -70,6 +70,13 @@ def cpu_baseline(K, N, B, pool, erase, rnd, target_cpu_s, decode_only=False):
     bps, secs = run(1)  # calibration pass (also warms the pages)
     passes = max(1, int(target_cpu_s / max(secs * threads, 1e-3)))
     bps, secs = run(passes)
+    # one core, same groups: about a tenth of the CPU time above
+    if kind == "reference":
+        g1 = max(64, G // 8)
+        bps1 = ref.bench_roundtrip(K, N, B, g1, pool, erase, rnd, 1, 1, 0x5EED0001, decode_only)[0]
+    else:
+        g1 = G
+        bps1 = None
     import platform
     model = platform.processor() or ""
     try:
@@ -82,9 +89,11 @@ def cpu_baseline(K, N, B, pool, erase, rnd, target_cpu_s, decode_only=False):
         pass
     what = "decode-only" if decode_only else "encode + decode"
     return {"value": round(bps / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "value_1core": round(bps1 / 2**30, 4) if bps1 else None,
             "sample": f"{G} distinct groups x {passes} passes of fec={K}:{N-K} B={B} {what} "
                       f"({'random 1-%d of all %d' % (erase, N) if rnd else '%d data' % erase} shards erased), "
-                      f"{secs:.1f} s wall on {threads} threads, {model}"}
+                      f"{secs:.1f} s wall on {threads} threads, {model}; value_1core: {g1} groups x 1 pass "
+                      f"on 1 thread"}
 
 
 def main():
@@ -178,11 +187,16 @@ def main():
     # roofline: algorithmic HBM bytes per launch / measured launch duration
     enc_bytes = G * (K + R) * B                    # read K*B, write R*B per group
     dec_bytes = G * K * B + n_rec * B              # read the K selected shares, write the m recovered
+    enc_read = G * K * B
+    dec_read = G * K * B
     if do_enc:
-        dom_bytes, dom_ms, dom_name = enc_bytes, enc_ms, "mac_kernel<16,3,encode> (kfec_encode_batch)"
+        dom_bytes, dom_read, dom_ms = enc_bytes, enc_read, enc_ms
+        dom_name = "mac_kernel<VEC,MT,encode> (kfec_encode_batch)"
     else:
-        dom_bytes, dom_ms, dom_name = dec_bytes, dec_ms, "decode_prep + mac_kernel<8,3,decode> (kfec_decode_batch)"
+        dom_bytes, dom_read, dom_ms = dec_bytes, dec_read, dec_ms
+        dom_name = "decode_prep_* + mac_kernel<VEC,MT,decode> (kfec_decode_batch)"
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    achieved_read = dom_read / (dom_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
@@ -210,7 +224,8 @@ def main():
                    "global_groups": G * world, "parallelism": f"{world} independent group ranges (no collective)"},
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4)},
+                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),
+                     "achieved_read": round(achieved_read, 1), "frac_read": round(achieved_read / HBM_PEAK_GBS, 4)},
         "encode_ms": round(enc_ms, 4) if do_enc else None,
         "decode_ms": round(dec_ms, 4),
         "decode_hbm_GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),

@@ -74,9 +74,10 @@ int kfec_decode(const kfec_ctx *ctx, const size_t *share_ids, const uint8_t *con
  * Layout (R = N - K, every slot `pitch` bytes apart, block size B <= pitch):
  *   d_data    [G][K][pitch]   data shards of group g
  *   d_parity  [G][R][pitch]   parity shards
- * The code is byte-column independent, so any pitch works; the kernels move V = 16/8/4-byte granules
- * (V = largest power dividing pitch and every base pointer) and may read/write bytes [B, ceil(B/V)*V) of
- * a slot, which lie inside the slot's pitch.  Bytes [0, B) are bit-exact with the reference. */
+ * The code is byte-column independent, so any pitch works.  When pitch and every base pointer are
+ * multiples of 4 the kernels move 32-byte granules (the last one of a row dword by dword) and may read and
+ * write bytes [B, ceil(B/4)*4) of a slot, which lie inside the slot's pitch; otherwise they move bytes
+ * and touch only [0, B).  Bytes [0, B) are bit-exact with the reference. */
 
 /* Parity of G groups: d_parity[g][r] = XOR_j enc[K+r][j] * d_data[g][j]. */
 int kfec_encode_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, const void *d_data,

@@ -104,12 +104,11 @@ __device__ __forceinline__ uint64_t bits_below(int n, int q)
     return v <= 0 ? 0ull : (v >= 64 ? ~0ull : ((1ull << v) - 1ull));
 }
 
-// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor_b32 otherwise
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor_b32 otherwise.
+// The builtin (not inline asm) leaves the scheduler free to interleave independent accumulator chains.
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
 // acc ^ c * x for 4 bytes, c given by its 5 permute tables (kfec_gf.hpp gf_perm_tables):
@@ -707,7 +706,6 @@ struct MacArgs {
     uint32_t rec_stride;
     uint32_t JC;            // shards per LDS chunk
     uint32_t gmax;          // group slots per chunk
-    uint32_t order;         // shard visiting order: bit 0 interleave (see mac_kernel), bits 8.. odd-wave lag
 };
 
 template <int VEC>
@@ -768,12 +766,31 @@ __device__ __forceinline__ void store_gran(uint8_t *p, const uint32_t *d, uint32
     }
 }
 
+// Last granule of a shard row when B is not a multiple of VEC (e.g. B = 1400 at VEC = 32): only the nd
+// dwords that hold bytes below B are loaded / stored (bytes [B, 4*ceil(B/4)) lie inside the pitch), so no
+// lane reads or writes past its own slot -- pitch only needs to be a multiple of 4.
+template <int VEC>
+__device__ __forceinline__ Gran<VEC> load_gran_tail(const uint8_t *p, uint32_t nd)
+{
+    Gran<VEC> v;
+#pragma unroll
+    for (int w = 0; w < Gran<VEC>::W; ++w) v.d[w] = (uint32_t)w < nd ? reinterpret_cast<const uint32_t *>(p)[w] : 0u;
+    return v;
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_gran_tail(uint8_t *p, const uint32_t *d, uint32_t nd)
+{
+#pragma unroll
+    for (int w = 0; w < Gran<VEC>::W; ++w)
+        if ((uint32_t)w < nd) reinterpret_cast<uint32_t *>(p)[w] = d[w];
+}
+
 template <int MT>
 struct MacLayout {
-    // per (group, shard): 8-byte share pointer + 8 pad, then t0..t3 of row r at 16 * r (one ds_read_b128),
-    // then t4 of every row (MT dwords, padded to 16 B)
-    static constexpr int T4OFF = 16 + 16 * MT;
-    static constexpr int ENTRY = T4OFF + ((4 * MT + 15) / 16) * 16;
+    static_assert(MT >= 1 && MT <= 8, "row tile");
+    static constexpr int TBL_DW = ((5 * MT + 3) / 4) * 4;  // table dwords per (group, shard): 5 per row
+    static constexpr int ENTRY = 16 + 4 * TBL_DW;          // + 8-byte share pointer, 8 pad
 };
 
 // expand coefficients of shards [c0, c0+nj) for group slots [0, ng) into LDS entries
@@ -806,8 +823,9 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
         }
         uint32_t t[5];
         gf_perm_tables(c, t);
-        *reinterpret_cast<uint4 *>(ent + 16 + 16 * r) = make_uint4(t[0], t[1], t[2], t[3]);
-        reinterpret_cast<uint32_t *>(ent + L::T4OFF)[r] = t[4];
+        uint32_t *tp = reinterpret_cast<uint32_t *>(ent + 16) + 5 * r;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) tp[i] = t[i];
     }
 }
 
@@ -833,6 +851,9 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
         const uint32_t g = item < a.total ? item / cols : 0;
         const uint32_t col = item < a.total ? item - g * cols : 0;
         const bool in = item < a.total && col < a.cols;
+        // dwords of this lane's granule below B: W except in the last granule of a row when VEC does not
+        // divide B (VEC >= 4 only; the bytewise VEC = 1 path checks every byte itself)
+        const uint32_t nd = (VEC >= 4 && (col + 1) * VB > a.B) ? (a.B - col * VB + 3) / 4 : (uint32_t)W;
         const uint32_t gfirst = base / cols;
         const uint32_t glast = min(base + kBlock - 1, a.total - 1) / cols;
         const uint32_t ng = glast - gfirst + 1;
@@ -864,23 +885,9 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
             }
             if (rows == 0) continue;
             const uint8_t *ent0 = s_ent + (gs * a.JC) * L::ENTRY;
-            // Shard visiting order.  A 128-B line straddling shards j and j+1 (3 of every 4 boundaries at
-            // B = 1440) is requested twice; the L2 does not merge a request with an in-flight miss of the
-            // same line, so both go to DRAM when j and j+1 are issued back to back.  Interleaving (order
-            // bit 0) visits each block of 2*PD shards odd-first ([1,3,..,0,2,..]): neighbours are then >= PD
-            // positions apart, i.e. the second request is issued after the first has landed and hits L2.
-            // Bits 8.. lag odd waves by that many positions (lines split between two waves).
-            const uint32_t lag = ((threadIdx.x >> 6) & 1u) ? (a.order >> 8) % nj : 0u;
-            const uint32_t nblk = (a.order & 1u) ? nj & ~(2u * PD - 1u) : 0u;
-            auto sj = [&](uint32_t jj) -> uint32_t {
-                uint32_t p = jj + lag;
-                p = p >= nj ? p - nj : p;
-                if (p < nblk) {
-                    const uint32_t q = p & (2u * PD - 1u);
-                    p = (p - q) + (q < (uint32_t)PD ? 2u * q + 1u : 2u * (q - PD));
-                }
-                return p;
-            };
+            // (a shard visiting order that puts the two readers of a line straddling shards j and j+1 >= PD
+            // loads apart, or lags odd waves, was measured: no gain at 20:3, -15% at 10:3 -- DESIGN.md 4.5)
+            auto sj = [](uint32_t jj) -> uint32_t { return jj; };
             auto share_ptr = [&](uint32_t jj) -> const uint8_t * {
                 const uint32_t j = sj(jj);
                 if constexpr (DEC) {
@@ -892,34 +899,38 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
             Gran<VEC> x[PD];
 #pragma unroll
             for (int u = 0; u < PD; ++u)
-                if ((uint32_t)u < nj) x[u] = load_gran<VEC>(share_ptr(u), col, a.B);
+                if ((uint32_t)u < nj)
+                    x[u] = nd < (uint32_t)W ? load_gran_tail<VEC>(share_ptr(u), nd) : load_gran<VEC>(share_ptr(u), col, a.B);
             for (uint32_t jb = 0; jb < nj; jb += PD) {
 #pragma unroll
                 for (int u = 0; u < PD; ++u) {
                     const uint32_t jj = jb + u;
                     if (jj < nj) {
                         const Gran<VEC> cur = x[u];
-                        if (jj + PD < nj) x[u] = load_gran<VEC>(share_ptr(jj + PD), col, a.B);
+                        if (jj + PD < nj)
+                            x[u] = nd < (uint32_t)W ? load_gran_tail<VEC>(share_ptr(jj + PD), nd)
+                                                    : load_gran<VEC>(share_ptr(jj + PD), col, a.B);
                         const uint8_t *ent = ent0 + sj(jj) * L::ENTRY;
-                        uint32_t s0[W], s1[W], s2[W];
+                        uint32_t t[L::TBL_DW];
+                        const uint4 *tv = reinterpret_cast<const uint4 *>(ent + 16);
+#pragma unroll
+                        for (int i = 0; i < L::TBL_DW / 4; ++i) {
+                            const uint4 q = tv[i];
+                            t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+                        }
 #pragma unroll
                         for (int w = 0; w < W; ++w) {
                             const uint32_t xv = cur.d[w];
-                            s0[w] = xv & 0x07070707u;
-                            s1[w] = (xv >> 3) & 0x07070707u;
-                            s2[w] = (xv >> 6) & 0x03030303u;
-                        }
+                            const uint32_t s0 = xv & 0x07070707u;
+                            const uint32_t s1 = (xv >> 3) & 0x07070707u;
+                            const uint32_t s2 = (xv >> 6) & 0x03030303u;
 #pragma unroll
-                        for (int r = 0; r < MT; ++r) {
-                            const uint4 q = *reinterpret_cast<const uint4 *>(ent + 16 + 16 * r);
-                            const uint32_t t[5] = {q.x, q.y, q.z, q.w,
-                                                   reinterpret_cast<const uint32_t *>(ent + L::T4OFF)[r]};
-#pragma unroll
-                            for (int w = 0; w < W; ++w) {
+                            for (int r = 0; r < MT; ++r) {
 #if KFEC_ABLATE == 1  // timing-only build: memory traffic of the real kernel, XOR instead of the GF MAC
-                                acc[r][w] ^= cur.d[w] ^ t[0];
+                                acc[r][w] ^= xv ^ t[5 * r];
+                                (void)s0; (void)s1; (void)s2;
 #else
-                                acc[r][w] = perm_mac(acc[r][w], t, s0[w], s1[w], s2[w]);
+                                acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
 #endif
                             }
                         }
@@ -931,7 +942,11 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
             const uint64_t obase = ((uint64_t)g * a.R + row0) * a.pitch + (uint64_t)col * VB;
 #pragma unroll
             for (int r = 0; r < MT; ++r)
-                if ((uint32_t)r < rows) store_gran<VEC>(a.out + obase + (uint64_t)r * a.pitch, acc[r], col, a.B);
+                if ((uint32_t)r < rows) {
+                    uint8_t *o = a.out + obase + (uint64_t)r * a.pitch;
+                    if (nd < (uint32_t)W) store_gran_tail<VEC>(o, acc[r], nd);
+                    else store_gran<VEC>(o, acc[r], col, a.B);
+                }
         }
     }
 }
@@ -1663,19 +1678,25 @@ static int pick_vec(size_t pitch, std::initializer_list<const void *> ptrs)
     return 1;
 }
 
+// granule of the flattened kernel: 32 B whenever the pitch and every base pointer are dword aligned (the
+// tail granule of a row is loaded / stored dword by dword), bytewise otherwise
+static int pick_vec_mac(size_t pitch, std::initializer_list<const void *> ptrs)
+{
+    bool ok = (pitch % 4) == 0;
+    for (const void *p : ptrs) ok = ok && (reinterpret_cast<uintptr_t>(p) % 4) == 0;
+#if KFEC_VEC32
+    return ok ? 32 : 1;
+#else
+    return ok ? 16 : 1;
+#endif
+}
+
 // resident 256-thread blocks per CU for a kernel (occupancy API, capped at 8: MI355X_MICROARCH.md
 // "Residency": the API can over-report by one for SGPR-heavy kernels; ours stay below 80 SGPRs)
 static int env_int(const char *name, int dflt)
 {
     const char *e = getenv(name);
     return e && *e ? atoi(e) : dflt;
-}
-
-// shard visiting order of mac_kernel (MacArgs::order); KFEC_ORDER overrides for experiments
-static uint32_t mac_order()
-{
-    static const uint32_t o = (uint32_t)env_int("KFEC_ORDER", 0);
-    return o;
 }
 
 static int resident_blocks(const void *kernel, size_t lds)
@@ -1688,19 +1709,17 @@ static int resident_blocks(const void *kernel, size_t lds)
 
 static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
 
-// (granule bytes, output rows per tile) of the flattened kernel.  Accumulators take MT * VEC/4 VGPRs;
-// keeping that at <= 64 lets a larger R use taller row tiles on narrower granules, so each input byte
-// is read by fewer tiles (200:55: 7 tiles of 8 rows -> 2 of 32).  KFEC_MT / KFEC_VEC override.
+// (granule bytes, output rows per tile) of the flattened kernel: the widest granule and MT = min(R, 8)
+// rows.  Measured at 200:55: taller tiles on narrower granules (16 x 16 B, 32 x 8 B) read each
+// input byte fewer times but are no faster -- the re-reads hit L2 and the kernel is VALU-bound there,
+// where 32-B granules amortise each table read over the most bytes.  KFEC_MT / KFEC_VEC override.
 static void mac_shape(int R, int vec_max, int &vec, int &mt)
 {
     static const int mt_env = env_int("KFEC_MT", 0), vec_env = env_int("KFEC_VEC", 0);
-    if (R <= 4) mt = std::max(R, 1), vec = vec_max;
-    else if (R <= 8) mt = 8, vec = std::min(vec_max, 32);
-    else if (R <= 16) mt = 16, vec = std::min(vec_max, 16);
-    else mt = 32, vec = std::min(vec_max, 8);
-    if (mt_env == 1 || mt_env == 2 || mt_env == 3 || mt_env == 4 || mt_env == 8 || mt_env == 16 || mt_env == 32)
-        mt = mt_env;
-    if (vec_env > 0 && vec_env < vec && (vec_env & (vec_env - 1)) == 0) vec = vec_env;
+    vec = vec_max;
+    mt = pick_mt(R);
+    if (mt_env == 1 || mt_env == 2 || mt_env == 3 || mt_env == 4 || mt_env == 8) mt = mt_env;
+    if (vec_env > 0 && vec_env <= vec_max && (vec_env & (vec_env - 1)) == 0) vec = vec_env;
 }
 
 // KFEC_PAD=1: pad a group's items to whole waves, so one wave-instruction reads a whole shard row and
@@ -1742,9 +1761,7 @@ static int dispatch_mac(const DeviceInfo &di, int vec, int mt, MacArgs a, int ti
     case 2: return run_mac<V, 2, DEC>(di, a, tiles, s);                      \
     case 3: return run_mac<V, 3, DEC>(di, a, tiles, s);                      \
     case 4: return run_mac<V, 4, DEC>(di, a, tiles, s);                      \
-    case 8: return run_mac<V, 8, DEC>(di, a, tiles, s);                      \
-    case 16: return run_mac<V, 16, DEC>(di, a, tiles, s);                    \
-    default: return run_mac<V, 32, DEC>(di, a, tiles, s);                    \
+    default: return run_mac<V, 8, DEC>(di, a, tiles, s);                     \
     }
     switch (vec) {
 #if KFEC_VEC32
@@ -1765,9 +1782,7 @@ static int entry_bytes(int mt)
     case 2: return MacLayout<2>::ENTRY;
     case 3: return MacLayout<3>::ENTRY;
     case 4: return MacLayout<4>::ENTRY;
-    case 8: return MacLayout<8>::ENTRY;
-    case 16: return MacLayout<16>::ENTRY;
-    default: return MacLayout<32>::ENTRY;
+    default: return MacLayout<8>::ENTRY;
     }
 }
 
@@ -2038,7 +2053,7 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         }
     }
     int vec = 0, mt = 0;
-    mac_shape(R, pick_vec(pitch, {d_data, d_parity}), vec, mt);
+    mac_shape(R, pick_vec_mac(pitch, {d_data, d_parity}), vec, mt);
     const int vb = vec >= 4 ? vec : 4;
     const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
     const int tiles = (R + mt - 1) / mt;
@@ -2060,7 +2075,6 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.rec_stride = 0;
         a.JC = JC;
         a.gmax = 1;
-        a.order = mac_order();
         return dispatch_mac<false>(di, vec, mt, a, tiles, s);
     });
 }
@@ -2161,7 +2175,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     }
 
     int vec = 0, mt = 0;
-    mac_shape(R, pick_vec(pitch, {d_data, d_parity, d_out}), vec, mt);
+    mac_shape(R, pick_vec_mac(pitch, {d_data, d_parity, d_out}), vec, mt);
     const int vb = vec >= 4 ? vec : 4;
     const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
     const int tiles = (R + mt - 1) / mt;
@@ -2184,7 +2198,6 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.rec_stride = (uint32_t)rs;
         a.JC = JC;
         a.gmax = gmax;
-        a.order = mac_order();
         return dispatch_mac<true>(di, vec, mt, a, tiles, s);
     });
 }

@@ -188,11 +188,12 @@ def _scribble_absent(data, par, masks, K):
 # ---------------------------------------------------------------------------------------------------
 CASES = [
     # K, N, B, pitch, G, erase (None = random 0..R over all N), note
-    (20, 23, 1440, 1440, 37, 3, "headline shape, V=16"),
-    (10, 13, 1400, 1400, 41, None, "B=1400 -> V=8, random erasures"),
-    (20, 23, 1407, 1407, 9, 3, "odd B -> bytewise kernel"),
-    (20, 23, 1406, 1408, 9, 2, "pitch > B, V=16 with overhang"),
-    (7, 9, 100, 100, 300, None, "V=4, many groups per workgroup"),
+    (20, 23, 1440, 1440, 37, 3, "headline shape, V=32, no tail granule"),
+    (10, 13, 1400, 1400, 41, None, "B=1400 -> V=32 with a 6-dword tail granule, random erasures"),
+    (10, 13, 1402, 1404, 19, 3, "pitch % 16 = 12 -> V=32, 1-dword tail, 2 overhang bytes"),
+    (20, 23, 1407, 1407, 9, 3, "odd pitch -> bytewise kernel"),
+    (20, 23, 1406, 1408, 9, 2, "pitch > B, tail granule with overhang"),
+    (7, 9, 100, 100, 300, None, "many groups per workgroup"),
     (1, 2, 16, 16, 513, 1, "K=1"),
     (3, 5, 1, 1, 1000, None, "B=1, one column"),
     (16, 24, 256, 256, 33, 8, "R=8 -> MT=8, prep_small<8>"),
@@ -201,11 +202,11 @@ CASES = [
     (5, 5, 32, 32, 10, 0, "R=0"),
     (128, 256, 48, 48, 3, 100, "R=128, m up to 100"),
     (255, 256, 40, 40, 6, 1, "K=255"),
-    (5, 8, 9000, 9000, 7, 3, "B > 8 KiB -> flattened kernel, V=8"),
-    (3, 5, 8193, 8208, 5, None, "B > 8 KiB, pitch > B -> flattened kernel, V=16"),
-    (4, 7, 2047, 2047, 5, 3, "largest tile-kernel B, bytewise staging"),
-    (6, 9, 2048, 2048, 5, 3, "largest tile-kernel B, LDS-DMA staging"),
-    (6, 9, 2049, 2064, 5, 3, "smallest flattened-kernel B"),
+    (5, 8, 9000, 9000, 7, 3, "B > 8 KiB, 2-dword tail"),
+    (3, 5, 8193, 8208, 5, None, "B > 8 KiB, pitch > B, 1-dword tail with overhang"),
+    (4, 7, 2047, 2047, 5, 3, "odd B, bytewise"),
+    (6, 9, 2048, 2048, 5, 3, "B = 2048"),
+    (6, 9, 2049, 2064, 5, 3, "B = 2049, pitch > B"),
 ]
 
 
@@ -222,6 +223,9 @@ def test_batch_vs_oracle(dev, oracle, K, N, B, pitch, G, erase, note):
     torch.cuda.synchronize()
     exp_par = oracle.encode_batch(K, N, data_np, B)
     np.testing.assert_array_equal(_np(par)[:, :, :B], exp_par[:, :, :B], err_msg=note)
+    # writes stay inside [0, ceil(B/4)*4) of each slot (kfec.h), [0, B) for a pitch that is not dword aligned
+    hi = B if pitch % 4 else min(pitch, (B + 3) // 4 * 4)
+    assert (_np(par)[:, :, hi:] == 0x77).all(), note
 
     masks_np = np.zeros((G, 4), np.uint64)
     for g in range(G):
@@ -256,6 +260,7 @@ def test_batch_vs_oracle(dev, oracle, K, N, B, pitch, G, erase, note):
         want = exp_out[:, :, :B].copy()
         want[exp_idx == 0xFF] = 0
         np.testing.assert_array_equal(got, want, err_msg=note)
+        assert (_np(out)[:, :, hi:] == 0).all(), note
 
 
 def test_single_group_api_vs_oracle(dev, oracle):

@@ -18,7 +18,10 @@ idx = torch.empty((G, R), dtype=torch.uint8, device=dev)
 st = torch.empty((G,), dtype=torch.uint8, device=dev)
 ws = c.decode_workspace(G)
 c.synth(data, 1)
-c.erasure_masks(masks, 1, K, min(R, K))
+if os.environ.get("AB_RANDOM"):  # bench config 10:3dec: random 1..R erasures over all N shards
+    c.erasure_masks(masks, 0x5EED0001, N, R, True)
+else:
+    c.erasure_masks(masks, 1, K, min(R, K))
 s = torch.cuda.current_stream()
 e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
 enc, dec = [], []
