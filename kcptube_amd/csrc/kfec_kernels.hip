@@ -1738,16 +1738,23 @@ static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
 {
     using L = MacLayout<MT>;
     const size_t lds = (size_t)a.gmax * a.JC * L::ENTRY;
-    // persistent grid sized to what is resident at once: a grid one block per CU larger than that
-    // leaves a tail in which a single block per CU runs alone (measured: +45% kernel time)
+    // one workgroup per 256 items (non-persistent): the dispatcher refills each CU as workgroups retire.
+    // Measured against a persistent grid sized to the resident workgroups (KFEC_GRID_PERSIST=1): encode
+    // 6.90 -> 6.08 ms and decode 7.39 -> 6.75 ms at 20:3 B=1440 1M groups, 205 -> 173 ms encode at 200:55
+    // (DESIGN.md 5).  With several row tiles the grid's x extent stays a multiple of the 8 XCDs, so
+    // workgroups (x, y) and (x, y') share an XCD and the tiles' re-reads of the same shard bytes hit its L2.
     const uint32_t want = (a.total + kBlock - 1) / kBlock;
-    uint32_t cap = (uint32_t)(std::max(1, di.cus) * resident_blocks((const void *)mac_kernel<VEC, MT, DEC>, lds))
-                   / (uint32_t)std::max(1, tiles);
-    // with several row tiles, keep gridDim.x a multiple of the 8 XCDs: workgroups (x, y) and (x, y') then
-    // share an XCD (dispatch is round-robin over XCDs in linear block order), so the tiles' re-reads of
-    // the same shard bytes hit that XCD's L2
-    if (tiles > 1 && cap >= 8) cap &= ~7u;
-    const uint32_t gx = std::max(1u, std::min(want, std::max(cap, 1u)));
+    static const int persist = env_int("KFEC_GRID_PERSIST", 0);
+    uint32_t gx = want;
+    if (persist) {
+        uint32_t cap = (uint32_t)(std::max(1, di.cus) * resident_blocks((const void *)mac_kernel<VEC, MT, DEC>, lds))
+                       / (uint32_t)std::max(1, tiles);
+        if (tiles > 1 && cap >= 8) cap &= ~7u;
+        gx = std::min(want, std::max(cap, 1u));
+    } else if (tiles > 1) {
+        gx = (want + 7) & ~7u;
+    }
+    gx = std::max(1u, gx);
     hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC>), dim3(gx, tiles), dim3(kBlock), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

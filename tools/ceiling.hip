@@ -1,0 +1,202 @@
+// ceiling.hip -- what the encode's byte mix can reach on this box (XOR only, no GF arithmetic).
+//   The encode at fec=20:3, B=1440 reads 28,800 B and writes 4,320 B per group.  These kernels move the
+//   same bytes with different access shapes, to separate "HBM can't do better" from "our shape loses":
+//   read_chunk<U>   : each workgroup reads one contiguous chunk of U x 4 KiB (16-B lanes), non-persistent grid
+//   write_chunk<U>  : the same with stores
+//   copy_chunk<U>   : read chunk + store chunk
+//   enc_lin         : one workgroup per group: the group's 28,800 B read as 1,800 consecutive 16-B granules,
+//                     4,320 B written (the ideal streaming form of the encode's traffic)
+//   enc_cols<V,PD>  : lane = (group, V-byte column), reads the column of the 20 shards, PD shards in flight,
+//                     writes 3 columns (the flattened kernel's shape), persistent grid of occ WG/CU
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/ceiling tools/ceiling.hip
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x4 ld16(const uint8_t *p) { return *reinterpret_cast<const u32x4 *>(p); }
+__device__ __forceinline__ void st16(uint8_t *p, u32x4 v, bool nt)
+{
+    if (nt) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    else *reinterpret_cast<u32x4 *>(p) = v;
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) read_chunk(const uint8_t *a, uint8_t *sink)
+{
+    const uint8_t *p = a + ((size_t)blockIdx.x * U * 256 + threadIdx.x) * 16;
+    u32x4 v[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) v[i] = ld16(p + (size_t)i * 4096);
+    u32x4 acc = v[0];
+#pragma unroll
+    for (int i = 1; i < U; ++i) acc ^= v[i];
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) st16(sink, acc, false);
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) write_chunk(uint8_t *b, bool nt)
+{
+    uint8_t *p = b + ((size_t)blockIdx.x * U * 256 + threadIdx.x) * 16;
+    const u32x4 v = {threadIdx.x, blockIdx.x, 1u, 2u};
+#pragma unroll
+    for (int i = 0; i < U; ++i) st16(p + (size_t)i * 4096, v, nt);
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) copy_chunk(const uint8_t *a, uint8_t *b, bool nt)
+{
+    const size_t off = ((size_t)blockIdx.x * U * 256 + threadIdx.x) * 16;
+    u32x4 v[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) v[i] = ld16(a + off + (size_t)i * 4096);
+#pragma unroll
+    for (int i = 0; i < U; ++i) st16(b + off + (size_t)i * 4096, v[i], nt);
+}
+
+// one workgroup (256 lanes) per group: 1800 granules read, 270 written
+__global__ void __launch_bounds__(256) enc_lin(const uint8_t *d, uint8_t *par, bool nt)
+{
+    const uint8_t *p = d + (size_t)blockIdx.x * 28800;
+    u32x4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const unsigned q = i * 256 + threadIdx.x;
+        v[i] = q < 1800 ? ld16(p + q * 16) : u32x4{0, 0, 0, 0};
+    }
+    u32x4 acc = v[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) acc ^= v[i];
+    uint8_t *o = par + (size_t)blockIdx.x * 4320;
+    st16(o + threadIdx.x * 16, acc, nt);
+    if (threadIdx.x < 14) st16(o + (256 + threadIdx.x) * 16, acc, nt);
+}
+
+// one wave per group, 4 groups per workgroup
+__global__ void __launch_bounds__(256) enc_lin_wave(const uint8_t *d, uint8_t *par, unsigned G, bool nt)
+{
+    const unsigned g = blockIdx.x * 4 + threadIdx.x / 64, l = threadIdx.x % 64;
+    if (g >= G) return;
+    const uint8_t *p = d + (size_t)g * 28800;
+    u32x4 acc = {0, 0, 0, 0};
+    for (int i0 = 0; i0 < 29; i0 += 8) {
+        u32x4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const unsigned q = (i0 + i) * 64 + l;
+            v[i] = q < 1800 ? ld16(p + q * 16) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc ^= v[i];
+    }
+    uint8_t *o = par + (size_t)g * 4320;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const unsigned q = i * 64 + l;
+        if (q < 270) st16(o + q * 16, acc, nt);
+    }
+}
+
+template <int V, int PD>
+__global__ void __launch_bounds__(256) enc_cols(const uint8_t *d, uint8_t *par, unsigned total, unsigned cols, bool nt)
+{
+    constexpr int NV = V / 16;
+    for (unsigned it = blockIdx.x * 256 + threadIdx.x; it < total; it += gridDim.x * 256) {
+        const unsigned g = it / cols, c = it - g * cols;
+        const uint8_t *p = d + (size_t)g * 28800 + c * V;
+        u32x4 acc[NV];
+#pragma unroll
+        for (int w = 0; w < NV; ++w) acc[w] = u32x4{0, 0, 0, 0};
+        u32x4 x[PD][NV];
+#pragma unroll
+        for (int u = 0; u < PD; ++u)
+#pragma unroll
+            for (int w = 0; w < NV; ++w) x[u][w] = ld16(p + u * 1440 + w * 16);
+#pragma unroll
+        for (int j = 0; j < 20; ++j) {
+            const int u = j % PD;
+#pragma unroll
+            for (int w = 0; w < NV; ++w) {
+                const u32x4 cur = x[u][w];
+                if (j + PD < 20) x[u][w] = ld16(p + (j + PD) * 1440 + w * 16);
+                acc[w] ^= cur;
+            }
+        }
+        uint8_t *o = par + (size_t)g * 4320 + c * V;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int w = 0; w < NV; ++w) st16(o + r * 1440 + w * 16, acc[w] + (u32x4){(unsigned)r, 0, 0, 0}, nt);
+    }
+}
+
+int main(int argc, char **argv)
+{
+    const size_t G = 1u << 20;
+    const size_t dbytes = G * 28800, pbytes = G * 4320;
+    uint8_t *a, *b, *sink;
+    if (hipMalloc(&a, dbytes) != hipSuccess || hipMalloc(&b, pbytes) != hipSuccess || hipMalloc(&sink, 64) != hipSuccess) {
+        printf("alloc failed\n");
+        return 1;
+    }
+    hipMemset(a, 0x5A, dbytes);
+    hipMemset(b, 0, pbytes);
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    auto run = [&](const char *name, double moved, auto launch) {
+        std::vector<float> t;
+        for (int i = 0; i < 7; ++i) {
+            hipEventRecord(e0);
+            launch();
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        printf("%-34s %8.3f ms  %7.1f GB/s  (min %.3f)\n", name, t[3], moved / t[3] / 1e6, t[0]);
+        fflush(stdout);
+    };
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) printf("err %s\n", hipGetErrorString(err));
+    // chunk kernels over the 30.2 GB data buffer / 4.5 GB parity buffer
+    const unsigned nr4 = dbytes / (4 * 4096), nr8 = dbytes / (8 * 4096), nr16 = dbytes / (16 * 4096);
+    const unsigned nw4 = pbytes / (4 * 4096), nw8 = pbytes / (8 * 4096);
+    run("read_chunk<4>", nr4 * 4.0 * 4096, [&] { read_chunk<4><<<nr4, 256>>>(a, sink); });
+    run("read_chunk<8>", nr8 * 8.0 * 4096, [&] { read_chunk<8><<<nr8, 256>>>(a, sink); });
+    run("read_chunk<16>", nr16 * 16.0 * 4096, [&] { read_chunk<16><<<nr16, 256>>>(a, sink); });
+    run("write_chunk<4>", nw4 * 4.0 * 4096, [&] { write_chunk<4><<<nw4, 256>>>(b, false); });
+    run("write_chunk<8>", nw8 * 8.0 * 4096, [&] { write_chunk<8><<<nw8, 256>>>(b, false); });
+    run("write_chunk<8> nt", nw8 * 8.0 * 4096, [&] { write_chunk<8><<<nw8, 256>>>(b, true); });
+    run("copy_chunk<8> 4.5GB", nw8 * 16.0 * 4096, [&] { copy_chunk<8><<<nw8, 256>>>(a, b, false); });
+    run("copy_chunk<8> 4.5GB nt", nw8 * 16.0 * 4096, [&] { copy_chunk<8><<<nw8, 256>>>(a, b, true); });
+    run("copy_chunk<4> 4.5GB", nw4 * 8.0 * 4096, [&] { copy_chunk<4><<<nw4, 256>>>(a, b, false); });
+    const double enc = (double)G * (28800 + 4320);
+    run("enc_lin (WG/group)", enc, [&] { enc_lin<<<G, 256>>>(a, b, false); });
+    run("enc_lin (WG/group) nt", enc, [&] { enc_lin<<<G, 256>>>(a, b, true); });
+    run("enc_lin_wave", enc, [&] { enc_lin_wave<<<G / 4, 256>>>(a, b, G, false); });
+    run("enc_lin_wave nt", enc, [&] { enc_lin_wave<<<G / 4, 256>>>(a, b, G, true); });
+    const unsigned t16 = G * 90, t32 = G * 45;
+    for (int occ : {4, 8, 16}) {
+        char nm[64];
+        snprintf(nm, 64, "enc_cols<16,4> occ%d nt", occ);
+        run(nm, enc, [&] { enc_cols<16, 4><<<cus * occ, 256>>>(a, b, t16, 90, true); });
+        snprintf(nm, 64, "enc_cols<32,2> occ%d nt", occ);
+        run(nm, enc, [&] { enc_cols<32, 2><<<cus * occ, 256>>>(a, b, t32, 45, true); });
+        snprintf(nm, 64, "enc_cols<32,4> occ%d nt", occ);
+        run(nm, enc, [&] { enc_cols<32, 4><<<cus * occ, 256>>>(a, b, t32, 45, true); });
+    }
+    run("enc_cols<16,4> nonpersist nt", enc, [&] { enc_cols<16, 4><<<(t16 + 255) / 256, 256>>>(a, b, t16, 90, true); });
+    run("enc_cols<32,2> nonpersist nt", enc, [&] { enc_cols<32, 2><<<(t32 + 255) / 256, 256>>>(a, b, t32, 45, true); });
+    run("enc_cols<32,4> nonpersist nt", enc, [&] { enc_cols<32, 4><<<(t32 + 255) / 256, 256>>>(a, b, t32, 45, true); });
+    const hipError_t e2 = hipDeviceSynchronize();
+    printf("status %s\n", hipGetErrorString(e2));
+    return 0;
+}
