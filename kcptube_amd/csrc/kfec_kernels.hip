@@ -496,40 +496,56 @@ __global__ void __launch_bounds__(kBlock) decode_prep_perm(PrepArgs a)
     }
 }
 
-// General m (up to min(K, R) <= 128): one 256-thread workgroup per group.  All row arithmetic uses the
-// perm MAC on packed dwords (4 bytes per op), not per-byte log/antilog lookups:
-//   Gauss-Jordan on A = [S | I] (m rows of W4 dwords), one phase per pivot c: threads build the permute
-//   tables of each row's factor (A[r][c] / piv, or 1 / piv for the pivot row) and copy the pivot row;
-//   then threads over (row, dword) items do A[r] ^= f_r * A[c] (A[c] = f_c * A[c] for the pivot row).
-//   coef = Sinv * E_P: each thread owns fixed (u, dword) items with accumulators in VGPRs; the tables of
-//   Sinv[u][t] are built kTC columns t at a time.
-constexpr int kPrepThreads = 256;
-constexpr int kPrepTC = 8;                       // Sinv columns per table batch
-constexpr int kPrepAcc = 32;                     // dwords per thread: K4/4 <= 64 over >= 2 threads per row
-
-__device__ __forceinline__ void store_tables(uint32_t *dst, uint32_t c)
+// number of set bits of a 256-bit id map below id s
+__device__ __forceinline__ int rank_below(const uint64_t (&b)[4], int s)
 {
-    uint32_t t[5];
-    gf_perm_tables(c, t);
+    int r = 0;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) dst[i] = t[i];
+    for (int q = 0; q < 4; ++q) {
+        const int lo = 64 * q;
+        if (s >= lo + 64) r += __popcll(b[q]);
+        else if (s > lo) r += __popcll(b[q] & ((1ull << (s - lo)) - 1ull));
+    }
+    return r;
 }
 
-__global__ void __launch_bounds__(kPrepThreads) decode_prep_wave(PrepArgs a, int MMAX)
+// General m (fec=200:55 and any m > 8): Lagrange (barycentric) form, one 256-thread workgroup per group.
+//   Every share s is an evaluation of the data polynomial f (deg < K) at the point x_s (x_0 = 0,
+//   x_s = alpha^s: the rows of the reference's Vandermonde matrix, fecpp.cpp:401,467), and the K selected
+//   shares S (fecpp.cpp:528-548) determine f.  So the missing data shard M_u is
+//     D_{M_u} = XOR_{i in S} share_i * prod_{k in S, k != i} (x_{M_u} ^ x_k) / (x_i ^ x_k).
+//   The decoding map from the K selected shares is unique, so these coefficients are byte for byte the rows
+//   of the reference's K x K inverse (fecpp.cpp:550-585) -- no elimination, nothing can be singular.
+//   With FULL_s = sum_{k < N, k != s} log(x_s ^ x_k) (once per workgroup) and C = the R ids outside S:
+//     log den_i = FULL_i - sum_{k in C} log(x_i ^ x_k)
+//     log num_u = FULL_{M_u} - sum_{k in C, k != M_u} log(x_{M_u} ^ x_k)          (M_u is in C)
+//     coef[u][i] = exp(log num_u - log(x_{M_u} ^ x_i) - log den_i)
+//   That is O(K*R + m*R + m*K) table lookups per group, against O(m^3 + m^2*K) byte MACs for Gauss-Jordan
+//   followed by the product with the parity rows (measured at 200:55: 63.8 ms -> see DESIGN.md 5).
+constexpr int kPrepThreads = 256;
+
+__global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int K = a.K, N = a.N, R = a.R, tid = threadIdx.x, lane = tid & 63;
-    const int K4 = (K + 3) & ~3, kd = K4 / 4, W4 = (2 * MMAX + 3) / 4;  // augmented row: 2m bytes
-    uint8_t *s_exp = smem, *s_log = smem + 512;
-    uint8_t *s_M = smem + 768, *s_P = s_M + 256, *s_rank = s_P + 256;  // 3 x 256 bytes
-    uint32_t *s_T = reinterpret_cast<uint32_t *>(smem + 1536);         // 128 * kPrepTC tables x 5 dwords
-    uint32_t *s_row = s_T + 128 * kPrepTC * 5;                          // copy of the pivot row (64 dwords)
-    uint8_t *s_E = reinterpret_cast<uint8_t *>(s_row + 64);             // parity rows R x K4 (zero padded)
-    uint32_t *s_A = reinterpret_cast<uint32_t *>(s_E + R * K4);         // MMAX rows x W4 dwords
+    __shared__ uint8_t s_exp[512], s_log[256];
+    __shared__ uint16_t s_full[256];  // FULL_s mod 255
+    __shared__ uint8_t s_C[256];      // ids outside S, ascending
+    __shared__ uint8_t s_xC[256];     // their points
+    __shared__ uint8_t s_M[256];      // missing data ids, ascending
+    __shared__ uint8_t s_P[256];      // parity share used for missing rank t: the highest present ids, descending
+    __shared__ uint8_t s_src[256];    // source share of column j
+    __shared__ uint16_t s_lden[256];  // log den of the source of column j
+    __shared__ uint16_t s_lnum[256];  // log num_u without the (x_{M_u} ^ x_i) factor
+    const int K = a.K, N = a.N, R = a.R, tid = threadIdx.x;
+    const int K4 = (K + 3) & ~3, kd = K4 / 4;
     stage_gf(s_exp, s_log);
-    for (int i = tid; i < R * K4; i += kPrepThreads) {
-        const int r = i / K4, j = i - r * K4;
-        s_E[i] = j < K ? a.enc[(K + r) * K + j] : 0;
+    __syncthreads();
+    auto xpt = [&](int sid) -> uint32_t { return sid ? (uint32_t)s_exp[sid] : 0u; };  // s_exp[255] = 1
+    for (int sid = tid; sid < N; sid += kPrepThreads) {
+        const uint32_t xs = xpt(sid);
+        uint32_t acc = 0;
+        for (int k = 0; k < N; ++k)
+            if (k != sid) acc += s_log[xs ^ xpt(k)];
+        s_full[sid] = (uint16_t)(acc % 255u);
     }
     __syncthreads();
 
@@ -544,7 +560,7 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_wave(PrepArgs a, int
             m += __popcll(dm[q]);
         }
         uint8_t *rec = a.rec + g * a.rec_stride;
-        if (cnt < K || m > MMAX) {
+        if (cnt < K) {  // uniform over the workgroup
             if (tid == 0) {
                 rec[0] = 1;
                 rec[1] = 0;
@@ -553,130 +569,74 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_wave(PrepArgs a, int
             for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = 0xFF;
             continue;
         }
-        // wave 0: missing data ids ascending (and their ranks), highest present ids descending
-        if (tid < 64) {
-            int base = 0;
-            for (int q = 0; q < 4; ++q) {
-                const bool f = (dm[q] >> lane) & 1ull;
-                const int below = __popcll(dm[q] & ((1ull << lane) - 1ull));
-                if (f) {
-                    s_M[base + below] = (uint8_t)(q * 64 + lane);
-                    s_rank[q * 64 + lane] = (uint8_t)(base + below);
-                }
-                base += __popcll(dm[q]);
-            }
-            base = 0;
-            for (int q = 3; q >= 0; --q) {
-                const bool f = (w[q] >> lane) & 1ull;
-                const int above = __popcll(lane == 63 ? 0ull : (w[q] & ~((2ull << lane) - 1ull)));
-                if (f && base + above < m) s_P[base + above] = (uint8_t)(q * 64 + lane);
-                base += __popcll(w[q]);
+        // P_t = the present id with exactly t present ids above it (t < m; all parity since cnt >= K);
+        // the lowest of them, P_{m-1}, bounds the used-parity set from below
+        for (int sid = tid; sid < N; sid += kPrepThreads) {
+            if ((w[sid >> 6] >> (sid & 63)) & 1ull) {
+                const int above = cnt - 1 - rank_below(w, sid);
+                if (above < m) s_P[above] = (uint8_t)sid;
             }
         }
         __syncthreads();
-        const int w4 = (2 * m + 3) / 4;  // dwords per augmented row for this m
-        // A = [S | I]: S[t][u] = enc[P_t][M_u]
-        for (int e = tid; e < m * w4; e += kPrepThreads) {
-            const int t = e / w4, d = e - t * w4;
-            uint32_t v = 0;
+        const int thr = m > 0 ? (int)s_P[m - 1] : 256;
+        uint64_t Cb[4];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int col = 4 * d + b;
-                uint32_t x = 0;
-                if (col < m) x = s_E[(s_P[t] - K) * K4 + s_M[col]];
-                else if (col < 2 * m) x = (col - m == t);
-                v |= x << (8 * b);
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t used_par = w[q] & ~bits_below(thr, q);
+            const uint64_t S = (w[q] & bits_below(K, q)) | used_par;
+            Cb[q] = ~S & bits_below(N, q);
+        }
+        for (int sid = tid; sid < N; sid += kPrepThreads) {
+            const int q = sid >> 6, b = sid & 63;
+            if ((Cb[q] >> b) & 1ull) {
+                const int r = rank_below(Cb, sid);
+                s_C[r] = (uint8_t)sid;
+                s_xC[r] = (uint8_t)xpt(sid);
             }
-            s_A[t * W4 + d] = v;
+            if (sid < K && ((dm[q] >> b) & 1ull)) s_M[rank_below(dm, sid)] = (uint8_t)sid;
         }
         __syncthreads();
-        bool singular = false;
-        for (int c = 0; c < m; ++c) {
-            const uint32_t piv = reinterpret_cast<const uint8_t *>(s_A + c * W4)[c];
-            singular |= (piv == 0);
-            const uint32_t inv = ginv(s_exp, s_log, piv);
-            for (int r = tid; r < m; r += kPrepThreads) {
-                const uint32_t f = r == c ? inv : gmul(s_exp, s_log, reinterpret_cast<const uint8_t *>(s_A + r * W4)[c], inv);
-                store_tables(s_T + r * 5, f);
-            }
-            for (int d = tid; d < w4; d += kPrepThreads) s_row[d] = s_A[c * W4 + d];
-            __syncthreads();
-            for (int e = tid; e < m * w4; e += kPrepThreads) {
-                const int r = e / w4, d = e - r * w4;
-                s_A[r * W4 + d] = pm_apply(r == c ? 0u : s_A[r * W4 + d], s_T + r * 5, s_row[d]);
-            }
-            __syncthreads();
+        for (int j = tid; j < K; j += kPrepThreads) {
+            const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
+            const int i = miss ? (int)s_P[rank_below(dm, j)] : j;
+            s_src[j] = (uint8_t)i;
+            const uint32_t xi = xpt(i);
+            uint32_t acc = 0;
+            for (int c = 0; c < R; ++c) acc += s_log[xi ^ s_xC[c]];
+            s_lden[j] = (uint16_t)((s_full[i] + 255u - acc % 255u) % 255u);
         }
-        if (singular) {
-            if (tid == 0) {
-                rec[0] = 2;
-                rec[1] = 0;
-                a.status[g] = 2;
-            }
-            for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = 0xFF;
-            continue;
+        for (int u = tid; u < m; u += kPrepThreads) {
+            const int mu = s_M[u];
+            const uint32_t xm = xpt(mu);
+            uint32_t acc = 0;
+            for (int c = 0; c < R; ++c)
+                if (s_C[c] != mu) acc += s_log[xm ^ s_xC[c]];
+            s_lnum[u] = (uint16_t)((s_full[mu] + 255u - acc % 255u) % 255u);
         }
-        // coef[u][k] = XOR_t Sinv[u][t] * E[P_t][k] for present k.  tpr threads per row u (power of two,
-        // m * tpr <= 256); thread (u, sub) owns dwords d = sub + tpr * i with accumulators in VGPRs, so the
-        // tables of Sinv[u][t] are read once per thread and t
-        const int tpr = m <= 32 ? 8 : (m <= 64 ? 4 : 2);
-        const int u = tid / tpr, sub = tid - u * tpr;
-        uint32_t acc[kPrepAcc];
-#pragma unroll
-        for (int i = 0; i < kPrepAcc; ++i) acc[i] = 0;
-        for (int t0 = 0; t0 < m; t0 += kPrepTC) {
-            const int tn = min(kPrepTC, m - t0);
-            for (int e = tid; e < m * tn; e += kPrepThreads) {
-                const int uu = e / tn, tt = e - uu * tn;
-                store_tables(s_T + (uu * kPrepTC + tt) * 5, reinterpret_cast<const uint8_t *>(s_A + uu * W4)[m + t0 + tt]);
-            }
-            __syncthreads();
-            if (u < m) {
-                for (int tt = 0; tt < tn; ++tt) {
-                    uint32_t tb[5];
-#pragma unroll
-                    for (int i = 0; i < 5; ++i) tb[i] = s_T[(u * kPrepTC + tt) * 5 + i];
-                    const uint32_t *erow = reinterpret_cast<const uint32_t *>(s_E + (s_P[t0 + tt] - K) * K4);
-#pragma unroll
-                    for (int i = 0; i < kPrepAcc; ++i) {
-                        const int d = sub + tpr * i;
-                        if (d < kd) acc[i] = pm_apply(acc[i], tb, erow[d]);
-                    }
-                }
-            }
-            __syncthreads();
-        }
-        // missing columns carry Sinv[u][rank] instead; write the record as whole dwords
+        __syncthreads();
         uint32_t *srcw = reinterpret_cast<uint32_t *>(rec + 4);
         uint32_t *coefw = reinterpret_cast<uint32_t *>(rec + 4 + K4);
         for (int d = tid; d < kd; d += kPrepThreads) {
             uint32_t v = 0;
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int j = 4 * d + b;
-                if (j >= K) break;
-                const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
-                v |= (uint32_t)(miss ? s_P[s_rank[j]] : j) << (8 * b);
-            }
+            for (int b = 0; b < 4; ++b)
+                if (4 * d + b < K) v |= (uint32_t)s_src[4 * d + b] << (8 * b);
             srcw[d] = v;
         }
-        if (u < m) {
+        for (int e = tid; e < m * kd; e += kPrepThreads) {
+            const int u = e / kd, d = e - u * kd;
+            const uint32_t xm = xpt(s_M[u]);
+            const int ln = s_lnum[u];
+            uint32_t v = 0;
 #pragma unroll
-            for (int i = 0; i < kPrepAcc; ++i) {
-                const int d = sub + tpr * i;
-                if (d < kd) {
-                    uint32_t v = acc[i];
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        const int j = 4 * d + b;
-                        if (j < K && ((dm[j >> 6] >> (j & 63)) & 1ull)) {
-                            const uint32_t sv = reinterpret_cast<const uint8_t *>(s_A + u * W4)[m + s_rank[j]];
-                            v = (v & ~(0xFFu << (8 * b))) | (sv << (8 * b));
-                        }
-                    }
-                    coefw[u * kd + d] = v;
+            for (int b = 0; b < 4; ++b) {
+                const int j = 4 * d + b;
+                if (j < K) {
+                    const int ex = (ln + 510 - (int)s_log[xm ^ xpt(s_src[j])] - (int)s_lden[j]) % 255;
+                    v |= (uint32_t)s_exp[ex] << (8 * b);
                 }
             }
+            coefw[u * kd + d] = v;
         }
         for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
         if (tid == 0) {
@@ -685,7 +645,7 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_wave(PrepArgs a, int
             rec[2] = rec[3] = 0;
             a.status[g] = 0;
         }
-        __syncthreads();
+        __syncthreads();  // the lists are rewritten for the next group
     }
 }
 
@@ -822,7 +782,11 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
             if (u < a.R) c = a.enc[(uint64_t)(a.K + u) * a.K + j];
         }
         uint32_t t[5];
+#if KFEC_ABLATE == 4  // timing-only: no table construction in the per-workgroup expansion
+        t[0] = t[1] = t[2] = t[3] = t[4] = c;
+#else
         gf_perm_tables(c, t);
+#endif
         uint32_t *tp = reinterpret_cast<uint32_t *>(ent + 16) + 5 * r;
 #pragma unroll
         for (int i = 0; i < 5; ++i) tp[i] = t[i];
@@ -891,6 +855,9 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
             auto share_ptr = [&](uint32_t jj) -> const uint8_t * {
                 const uint32_t j = sj(jj);
                 if constexpr (DEC) {
+#if KFEC_ABLATE == 2  // timing-only: decode reads shards like encode (data buffer, no pointer indirection)
+                    return enc_base + (uint64_t)(c0 + j) * a.pitch;
+#endif
                     return *reinterpret_cast<const uint8_t *const *>(ent0 + j * L::ENTRY) + (uint64_t)col * VB;
                 } else {
                     return enc_base + (uint64_t)(c0 + j) * a.pitch;
@@ -2117,21 +2084,12 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         else if (mmax == 4) hipLaunchKernelGGL((decode_prep_perm<4>), dim3(blocks), dim3(kBlock), lds4, s, p);
         else hipLaunchKernelGGL((decode_prep_small<8>), dim3(blocks), dim3(kBlock), lds, s, p);
     } else {
-        const size_t K4 = (K + 3) & ~size_t(3), W4 = (2 * (size_t)mmax + 3) / 4;
-        const size_t lds = 1536 + 128 * kPrepTC * 20 + 256 + (size_t)R * K4 + (size_t)mmax * W4 * 4;
-        static bool attr = false;  // up to ~70 KB for R = K = 128
-        if (!attr) {
-            if (hipFuncSetAttribute((const void *)decode_prep_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    96 * 1024) != hipSuccess)
-                return -3;
-            attr = true;
-        }
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)decode_prep_wave, kPrepThreads, lds) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)decode_prep_lagrange, kPrepThreads, 0) !=
                 hipSuccess || occ <= 0)
             occ = 1;
         const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>(G, (size_t)std::max(di.cus, 1) * occ));
-        hipLaunchKernelGGL(decode_prep_wave, dim3(blocks), dim3(kPrepThreads), lds, s, p, mmax);
+        hipLaunchKernelGGL(decode_prep_lagrange, dim3(blocks), dim3(kPrepThreads), 0, s, p);
     }
     if (hipGetLastError() != hipSuccess) return -3;
     if (R == 0 || B == 0) return 0;

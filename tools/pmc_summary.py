@@ -9,7 +9,7 @@ reads for the roofline "traffic" field.  HBM bytes follow MI355X_MICROARCH.md "H
 WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reads exactly half the bytes of a wide (16 B/lane) coalesced
 stream, so it is doubled; WRITE_SIZE is exact for 16-B streaming stores.
 """
-import argparse, collections, csv, glob, json, os, shutil
+import argparse, collections, csv, glob, json, os, re, shutil
 
 ap = argparse.ArgumentParser()
 ap.add_argument("prof_dir"); ap.add_argument("tag")
@@ -43,8 +43,9 @@ for k, v in agg.items():
 json.dump(summary, open(os.path.join(out, f"{args.tag}_pmc.json"), "w"), indent=1)
 trf_path = os.path.join(out, "pmc_traffic.json")
 trf = json.load(open(trf_path)) if os.path.exists(trf_path) else {}
+dominant = re.compile(r"mac_kernel<\d+, \d+, %s>" % ("true" if args.config.endswith("dec") else "false"))
 for k, d in summary.items():
-    if "mac_kernel<16, 3, false>" in k and "hbm_bytes_per_launch" in d:
+    if dominant.search(k) and "hbm_bytes_per_launch" in d:
         trf[args.config] = {"groups": args.groups, "kernel": k, "hbm_bytes_per_launch": int(d["hbm_bytes_per_launch"]),
                             "source": f"profiles/{args.tag}_pmc.json"}
 json.dump(trf, open(trf_path, "w"), indent=1)
