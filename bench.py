@@ -174,6 +174,7 @@ def main():
     c.verify_recovered(data, out, idx, mism)
     torch.cuda.synchronize()
     n_rec = int((idx != 0xFF).sum().item())
+    n_dec = int((idx[:, 0] != 0xFF).sum().item()) if R > 0 else 0  # groups with m > 0 (m = 0 reads nothing)
     ok = int(mism.item()) == 0 and int(st.max().item()) == 0 and n_rec > 0
     if world > 1:
         t = torch.tensor([0 if ok else 1], dtype=torch.int64)
@@ -186,9 +187,9 @@ def main():
 
     # roofline: algorithmic HBM bytes per launch / measured launch duration
     enc_bytes = G * (K + R) * B                    # read K*B, write R*B per group
-    dec_bytes = G * K * B + n_rec * B              # read the K selected shares, write the m recovered
+    dec_bytes = n_dec * K * B + n_rec * B          # read the K selected shares, write the m recovered
     enc_read = G * K * B
-    dec_read = G * K * B
+    dec_read = n_dec * K * B
     if do_enc:
         dom_bytes, dom_read, dom_ms = enc_bytes, enc_read, enc_ms
         dom_name = "mac_kernel<VEC,MT,encode> (kfec_encode_batch)"
@@ -231,6 +232,7 @@ def main():
         "decode_hbm_GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),
         "roundtrip_hbm_GBps": round(((enc_bytes if do_enc else 0) + dec_bytes) / ((enc_ms if do_enc else 0) + dec_ms) / 1e6, 1),
         "recovered_shards_per_step": n_rec * world,
+        "decoded_groups_per_step": n_dec * world,
         "verified_bit_exact": ok,
         "cpu_baseline": None,
     }
