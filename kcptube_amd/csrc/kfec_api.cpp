@@ -2,6 +2,7 @@
 // reference's error conventions, single-group staging for the fecpp::fec_code drop-in, and the
 // batched device-resident entry points.  All arithmetic runs in the HIP kernels of kfec_kernels.hip.
 #include "../../include/kfec.h"
+#include "../../include/kfec_frame.h"
 
 #include <hip/hip_runtime.h>
 
@@ -277,6 +278,89 @@ int kfec_verify_recovered(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch,
     if (set_dev(ctx)) return KFEC_EHIP;
     return kfec::launch_verify((int)ctx->K, (int)ctx->N, G, B, pitch, d_data, d_out, d_out_idx, d_mismatch,
                                as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
+
+// ---- framing and wire layer (include/kfec_frame.h) ---------------------------------------------------
+static bool al4(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
+
+int kfec_frame_data_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size_t src_bytes, const uint64_t *d_off,
+                          const uint16_t *d_len, size_t B, size_t pitch, void *d_data, uint16_t *d_align, void *stream)
+{
+    if (!ctx || pitch < B || pitch % 4 || B > 0xFFFF) return KFEC_EINVAL;
+    if (G && (!d_src || !al4(d_src) || !d_off || !d_len || !d_data || !al4(d_data) || !d_align)) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_frame((int)ctx->K, (int)ctx->N, false, G, d_src, src_bytes, d_off, d_len, nullptr, B, pitch,
+                              d_data, nullptr, d_align, as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
+int kfec_frame_shards_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size_t src_bytes,
+                            const uint64_t *d_off, const uint16_t *d_len, const uint64_t *d_present, size_t B,
+                            size_t pitch, void *d_data, void *d_parity, uint16_t *d_align, void *stream)
+{
+    if (!ctx || pitch < B || pitch % 4 || B > 0xFFFF) return KFEC_EINVAL;
+    if (G && (!d_src || !al4(d_src) || !d_off || !d_len || !d_present || !d_data || !al4(d_data) || !d_align))
+        return KFEC_EINVAL;
+    if (G && ctx->N > ctx->K && (!d_parity || !al4(d_parity))) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_frame((int)ctx->K, (int)ctx->N, true, G, d_src, src_bytes, d_off, d_len, d_present, B, pitch,
+                              d_data, d_parity, d_align, as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
+int kfec_unframe_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, const void *d_out,
+                       const uint8_t *d_out_idx, uint16_t *d_rec_len, void *d_dst, size_t dst_pitch, void *stream)
+{
+    if (!ctx || pitch < B || pitch % 4 || B < KFEC_FEC_CONTAINER_HEADER || B > 0xFFFF) return KFEC_EINVAL;
+    if (d_dst && (dst_pitch % 4 || dst_pitch + KFEC_FEC_CONTAINER_HEADER < B || !al4(d_dst))) return KFEC_EINVAL;
+    if (G && ctx->N > ctx->K && (!d_out || !al4(d_out) || !d_out_idx || !d_rec_len)) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_unframe((int)ctx->K, (int)ctx->N, G, B, pitch, d_out, d_out_idx, d_rec_len, d_dst, dst_pitch,
+                                as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
+int kfec_pack_batch(const kfec_ctx *ctx, size_t G, unsigned which, const void *d_src, size_t src_bytes,
+                    const uint64_t *d_off, const uint16_t *d_len, size_t pitch, const void *d_parity,
+                    const uint16_t *d_align, const uint32_t *d_sn, const uint32_t *d_conv, uint32_t timestamp,
+                    void *d_pkt, size_t pkt_pitch, uint16_t *d_pkt_len, void *stream)
+{
+    if (!ctx || pkt_pitch % 4 || (which & ~(KFEC_PACK_DATA | KFEC_PACK_REDUNDANT))) return KFEC_EINVAL;
+    if (G && (!d_sn || !d_pkt || !al4(d_pkt) || !d_pkt_len)) return KFEC_EINVAL;
+    if (G && (which & KFEC_PACK_DATA) && (!d_src || !al4(d_src) || !d_off || !d_len)) return KFEC_EINVAL;
+    if (G && (which & KFEC_PACK_REDUNDANT) && ctx->N > ctx->K &&
+        (!d_parity || !al4(d_parity) || pitch % 4 || !d_align || !d_conv))
+        return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_pack((int)ctx->K, (int)ctx->N, G, which, d_src, src_bytes, d_off, d_len, pitch, d_parity,
+                             d_align, d_sn, d_conv, timestamp, d_pkt, pkt_pitch, d_pkt_len, as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
+int kfec_unpack_batch(const kfec_ctx *ctx, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
+                      const uint32_t *d_len, kfec_pkt_hdr *d_hdr, void *stream)
+{
+    (void)src_bytes;
+    if (!ctx || (P && (!d_src || !d_off || !d_len || !d_hdr))) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_unpack((int)ctx->K, P, d_src, d_off, d_len, d_hdr, as_stream(stream)) ? KFEC_EHIP : KFEC_OK;
+}
+
+int kfec_group_scatter(const kfec_ctx *ctx, size_t P, const kfec_pkt_hdr *d_hdr, const int32_t *d_slot,
+                       uint32_t sn_base, size_t G, uint64_t *d_present, uint64_t *d_off, uint16_t *d_len,
+                       void *stream)
+{
+    if (!ctx || (P && (!d_hdr || !d_present || !d_off || !d_len))) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    return kfec::launch_scatter((int)ctx->N, P, d_hdr, d_slot, sn_base, G, d_present, d_off, d_len,
+                                as_stream(stream))
                ? KFEC_EHIP
                : KFEC_OK;
 }

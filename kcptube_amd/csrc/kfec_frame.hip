@@ -1,0 +1,376 @@
+// kfec_frame.hip -- gfx950 kernels of the framing and wire layer around the coder (include/kfec_frame.h):
+// shard framing on both sides (compact_into_container, data_operations.cpp:610-667), datagram extraction
+// (extract_from_container, :697-704), FEC wire packets (connections.cpp:395-430, 488-511) and the device
+// form of the receive cache's shard insert (client.cpp:851-892).
+//
+// All of it is byte movement: HBM-bound, one dword per lane per item, consecutive lanes on consecutive
+// dwords of one slot / packet so that every wave-instruction stores 256 contiguous bytes.  Payloads sit at
+// arbitrary byte offsets and are re-based by a 2-, 9- or 13-byte header, so each output dword is
+// assembled from the two aligned source dwords that cover it (v_alignbyte_b32) and masked to the payload;
+// the neighbouring lanes' overlapping source dwords come from the same cache lines, so HBM sees each
+// payload byte about once.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../../include/kfec_frame.h"
+#include "kfec_internal.hpp"
+
+namespace kfec {
+
+namespace {
+
+constexpr int kFrameBlock = 256;
+constexpr uint64_t kMaxGrid = 1u << 24;
+
+__device__ __forceinline__ uint32_t byte_mask(int64_t q0, int64_t len)
+{
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int64_t q = q0 + b;
+        if (q >= 0 && q < len) m |= 0xFFu << (8 * b);
+    }
+    return m;
+}
+
+// bytes [q0, q0 + 4) of the payload base[start, start + len), zero outside it; base is dword aligned and
+// only dwords below lim32 are read
+__device__ __forceinline__ uint32_t payload_dword(const uint32_t *base32, uint64_t lim32, uint64_t start, uint32_t len,
+                                                  int64_t q0)
+{
+    const uint32_t m = byte_mask(q0, len);
+    if (!m) return 0u;
+    const uint64_t a4 = start + (uint64_t)(q0 + 4);  // address of the first byte + 4 (q0 >= -3 here)
+    const uint64_t w1 = a4 >> 2;                      // its dword index + 1
+    const uint32_t sh = (uint32_t)(a4 & 3u);
+    const uint32_t lo = (w1 >= 1 && w1 - 1 < lim32) ? base32[w1 - 1] : 0u;
+    const uint32_t hi = (sh && w1 < lim32) ? base32[w1] : 0u;
+    const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+    return v & m;
+}
+
+// header bytes [4k, 4k + 4) of an H-byte header packed little-endian into h[0..3]
+__device__ __forceinline__ uint32_t header_dword(const uint32_t (&h)[4], uint32_t H, uint64_t k)
+{
+    if (4 * k >= H) return 0u;
+    const uint32_t w = k == 0 ? h[0] : (k == 1 ? h[1] : (k == 2 ? h[2] : h[3]));
+    const uint32_t n = H - 4 * (uint32_t)k;
+    return n >= 4 ? w : (w & ((1u << (8 * n)) - 1u));
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// ---- alignment (block size) per group ------------------------------------------------------------------
+
+// send: align = max len + 2 (data_operations.cpp:613-616); receive: max(len + 2 for data, len for parity)
+// over the present shards (:638-646).  0 when a shard does not fit in B.
+__global__ void __launch_bounds__(kFrameBlock) align_kernel(uint64_t G, uint32_t S, uint32_t K, const uint16_t *len,
+                                                            const uint64_t *present, uint32_t B, uint16_t *align)
+{
+    const uint64_t g = blockIdx.x * (uint64_t)kFrameBlock + threadIdx.x;
+    if (g >= G) return;
+    uint32_t a = 0;
+    bool over = false;
+    for (uint32_t s = 0; s < S; ++s) {
+        if (present && !((present[g * 4 + (s >> 6)] >> (s & 63)) & 1ull)) continue;
+        const uint32_t need = len[g * S + s] + (s < K ? KFEC_FEC_CONTAINER_HEADER : 0u);
+        a = max(a, need);
+        over |= need > B;
+    }
+    align[g] = over ? 0 : (uint16_t)a;
+}
+
+// ---- framing: one dword of one shard slot per item ----------------------------------------------------
+struct FrameArgs {
+    const uint32_t *src;
+    uint64_t src_dw;
+    const uint64_t *off;
+    const uint16_t *len;
+    const uint64_t *present;  // null on the send side (every slot written)
+    const uint16_t *align;
+    uint8_t *data;
+    uint8_t *parity;
+    uint64_t pitch;
+    uint64_t total;  // G * S * cols
+    uint32_t S, K, R, cols;
+};
+
+__global__ void __launch_bounds__(kFrameBlock) frame_kernel(FrameArgs a)
+{
+    for (uint64_t it = blockIdx.x * (uint64_t)kFrameBlock + threadIdx.x; it < a.total;
+         it += (uint64_t)gridDim.x * kFrameBlock) {
+        const uint64_t slot = it / a.cols, k = it - slot * a.cols;
+        const uint64_t g = slot / a.S;
+        const uint32_t s = (uint32_t)(slot - g * a.S);
+        if (a.present && !((a.present[g * 4 + (s >> 6)] >> (s & 63)) & 1ull)) continue;
+        uint8_t *dst = s < a.K ? a.data + (g * a.K + s) * a.pitch : a.parity + (g * a.R + (s - a.K)) * a.pitch;
+        uint32_t v = 0;
+        if (a.align[g] != 0) {
+            const uint32_t n = a.len[slot];
+            const uint32_t H = s < a.K ? KFEC_FEC_CONTAINER_HEADER : 0u;
+            const uint32_t h[4] = {(n >> 8) | ((n & 0xFFu) << 8), 0u, 0u, 0u};  // htons(length)
+            v = header_dword(h, H, k) | payload_dword(a.src, a.src_dw, a.off[slot], n, (int64_t)(4 * k) - H);
+        }
+        reinterpret_cast<uint32_t *>(dst)[k] = v;
+    }
+}
+
+// ---- extraction of recovered datagrams ----------------------------------------------------------------
+struct UnframeArgs {
+    const uint8_t *out;
+    const uint8_t *out_idx;
+    uint16_t *rec_len;
+    uint8_t *dst;
+    uint64_t pitch, dst_pitch, total;
+    uint32_t R, B, cols;
+};
+
+__global__ void __launch_bounds__(kFrameBlock) unframe_kernel(UnframeArgs a)
+{
+    for (uint64_t it = blockIdx.x * (uint64_t)kFrameBlock + threadIdx.x; it < a.total;
+         it += (uint64_t)gridDim.x * kFrameBlock) {
+        const uint64_t slot = it / a.cols, k = it - slot * a.cols;
+        const uint32_t *s32 = reinterpret_cast<const uint32_t *>(a.out + slot * a.pitch);
+        uint32_t n = 0xFFFFu;
+        if (a.out_idx[slot] != 0xFF) {
+            const uint32_t d0 = s32[0];
+            n = ((d0 & 0xFFu) << 8) | ((d0 >> 8) & 0xFFu);  // ntohs(data_length)
+            if (n + KFEC_FEC_CONTAINER_HEADER > a.B) n = 0xFFFFu;
+        }
+        if (k == 0) a.rec_len[slot] = (uint16_t)n;
+        if (a.dst && n != 0xFFFFu && 4 * k < n)
+            reinterpret_cast<uint32_t *>(a.dst + slot * a.dst_pitch)[k] =
+                payload_dword(s32, a.pitch / 4, KFEC_FEC_CONTAINER_HEADER, n, (int64_t)(4 * k));
+    }
+}
+
+// ---- wire packets ---------------------------------------------------------------------------------------
+struct PackArgs {
+    const uint32_t *src;
+    uint64_t src_dw;
+    const uint64_t *off;
+    const uint16_t *len;
+    const uint8_t *parity;
+    const uint16_t *align;
+    const uint32_t *sn, *conv;
+    uint8_t *pkt;
+    uint16_t *pkt_len;
+    uint64_t pitch, pkt_pitch, total;
+    uint32_t K, N, cols, which, timestamp;
+};
+
+__global__ void __launch_bounds__(kFrameBlock) pack_kernel(PackArgs a)
+{
+    for (uint64_t it = blockIdx.x * (uint64_t)kFrameBlock + threadIdx.x; it < a.total;
+         it += (uint64_t)gridDim.x * kFrameBlock) {
+        const uint64_t pk = it / a.cols, k = it - pk * a.cols;
+        const uint64_t g = pk / a.N;
+        const uint32_t s = (uint32_t)(pk - g * a.N);
+        const bool red = s >= a.K;
+        if (!(a.which & (red ? KFEC_PACK_REDUNDANT : KFEC_PACK_DATA))) continue;
+        const uint32_t H = red ? KFEC_PKT_REDUNDANT_HEADER : KFEC_PKT_DATA_HEADER;
+        const uint32_t n = red ? a.align[g] : a.len[g * a.K + s];
+        const bool fits = H + n <= a.pkt_pitch && !(red && n == 0);
+        if (k == 0) a.pkt_len[pk] = fits ? (uint16_t)(H + n) : (uint16_t)0;
+        if (!fits || 4 * k >= H + n) continue;
+        const uint32_t sn = bswap32(a.sn[g]);  // htonl
+        uint32_t h[4];
+        h[0] = a.timestamp;  // host_to_little_endian
+        h[1] = sn;
+        if (red) {
+            const uint32_t cv = bswap32(a.conv[g]);
+            h[2] = s | (cv << 8);
+            h[3] = cv >> 24;
+        } else {
+            h[2] = s;
+            h[3] = 0;
+        }
+        uint32_t p;
+        if (red) {
+            const uint8_t *slot = a.parity + (g * (a.N - a.K) + (s - a.K)) * a.pitch;
+            p = payload_dword(reinterpret_cast<const uint32_t *>(slot), a.pitch / 4, 0, n, (int64_t)(4 * k) - H);
+        } else {
+            p = payload_dword(a.src, a.src_dw, a.off[g * a.K + s], n, (int64_t)(4 * k) - H);
+        }
+        reinterpret_cast<uint32_t *>(a.pkt + pk * a.pkt_pitch)[k] = header_dword(h, H, k) | p;
+    }
+}
+
+__global__ void __launch_bounds__(kFrameBlock) unpack_kernel(uint64_t P, uint32_t K, const uint8_t *src,
+                                                             const uint64_t *off, const uint32_t *len,
+                                                             kfec_pkt_hdr *hdr)
+{
+    const uint64_t p = blockIdx.x * (uint64_t)kFrameBlock + threadIdx.x;
+    if (p >= P) return;
+    const uint8_t *b = src + off[p];
+    const uint32_t n = len[p];
+    kfec_pkt_hdr h{};
+    h.kind = KFEC_PKT_KIND_MALFORMED;
+    if (n >= KFEC_PKT_DATA_HEADER) {
+        h.timestamp = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+        h.sn = ((uint32_t)b[4] << 24) | ((uint32_t)b[5] << 16) | ((uint32_t)b[6] << 8) | (uint32_t)b[7];
+        h.sub_sn = b[8];
+        const bool red = h.sub_sn >= K;
+        const uint32_t H = red ? KFEC_PKT_REDUNDANT_HEADER : KFEC_PKT_DATA_HEADER;
+        if (n >= H && n - H <= 0xFFFFu) {
+            h.kind = red ? KFEC_PKT_KIND_REDUNDANT : KFEC_PKT_KIND_DATA;
+            h.payload_off = off[p] + H;
+            h.payload_len = (uint16_t)(n - H);
+            const uint8_t *q = b + H;
+            if (red)
+                h.conv = ((uint32_t)b[9] << 24) | ((uint32_t)b[10] << 16) | ((uint32_t)b[11] << 8) | (uint32_t)b[12];
+            else if (n - H >= 4)
+                h.conv = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+        }
+    }
+    hdr[p] = h;
+}
+
+// Receive-cache insert in three passes, so that a duplicated (sn, sub_sn) resolves to ONE packet -- the one
+// with the highest index, i.e. the last to arrive, as fec_rcv_cache[sn][sub_sn] = ... overwrites
+// (client.cpp:869,887) -- and its offset and length are never mixed with another copy's:
+//   clear:  off[e] = 0 for every targeted entry
+//   claim:  atomicMax(off[e], TAG | p)           (TAG = bit 63: no payload offset carries it)
+//   commit: the packet whose tag survived writes off / len and sets its present bit
+__device__ __forceinline__ int64_t scatter_entry(const kfec_pkt_hdr &h, uint64_t p, uint32_t N, const int32_t *slot_of,
+                                                 uint32_t sn_base, uint64_t G)
+{
+    if (h.kind == KFEC_PKT_KIND_MALFORMED || h.sub_sn >= N) return -1;
+    const int64_t slot = slot_of ? (int64_t)slot_of[p] : (int64_t)(uint32_t)(h.sn - sn_base);
+    if (slot < 0 || (uint64_t)slot >= G) return -1;
+    return slot * (int64_t)N + h.sub_sn;
+}
+
+constexpr uint64_t kScatterTag = 1ull << 63;
+
+__global__ void __launch_bounds__(kFrameBlock) scatter_kernel(int pass, uint64_t P, uint32_t N, const kfec_pkt_hdr *hdr,
+                                                              const int32_t *slot_of, uint32_t sn_base, uint64_t G,
+                                                              unsigned long long *present, uint64_t *off,
+                                                              uint16_t *len)
+{
+    const uint64_t p = blockIdx.x * (uint64_t)kFrameBlock + threadIdx.x;
+    if (p >= P) return;
+    const kfec_pkt_hdr h = hdr[p];
+    const int64_t e = scatter_entry(h, p, N, slot_of, sn_base, G);
+    if (e < 0) return;
+    if (pass == 0) {
+        off[e] = 0;
+    } else if (pass == 1) {
+        atomicMax(reinterpret_cast<unsigned long long *>(off + e), (unsigned long long)(kScatterTag | p));
+    } else if (off[e] == (kScatterTag | p)) {
+        off[e] = h.payload_off;
+        len[e] = h.payload_len;
+        atomicOr(&present[(uint64_t)e / N * 4 + (h.sub_sn >> 6)], 1ull << (h.sub_sn & 63));
+    }
+}
+
+uint32_t grid_for(uint64_t total)
+{
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((total + kFrameBlock - 1) / kFrameBlock, kMaxGrid));
+}
+
+int launched() { return hipGetLastError() == hipSuccess ? 0 : -3; }
+
+}  // namespace
+
+int launch_frame(int K, int N, bool recv, size_t G, const void *src, size_t src_bytes, const uint64_t *off,
+                 const uint16_t *len, const uint64_t *present, size_t B, size_t pitch, void *data, void *parity,
+                 uint16_t *align, hipStream_t s)
+{
+    if (G == 0) return 0;
+    const uint32_t S = recv ? N : K;
+    hipLaunchKernelGGL(align_kernel, dim3(grid_for(G)), dim3(kFrameBlock), 0, s, (uint64_t)G, S, (uint32_t)K, len,
+                       recv ? present : nullptr, (uint32_t)B, align);
+    if (launched()) return -3;
+    FrameArgs a{};
+    a.src = static_cast<const uint32_t *>(src);
+    a.src_dw = (src_bytes + 3) / 4;
+    a.off = off;
+    a.len = len;
+    a.present = recv ? present : nullptr;
+    a.align = align;
+    a.data = static_cast<uint8_t *>(data);
+    a.parity = static_cast<uint8_t *>(parity);
+    a.pitch = pitch;
+    a.S = S;
+    a.K = K;
+    a.R = N - K;
+    a.cols = (uint32_t)((B + 3) / 4);
+    a.total = (uint64_t)G * S * a.cols;
+    hipLaunchKernelGGL(frame_kernel, dim3(grid_for(a.total)), dim3(kFrameBlock), 0, s, a);
+    return launched();
+}
+
+int launch_unframe(int K, int N, size_t G, size_t B, size_t pitch, const void *out, const uint8_t *out_idx,
+                   uint16_t *rec_len, void *dst, size_t dst_pitch, hipStream_t s)
+{
+    const uint32_t R = N - K;
+    if (G == 0 || R == 0) return 0;
+    UnframeArgs a{};
+    a.out = static_cast<const uint8_t *>(out);
+    a.out_idx = out_idx;
+    a.rec_len = rec_len;
+    a.dst = static_cast<uint8_t *>(dst);
+    a.pitch = pitch;
+    a.dst_pitch = dst_pitch;
+    a.R = R;
+    a.B = (uint32_t)B;
+    a.cols = (uint32_t)std::max<size_t>(1, (B + 1) / 4);  // ceil((B - 2) / 4) dwords of datagram, >= 1 for the length
+    a.total = (uint64_t)G * R * a.cols;
+    hipLaunchKernelGGL(unframe_kernel, dim3(grid_for(a.total)), dim3(kFrameBlock), 0, s, a);
+    return launched();
+}
+
+int launch_pack(int K, int N, size_t G, unsigned which, const void *src, size_t src_bytes, const uint64_t *off,
+                const uint16_t *len, size_t pitch, const void *parity, const uint16_t *align, const uint32_t *sn,
+                const uint32_t *conv, uint32_t timestamp, void *pkt, size_t pkt_pitch, uint16_t *pkt_len,
+                hipStream_t s)
+{
+    if (G == 0) return 0;
+    PackArgs a{};
+    a.src = static_cast<const uint32_t *>(src);
+    a.src_dw = (src_bytes + 3) / 4;
+    a.off = off;
+    a.len = len;
+    a.parity = static_cast<const uint8_t *>(parity);
+    a.align = align;
+    a.sn = sn;
+    a.conv = conv;
+    a.pkt = static_cast<uint8_t *>(pkt);
+    a.pkt_len = pkt_len;
+    a.pitch = pitch;
+    a.pkt_pitch = pkt_pitch;
+    a.K = K;
+    a.N = N;
+    a.which = which;
+    a.timestamp = timestamp;
+    a.cols = (uint32_t)(pkt_pitch / 4);
+    a.total = (uint64_t)G * N * a.cols;
+    hipLaunchKernelGGL(pack_kernel, dim3(grid_for(a.total)), dim3(kFrameBlock), 0, s, a);
+    return launched();
+}
+
+int launch_unpack(int K, size_t P, const void *src, const uint64_t *off, const uint32_t *len, kfec_pkt_hdr *hdr,
+                  hipStream_t s)
+{
+    if (P == 0) return 0;
+    hipLaunchKernelGGL(unpack_kernel, dim3((uint32_t)((P + kFrameBlock - 1) / kFrameBlock)), dim3(kFrameBlock), 0, s,
+                       (uint64_t)P, (uint32_t)K, static_cast<const uint8_t *>(src), off, len, hdr);
+    return launched();
+}
+
+int launch_scatter(int N, size_t P, const kfec_pkt_hdr *hdr, const int32_t *slot, uint32_t sn_base, size_t G,
+                   uint64_t *present, uint64_t *off, uint16_t *len, hipStream_t s)
+{
+    if (P == 0) return 0;
+    for (int pass = 0; pass < 3; ++pass) {
+        hipLaunchKernelGGL(scatter_kernel, dim3((uint32_t)((P + kFrameBlock - 1) / kFrameBlock)), dim3(kFrameBlock), 0,
+                           s, pass, (uint64_t)P, (uint32_t)N, hdr, slot, sn_base, (uint64_t)G,
+                           reinterpret_cast<unsigned long long *>(present), off, len);
+        if (launched()) return -3;
+    }
+    return 0;
+}
+
+}  // namespace kfec

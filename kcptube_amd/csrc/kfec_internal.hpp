@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "../../include/kfec_frame.h"
+
 namespace kfec {
 
 // Per-group decode record written by the prep kernels and read by the MAC kernel (group-major, so the
@@ -35,5 +37,20 @@ int launch_verify(int K, int N, size_t G, size_t B, size_t pitch, const void *d_
                   const uint8_t *d_out_idx, uint64_t *d_mismatch, hipStream_t s);
 
 uint32_t engine_error_word();
+
+// framing and wire layer (kfec_frame.hip)
+int launch_frame(int K, int N, bool recv, size_t G, const void *src, size_t src_bytes, const uint64_t *off,
+                 const uint16_t *len, const uint64_t *present, size_t B, size_t pitch, void *data, void *parity,
+                 uint16_t *align, hipStream_t s);
+int launch_unframe(int K, int N, size_t G, size_t B, size_t pitch, const void *out, const uint8_t *out_idx,
+                   uint16_t *rec_len, void *dst, size_t dst_pitch, hipStream_t s);
+int launch_pack(int K, int N, size_t G, unsigned which, const void *src, size_t src_bytes, const uint64_t *off,
+                const uint16_t *len, size_t pitch, const void *parity, const uint16_t *align, const uint32_t *sn,
+                const uint32_t *conv, uint32_t timestamp, void *pkt, size_t pkt_pitch, uint16_t *pkt_len,
+                hipStream_t s);
+int launch_unpack(int K, size_t P, const void *src, const uint64_t *off, const uint32_t *len, kfec_pkt_hdr *hdr,
+                  hipStream_t s);
+int launch_scatter(int N, size_t P, const kfec_pkt_hdr *hdr, const int32_t *slot, uint32_t sn_base, size_t G,
+                   uint64_t *present, uint64_t *off, uint16_t *len, hipStream_t s);
 
 }  // namespace kfec

@@ -39,11 +39,17 @@ _szp = C.POINTER(C.c_size_t)
 _vp = C.c_void_p
 
 
+HEADERS = [HEADER, os.path.join(os.path.dirname(PKG), "include", "kfec_frame.h")]
+
+
 def header_functions() -> list[str]:
-    """Names of every function include/kfec.h declares."""
-    with open(HEADER) as f:
-        txt = f.read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(kfec_[a-z_0-9]+)\s*\(", txt, re.M)))
+    """Names of every function the C headers (include/kfec.h, include/kfec_frame.h) declare."""
+    names = set()
+    for h in HEADERS:
+        with open(h) as f:
+            txt = f.read()
+        names |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(kfec_[a-z_0-9]+)\s*\(", txt, re.M))
+    return sorted(names)
 
 
 def load_library():
@@ -73,6 +79,14 @@ def load_library():
         "kfec_version": (C.c_char_p, []),
         "kfec_debug_flags": (C.c_uint32, []),
         "kfec_device": (C.c_int, [_vp]),
+        # include/kfec_frame.h
+        "kfec_frame_data_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, sz, sz, _vp, _vp, _vp]),
+        "kfec_frame_shards_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, _vp, sz, sz, _vp, _vp, _vp, _vp]),
+        "kfec_unframe_batch": (C.c_int, [_vp, sz, sz, sz, _vp, _vp, _vp, _vp, sz, _vp]),
+        "kfec_pack_batch": (C.c_int, [_vp, sz, C.c_uint, _vp, sz, _vp, _vp, sz, _vp, _vp, _vp, _vp, C.c_uint32,
+                                      _vp, sz, _vp, _vp]),
+        "kfec_unpack_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, _vp, _vp]),
+        "kfec_group_scatter": (C.c_int, [_vp, sz, _vp, _vp, C.c_uint32, sz, _vp, _vp, _vp, _vp]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name)
