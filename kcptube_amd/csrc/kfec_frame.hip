@@ -50,6 +50,34 @@ __device__ __forceinline__ uint32_t payload_dword(const uint32_t *base32, uint64
     return v & m;
 }
 
+// 16 bytes [q0, q0 + 16) of the payload base[start, start + len) as 4 dwords, zero outside it: one 16-byte
+// load at the covering dword (dword aligned is enough on gfx950, as the MAC kernel's granules rely on) and
+// one more dword, re-based with v_alignbyte_b32.  Dwords at or beyond lim32 read as zero.
+__device__ __forceinline__ void payload_quad(const uint32_t *base32, uint64_t lim32, uint64_t start, uint32_t len,
+                                             int64_t q0, uint32_t (&o)[4])
+{
+    const uint64_t a4 = start + (uint64_t)(q0 + 16);  // first byte's address + 16 (q0 >= -15)
+    const uint64_t w4 = a4 >> 2;                       // its dword index + 4
+    const uint32_t sh = (uint32_t)(a4 & 3u);
+    uint32_t d[5];
+    if (w4 >= 4 && w4 + 1 <= lim32) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(base32 + (w4 - 4));
+        d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
+        d[4] = w4 < lim32 ? base32[w4] : 0u;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const uint64_t w = w4 - 4 + i;  // may wrap below zero: then >= lim32 and read as 0
+            d[i] = (w4 + i >= 4 && w < lim32) ? base32[w] : 0u;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t v = sh ? __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) : d[i];
+        o[i] = v & byte_mask(q0 + 4 * i, len);
+    }
+}
+
 // header bytes [4k, 4k + 4) of an H-byte header packed little-endian into h[0..3]
 __device__ __forceinline__ uint32_t header_dword(const uint32_t (&h)[4], uint32_t H, uint64_t k)
 {
@@ -83,7 +111,7 @@ __global__ void __launch_bounds__(kFrameBlock) align_kernel(uint64_t G, uint32_t
 
 // ---- framing: one dword of one shard slot per item ----------------------------------------------------
 struct FrameArgs {
-    const uint32_t *src;
+    const uint32_t *__restrict__ src;
     uint64_t src_dw;
     const uint64_t *off;
     const uint16_t *len;
@@ -92,27 +120,57 @@ struct FrameArgs {
     uint8_t *data;
     uint8_t *parity;
     uint64_t pitch;
-    uint64_t total;  // G * S * cols
+    uint64_t rows;  // G * S
     uint32_t S, K, R, cols;
 };
 
+// Half a wave (32 lanes) per row: a 1,444-byte shard slot is 91 chunks of 16 B = 32 + 32 + 27, so lanes stay
+// busy (one row per 64 lanes would leave the second pass 42% occupied).
+constexpr uint32_t kRowLanes = 32;
+constexpr uint32_t kRowsPerBlock = kFrameBlock / kRowLanes;
+
+__device__ __forceinline__ uint32_t row_in_block() { return threadIdx.x / kRowLanes; }
+
+// Write dwords [0, nd) of one row: an H-byte header followed by payload bytes [0, len) of base[start..],
+// zero after the payload.  Lane l of the row's 32 writes 16-byte chunks l, l + 32, ...; a row's last chunk, when it is
+// partial, is written dword by dword so that nothing past dword nd is touched.
+__device__ __forceinline__ void store_quads(uint32_t *__restrict__ dst, uint32_t nd, const uint32_t (&h)[4], uint32_t H,
+                                            const uint32_t *__restrict__ base, uint64_t lim32, uint64_t start,
+                                            uint32_t len, uint32_t lane)
+{
+    for (uint32_t j = lane; 4 * j < nd; j += kRowLanes) {
+        uint32_t o[4];
+        payload_quad(base, lim32, start, len, (int64_t)(16 * j) - H, o);
+        if (j == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] |= header_dword(h, H, i);
+        }
+        if (4 * j + 4 <= nd) {
+            *reinterpret_cast<uint4 *>(dst + 4 * j) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (4 * j + i < nd) dst[4 * j + i] = o[i];
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kFrameBlock) frame_kernel(FrameArgs a)
 {
-    for (uint64_t it = blockIdx.x * (uint64_t)kFrameBlock + threadIdx.x; it < a.total;
-         it += (uint64_t)gridDim.x * kFrameBlock) {
-        const uint64_t slot = it / a.cols, k = it - slot * a.cols;
+    const uint32_t lane = threadIdx.x % kRowLanes;
+    for (uint64_t slot = (uint64_t)blockIdx.x * kRowsPerBlock + row_in_block(); slot < a.rows;
+         slot += (uint64_t)gridDim.x * kRowsPerBlock) {
         const uint64_t g = slot / a.S;
         const uint32_t s = (uint32_t)(slot - g * a.S);
         if (a.present && !((a.present[g * 4 + (s >> 6)] >> (s & 63)) & 1ull)) continue;
-        uint8_t *dst = s < a.K ? a.data + (g * a.K + s) * a.pitch : a.parity + (g * a.R + (s - a.K)) * a.pitch;
-        uint32_t v = 0;
-        if (a.align[g] != 0) {
-            const uint32_t n = a.len[slot];
-            const uint32_t H = s < a.K ? KFEC_FEC_CONTAINER_HEADER : 0u;
-            const uint32_t h[4] = {(n >> 8) | ((n & 0xFFu) << 8), 0u, 0u, 0u};  // htons(length)
-            v = header_dword(h, H, k) | payload_dword(a.src, a.src_dw, a.off[slot], n, (int64_t)(4 * k) - H);
-        }
-        reinterpret_cast<uint32_t *>(dst)[k] = v;
+        uint32_t *dst = reinterpret_cast<uint32_t *>(s < a.K ? a.data + (g * a.K + s) * a.pitch
+                                                             : a.parity + (g * a.R + (s - a.K)) * a.pitch);
+        const bool ok = a.align[g] != 0;
+        const uint32_t n = ok ? a.len[slot] : 0u;
+        const uint64_t off = ok ? a.off[slot] : 0u;
+        const uint32_t H = (ok && s < a.K) ? KFEC_FEC_CONTAINER_HEADER : 0u;
+        const uint32_t h[4] = {(n >> 8) | ((n & 0xFFu) << 8), 0u, 0u, 0u};  // htons(length)
+        store_quads(dst, a.cols, h, H, a.src, a.src_dw, off, n, lane);
     }
 }
 
@@ -122,15 +180,15 @@ struct UnframeArgs {
     const uint8_t *out_idx;
     uint16_t *rec_len;
     uint8_t *dst;
-    uint64_t pitch, dst_pitch, total;
-    uint32_t R, B, cols;
+    uint64_t pitch, dst_pitch, rows;
+    uint32_t R, B;
 };
 
 __global__ void __launch_bounds__(kFrameBlock) unframe_kernel(UnframeArgs a)
 {
-    for (uint64_t it = blockIdx.x * (uint64_t)kFrameBlock + threadIdx.x; it < a.total;
-         it += (uint64_t)gridDim.x * kFrameBlock) {
-        const uint64_t slot = it / a.cols, k = it - slot * a.cols;
+    const uint32_t lane = threadIdx.x % kRowLanes;
+    for (uint64_t slot = (uint64_t)blockIdx.x * kRowsPerBlock + row_in_block(); slot < a.rows;
+         slot += (uint64_t)gridDim.x * kRowsPerBlock) {
         const uint32_t *s32 = reinterpret_cast<const uint32_t *>(a.out + slot * a.pitch);
         uint32_t n = 0xFFFFu;
         if (a.out_idx[slot] != 0xFF) {
@@ -138,16 +196,17 @@ __global__ void __launch_bounds__(kFrameBlock) unframe_kernel(UnframeArgs a)
             n = ((d0 & 0xFFu) << 8) | ((d0 >> 8) & 0xFFu);  // ntohs(data_length)
             if (n + KFEC_FEC_CONTAINER_HEADER > a.B) n = 0xFFFFu;
         }
-        if (k == 0) a.rec_len[slot] = (uint16_t)n;
-        if (a.dst && n != 0xFFFFu && 4 * k < n)
-            reinterpret_cast<uint32_t *>(a.dst + slot * a.dst_pitch)[k] =
-                payload_dword(s32, a.pitch / 4, KFEC_FEC_CONTAINER_HEADER, n, (int64_t)(4 * k));
+        if (lane == 0) a.rec_len[slot] = (uint16_t)n;
+        if (!a.dst || n == 0xFFFFu) continue;
+        uint32_t *dst = reinterpret_cast<uint32_t *>(a.dst + slot * a.dst_pitch);
+        const uint32_t h0[4] = {0u, 0u, 0u, 0u};
+        store_quads(dst, (n + 3) / 4, h0, 0u, s32, a.pitch / 4, KFEC_FEC_CONTAINER_HEADER, n, lane);
     }
 }
 
 // ---- wire packets ---------------------------------------------------------------------------------------
 struct PackArgs {
-    const uint32_t *src;
+    const uint32_t *__restrict__ src;
     uint64_t src_dw;
     const uint64_t *off;
     const uint16_t *len;
@@ -156,15 +215,15 @@ struct PackArgs {
     const uint32_t *sn, *conv;
     uint8_t *pkt;
     uint16_t *pkt_len;
-    uint64_t pitch, pkt_pitch, total;
-    uint32_t K, N, cols, which, timestamp;
+    uint64_t pitch, pkt_pitch, rows;
+    uint32_t K, N, which, timestamp;
 };
 
 __global__ void __launch_bounds__(kFrameBlock) pack_kernel(PackArgs a)
 {
-    for (uint64_t it = blockIdx.x * (uint64_t)kFrameBlock + threadIdx.x; it < a.total;
-         it += (uint64_t)gridDim.x * kFrameBlock) {
-        const uint64_t pk = it / a.cols, k = it - pk * a.cols;
+    const uint32_t lane = threadIdx.x % kRowLanes;
+    for (uint64_t pk = (uint64_t)blockIdx.x * kRowsPerBlock + row_in_block(); pk < a.rows;
+         pk += (uint64_t)gridDim.x * kRowsPerBlock) {
         const uint64_t g = pk / a.N;
         const uint32_t s = (uint32_t)(pk - g * a.N);
         const bool red = s >= a.K;
@@ -172,28 +231,27 @@ __global__ void __launch_bounds__(kFrameBlock) pack_kernel(PackArgs a)
         const uint32_t H = red ? KFEC_PKT_REDUNDANT_HEADER : KFEC_PKT_DATA_HEADER;
         const uint32_t n = red ? a.align[g] : a.len[g * a.K + s];
         const bool fits = H + n <= a.pkt_pitch && !(red && n == 0);
-        if (k == 0) a.pkt_len[pk] = fits ? (uint16_t)(H + n) : (uint16_t)0;
-        if (!fits || 4 * k >= H + n) continue;
-        const uint32_t sn = bswap32(a.sn[g]);  // htonl
+        if (lane == 0) a.pkt_len[pk] = fits ? (uint16_t)(H + n) : (uint16_t)0;
+        if (!fits) continue;
         uint32_t h[4];
-        h[0] = a.timestamp;  // host_to_little_endian
-        h[1] = sn;
+        h[0] = a.timestamp;      // host_to_little_endian
+        h[1] = bswap32(a.sn[g]);  // htonl
+        const uint32_t cv = red ? bswap32(a.conv[g]) : 0u;
+        h[2] = s | (cv << 8);
+        h[3] = cv >> 24;
+        const uint32_t *base;
+        uint64_t lim, off;
         if (red) {
-            const uint32_t cv = bswap32(a.conv[g]);
-            h[2] = s | (cv << 8);
-            h[3] = cv >> 24;
+            base = reinterpret_cast<const uint32_t *>(a.parity + (g * (a.N - a.K) + (s - a.K)) * a.pitch);
+            lim = a.pitch / 4;
+            off = 0;
         } else {
-            h[2] = s;
-            h[3] = 0;
+            base = a.src;
+            lim = a.src_dw;
+            off = a.off[g * a.K + s];
         }
-        uint32_t p;
-        if (red) {
-            const uint8_t *slot = a.parity + (g * (a.N - a.K) + (s - a.K)) * a.pitch;
-            p = payload_dword(reinterpret_cast<const uint32_t *>(slot), a.pitch / 4, 0, n, (int64_t)(4 * k) - H);
-        } else {
-            p = payload_dword(a.src, a.src_dw, a.off[g * a.K + s], n, (int64_t)(4 * k) - H);
-        }
-        reinterpret_cast<uint32_t *>(a.pkt + pk * a.pkt_pitch)[k] = header_dword(h, H, k) | p;
+        uint32_t *dst = reinterpret_cast<uint32_t *>(a.pkt + pk * a.pkt_pitch);
+        store_quads(dst, (H + n + 3) / 4, h, H, base, lim, off, n, lane);
     }
 }
 
@@ -270,6 +328,11 @@ uint32_t grid_for(uint64_t total)
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((total + kFrameBlock - 1) / kFrameBlock, kMaxGrid));
 }
 
+uint32_t grid_rows(uint64_t rows)
+{
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((rows + kRowsPerBlock - 1) / kRowsPerBlock, kMaxGrid));
+}
+
 int launched() { return hipGetLastError() == hipSuccess ? 0 : -3; }
 
 }  // namespace
@@ -297,8 +360,8 @@ int launch_frame(int K, int N, bool recv, size_t G, const void *src, size_t src_
     a.K = K;
     a.R = N - K;
     a.cols = (uint32_t)((B + 3) / 4);
-    a.total = (uint64_t)G * S * a.cols;
-    hipLaunchKernelGGL(frame_kernel, dim3(grid_for(a.total)), dim3(kFrameBlock), 0, s, a);
+    a.rows = (uint64_t)G * S;
+    hipLaunchKernelGGL(frame_kernel, dim3(grid_rows(a.rows)), dim3(kFrameBlock), 0, s, a);
     return launched();
 }
 
@@ -316,9 +379,8 @@ int launch_unframe(int K, int N, size_t G, size_t B, size_t pitch, const void *o
     a.dst_pitch = dst_pitch;
     a.R = R;
     a.B = (uint32_t)B;
-    a.cols = (uint32_t)std::max<size_t>(1, (B + 1) / 4);  // ceil((B - 2) / 4) dwords of datagram, >= 1 for the length
-    a.total = (uint64_t)G * R * a.cols;
-    hipLaunchKernelGGL(unframe_kernel, dim3(grid_for(a.total)), dim3(kFrameBlock), 0, s, a);
+    a.rows = (uint64_t)G * R;
+    hipLaunchKernelGGL(unframe_kernel, dim3(grid_rows(a.rows)), dim3(kFrameBlock), 0, s, a);
     return launched();
 }
 
@@ -345,9 +407,8 @@ int launch_pack(int K, int N, size_t G, unsigned which, const void *src, size_t 
     a.N = N;
     a.which = which;
     a.timestamp = timestamp;
-    a.cols = (uint32_t)(pkt_pitch / 4);
-    a.total = (uint64_t)G * N * a.cols;
-    hipLaunchKernelGGL(pack_kernel, dim3(grid_for(a.total)), dim3(kFrameBlock), 0, s, a);
+    a.rows = (uint64_t)G * N;
+    hipLaunchKernelGGL(pack_kernel, dim3(grid_rows(a.rows)), dim3(kFrameBlock), 0, s, a);
     return launched();
 }
 
