@@ -121,6 +121,32 @@ int kfec_group_scatter(const kfec_ctx *ctx, size_t P, const kfec_pkt_hdr *d_hdr,
                        uint32_t sn_base, size_t G, uint64_t *d_present, uint64_t *d_off, uint16_t *d_len,
                        void *stream);
 
+/* ---- packet integrity for the non-AEAD encryption modes (rank 4) -----------------------------------------
+ * encrypt_data / decrypt_data (data_operations.cpp:171-234, 373-435) for encryption=none and plain_xor:
+ * a 2-byte checksum16 (simple_hashing.hpp:10-25: CRC-32 -- Botan "CRC32", stored big-endian -- with its two
+ * 16-bit halves XORed) is appended to the packet, and plain_xor then runs xor_forward
+ * (data_operations.cpp:120-128) over packet + checksum; opening runs xor_backward (:140-148) and compares.
+ * The AEAD modes need Botan and are not provided.  These calls do not depend on a coder: they run on the
+ * current HIP device. */
+#define KFEC_SEAL_TRAILER 2     /* constant_values::iv_checksum_block_size, share_defines.hpp:41 */
+#define KFEC_SEAL_CHECKSUM 0    /* encryption_mode none (encrypt_data's default branch) */
+#define KFEC_SEAL_PLAIN_XOR 1   /* encryption_mode plain_xor */
+
+/* Seal P packets [d_off[p], +d_len[p]) of d_src into d_dst + p * dst_pitch (dst_pitch % 4 == 0):
+ * data || checksum16(data), xor_forward'ed for plain_xor.  d_out_len[p] = len + 2, or 0 for an empty packet
+ * (encrypt_data returns "empty data") or one that does not fit in dst_pitch.  Bytes after the sealed packet
+ * up to the next multiple of 4 are written as zero. */
+int kfec_seal_batch(int mode, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
+                    const uint32_t *d_len, void *d_dst, size_t dst_pitch, uint32_t *d_out_len, void *stream);
+
+/* Open P sealed packets: (plain_xor: xor_backward, then) split off the 2-byte trailer and compare it with
+ * checksum16 of the rest.  d_dst + p * dst_pitch receives the len - 2 plaintext bytes (zero-padded to a
+ * multiple of 4), d_out_len[p] = len - 2 and d_ok[p] = 1 when the checksum matches, 0 when it does not
+ * (decrypt_data's "checksum incorrect"); packets of <= 2 bytes get d_out_len = 0, d_ok = 0. */
+int kfec_open_batch(int mode, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
+                    const uint32_t *d_len, void *d_dst, size_t dst_pitch, uint32_t *d_out_len, uint8_t *d_ok,
+                    void *stream);
+
 #ifdef __cplusplus
 }
 #endif

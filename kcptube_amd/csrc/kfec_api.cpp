@@ -365,4 +365,32 @@ int kfec_group_scatter(const kfec_ctx *ctx, size_t P, const kfec_pkt_hdr *d_hdr,
                : KFEC_OK;
 }
 
+int kfec_seal_batch(int mode, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
+                    const uint32_t *d_len, void *d_dst, size_t dst_pitch, uint32_t *d_out_len, void *stream)
+{
+    if ((mode != KFEC_SEAL_CHECKSUM && mode != KFEC_SEAL_PLAIN_XOR) || dst_pitch % 4) return KFEC_EINVAL;
+    if (P && (!d_src || !al4(d_src) || !d_off || !d_len || !d_dst || !al4(d_dst) || !d_out_len)) return KFEC_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return KFEC_ENODEV;
+    return kfec::launch_seal(false, mode, P, d_src, src_bytes, d_off, d_len, d_dst, dst_pitch, d_out_len, nullptr,
+                             as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
+int kfec_open_batch(int mode, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
+                    const uint32_t *d_len, void *d_dst, size_t dst_pitch, uint32_t *d_out_len, uint8_t *d_ok,
+                    void *stream)
+{
+    if ((mode != KFEC_SEAL_CHECKSUM && mode != KFEC_SEAL_PLAIN_XOR) || dst_pitch % 4) return KFEC_EINVAL;
+    if (P && (!d_src || !al4(d_src) || !d_off || !d_len || !d_dst || !al4(d_dst) || !d_out_len || !d_ok))
+        return KFEC_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return KFEC_ENODEV;
+    return kfec::launch_seal(true, mode, P, d_src, src_bytes, d_off, d_len, d_dst, dst_pitch, d_out_len, d_ok,
+                             as_stream(stream))
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
 }  // extern "C"

@@ -87,6 +87,8 @@ def load_library():
                                       _vp, sz, _vp, _vp]),
         "kfec_unpack_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, _vp, _vp]),
         "kfec_group_scatter": (C.c_int, [_vp, sz, _vp, _vp, C.c_uint32, sz, _vp, _vp, _vp, _vp]),
+        "kfec_seal_batch": (C.c_int, [C.c_int, sz, _vp, sz, _vp, _vp, _vp, sz, _vp, _vp]),
+        "kfec_open_batch": (C.c_int, [C.c_int, sz, _vp, sz, _vp, _vp, _vp, sz, _vp, _vp, _vp]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name)

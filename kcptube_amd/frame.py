@@ -12,6 +12,8 @@ create_fec_data_packet / create_fec_redundant_packet                   ``FecFram
 (src/networks/connections.cpp:395-430)
 unpack_fec / unpack_fec_redundant (connections.cpp:488-511)            ``FecFrame.unpack``
 fec_rcv_cache[sn][sub_sn] = payload (src/modes/client.cpp:851-892)      ``FecFrame.scatter``
+encrypt_data / decrypt_data, modes none and plain_xor                  ``seal`` / ``open_``
+(src/shares/data_operations.cpp:171-234, 373-435)
 =====================================================================  ==========================================
 
 Everything runs as gfx950 kernels on device-resident ``torch`` tensors; no CPU path.  Shard slot padding is
@@ -21,13 +23,14 @@ from __future__ import annotations
 
 import numpy as np
 
-from .fec import FecCode, _check, _dptr, _stream_handle
+from .fec import FecCode, _check, _dptr, _stream_handle, load_library
 
 FEC_CONTAINER_HEADER = 2
 PKT_DATA_HEADER = 9
 PKT_REDUNDANT_HEADER = 13
 FEC_WAITS = 3
 PACK_DATA, PACK_REDUNDANT = 1, 2
+SEAL_TRAILER, SEAL_CHECKSUM, SEAL_PLAIN_XOR = 2, 0, 1
 KIND_DATA, KIND_REDUNDANT, KIND_MALFORMED = 0, 1, 255
 
 # struct kfec_pkt_hdr (include/kfec_frame.h), 24 bytes
@@ -107,3 +110,19 @@ class FecFrame:
         _check(self._lib.kfec_group_scatter(self.code._ctx, P, _dptr(hdr), _dptr(slot), sn_base & 0xFFFFFFFF, G,
                                             _dptr(present), _dptr(off), _dptr(length), _stream_handle(stream)),
                "kfec_group_scatter")
+
+
+def seal(mode: int, src, off, length, dst, out_len, stream=None) -> None:
+    """encrypt_data (none / plain_xor) for P packets [off[p], off[p] + length[p]) of src (length int32 [P]):
+    dst [P][dst_pitch] receives data || checksum16 (xor_forward'ed for plain_xor), out_len int32 [P]."""
+    P = off.numel()
+    _check(load_library().kfec_seal_batch(mode, P, _dptr(src), src.numel(), _dptr(off), _dptr(length), _dptr(dst),
+                                          dst.shape[-1], _dptr(out_len), _stream_handle(stream)), "kfec_seal_batch")
+
+
+def open_(mode: int, src, off, length, dst, out_len, ok, stream=None) -> None:
+    """decrypt_data (none / plain_xor): plaintext to dst [P][dst_pitch], out_len int32 [P], ok uint8 [P]."""
+    P = off.numel()
+    _check(load_library().kfec_open_batch(mode, P, _dptr(src), src.numel(), _dptr(off), _dptr(length), _dptr(dst),
+                                          dst.shape[-1], _dptr(out_len), _dptr(ok), _stream_handle(stream)),
+           "kfec_open_batch")

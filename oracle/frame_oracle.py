@@ -12,6 +12,10 @@ Restated (pure Python byte work, small cases only), with the reference lines eac
 * ``redundant_packet``  packet::create_fec_redundant_packet  src/networks/connections.cpp:413-430
 * ``unpack_fec``        packet::unpack_fec                   src/networks/connections.cpp:488-498
 * ``unpack_redundant``  packet::unpack_fec_redundant         src/networks/connections.cpp:500-511
+* ``checksum16``        simple_hashing::checksum16           src/shares/simple_hashing.hpp:10-25
+* ``xor_forward`` / ``xor_backward``                         src/shares/data_operations.cpp:120-148
+* ``seal`` / ``open_``  encrypt_data / decrypt_data, modes none and plain_xor
+                        src/shares/data_operations.cpp:171-234, 373-435
 * ``FecTx``             client_mode::fec_maker               src/modes/client.cpp:797-840
 * ``FecRx``             client_mode::fec_unpack + fec_find_missings  src/modes/client.cpp:842-938
                         (server.cpp:977-1020 and relay.cpp:1384-1428 are the same logic)
@@ -26,6 +30,11 @@ a shard slot is ZERO (the reference leaves it uninitialised: make_unique_for_ove
 data_operations.cpp:618 and :651), and packets shorter than their header are rejected
 (the reference's ``length - header`` would wrap).
 
+checksum16 is Botan's "CRC32" (the standard reflected CRC-32, the one zlib.crc32 computes), written out
+big-endian by Botan's CRC32::final_result, then ``*(uint16_t*)out = *(uint16_t*)crc ^ *(uint16_t*)(crc+2)``
+on a little-endian host.  Botan is absent here, so that byte order is restated from Botan's source, not
+run: parity unpinned for rank 4 as for the rest of this file.
+
 Parity status: the framing and packet functions live in data_operations.cpp / connections.cpp, which need
 asio (absent from this image), so the reference cannot be compiled here and its repository holds no tests
 or fixtures for them: this restatement is **parity unpinned** against the reference binary.  It is
@@ -35,6 +44,7 @@ pinned coder oracle (framed groups encode -> erase -> decode -> extract back to 
 from __future__ import annotations
 
 import struct
+import zlib
 
 FEC_CONTAINER_HEADER = 2  # share_defines.hpp:46
 DATA_HEADER = 9           # sizeof(packet_layer_data) - 1
@@ -128,6 +138,50 @@ def parse_packet(pkt: bytes, K: int) -> dict | None:
     ts, sn, sub, payload = unpack_fec(pkt)
     return {"timestamp": ts, "sn": sn, "sub_sn": sub, "conv": kcp_conv(payload), "payload": payload,
             "redundant": False}
+
+
+SEAL_CHECKSUM, SEAL_PLAIN_XOR = 0, 1
+
+
+def checksum16(data: bytes) -> bytes:
+    """simple_hashing::checksum16 (simple_hashing.hpp:17-24): CRC-32 stored big-endian, halves XORed."""
+    c = zlib.crc32(bytes(data)) & 0xFFFFFFFF
+    be = c.to_bytes(4, "big")
+    return bytes([be[0] ^ be[2], be[1] ^ be[3]])
+
+
+def xor_forward(data: bytes) -> bytes:
+    """data[i] ^= data[i + 1], i ascending (data_operations.cpp:120-128)."""
+    b = bytearray(data)
+    for i in range(len(b) - 1):
+        b[i] ^= b[i + 1]
+    return bytes(b)
+
+
+def xor_backward(data: bytes) -> bytes:
+    """data[i - 1] ^= data[i], i descending (data_operations.cpp:140-148)."""
+    b = bytearray(data)
+    for i in range(len(b) - 1, 0, -1):
+        b[i - 1] ^= b[i]
+    return bytes(b)
+
+
+def seal(data: bytes, mode: int) -> bytes | None:
+    """encrypt_data for encryption none / plain_xor (data_operations.cpp:171-234); None for empty data."""
+    if len(data) <= 0:
+        return None
+    out = bytes(data) + checksum16(data)
+    return xor_forward(out) if mode == SEAL_PLAIN_XOR else out
+
+
+def open_(packet: bytes, mode: int) -> tuple[bytes, bool] | None:
+    """decrypt_data for encryption none / plain_xor (data_operations.cpp:373-435): (plaintext, checksum ok);
+    None for packets of <= 2 bytes ("incorrect data length")."""
+    if len(packet) <= 2:
+        return None
+    b = xor_backward(packet) if mode == SEAL_PLAIN_XOR else bytes(packet)
+    body, trailer = b[:-2], b[-2:]
+    return body, checksum16(body) == trailer
 
 
 class FecTx:

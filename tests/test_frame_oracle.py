@@ -146,3 +146,35 @@ def test_restored_group_decoded_once():
         rx.push(fo.data_packet(b"d", 0, sub, 0) if sub < 2 else fo.redundant_packet(b"\0\0\0", 0, sub, 1, 0))
     assert calls == [[0, 1]]  # decoded when the 2nd share arrived, never again
     assert 0 in rx.restored
+
+
+# ---- rank 4: checksum16 and the non-AEAD encryption modes --------------------------------------------------
+def test_checksum16_known_answer():
+    # CRC-32 check value: crc32("123456789") = 0xCBF43926, stored big-endian CB F4 39 26 -> [CB^39, F4^26]
+    assert fo.checksum16(b"123456789") == bytes([0xCB ^ 0x39, 0xF4 ^ 0x26])
+    assert fo.checksum16(b"") == b"\x00\x00"  # crc32("") = 0
+
+
+def test_xor_forward_backward_inverse():
+    rng = random.Random(3)
+    for n in (1, 2, 3, 7, 64, 1443):
+        d = rng.randbytes(n)
+        assert fo.xor_backward(fo.xor_forward(d)) == d
+    assert fo.xor_forward(b"\x01\x02\x04") == b"\x03\x06\x04"
+    assert fo.xor_backward(b"\x03\x06\x04") == b"\x01\x02\x04"
+
+
+@pytest.mark.parametrize("mode", [fo.SEAL_CHECKSUM, fo.SEAL_PLAIN_XOR])
+def test_seal_open_roundtrip_and_corruption(mode):
+    rng = random.Random(mode)
+    for n in (1, 2, 3, 4, 5, 100, 1440):
+        d = rng.randbytes(n)
+        s = fo.seal(d, mode)
+        assert len(s) == n + 2
+        assert fo.open_(s, mode) == (d, True)
+        bad = bytearray(s)
+        bad[rng.randrange(len(bad))] ^= 0x10
+        body, ok = fo.open_(bytes(bad), mode)
+        assert not ok
+    assert fo.seal(b"", mode) is None
+    assert fo.open_(b"\x00\x00", mode) is None

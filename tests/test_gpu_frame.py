@@ -374,3 +374,67 @@ def test_device_pipeline_end_to_end(dev, oracle):
     exp = [dgs[g * K + s] for g, s in keep if s < K]
     exp += [gd[g, t, :rl[g, t]].tobytes() for g in range(G) for t in range(R) if ix[g, t] != 0xFF]
     assert sorted(got) == sorted(exp)
+
+
+@pytest.mark.parametrize("mode", [fo.SEAL_CHECKSUM, fo.SEAL_PLAIN_XOR])
+def test_seal_open_match_oracle(dev, mode):
+    """encrypt_data / decrypt_data (none, plain_xor) on the device vs the restatement: ragged lengths at odd
+    offsets, empty / 1-3 byte packets, corrupted packets (checksum must fail), and a full round trip."""
+    from kcptube_amd.frame import open_, seal
+    rng = random.Random(100 + mode)
+    pk = [b"", b"\x01", b"ab", b"abc", b"1234"] + [rng.randbytes(rng.choice([5, 1440, 1442, rng.randint(1, 1500)]))
+                                                   for _ in range(400)]
+    src, off, lens = _arena(pk, dev)
+    P = len(pk)
+    pitch = 1504
+    d_len = torch.tensor(lens, dtype=torch.int32, device=dev)
+    dst = torch.full((P, pitch), SENT, dtype=torch.uint8, device=dev)
+    olen = torch.full((P,), -1, dtype=torch.int32, device=dev)
+    seal(mode, src, off, d_len, dst, olen)
+    torch.cuda.synchronize()
+    gd, ol = dst.cpu().numpy(), olen.cpu().numpy()
+    sealed = []
+    for p, d in enumerate(pk):
+        exp = fo.seal(d, mode)
+        if exp is None or len(exp) > pitch:
+            assert ol[p] == 0
+            sealed.append(b"")
+            continue
+        n = len(exp)
+        assert ol[p] == n
+        assert gd[p, :n].tobytes() == exp, p
+        n4 = (n + 3) // 4 * 4
+        assert not gd[p, n:n4].any() and (gd[p, n4:] == SENT).all()
+        sealed.append(exp)
+    # open: the sealed packets, a third of them with one flipped byte, plus short ones
+    rx = []
+    for p, s in enumerate(sealed):
+        if s and p % 3 == 0:
+            b = bytearray(s)
+            b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+            s = bytes(b)
+        rx.append(s)
+    rx += [b"\x00", b"\x00\x00", b"\x00\x00\x01"]
+    src2, off2, lens2 = _arena(rx, dev)
+    Q = len(rx)
+    dst2 = torch.full((Q, pitch), SENT, dtype=torch.uint8, device=dev)
+    olen2 = torch.full((Q,), -1, dtype=torch.int32, device=dev)
+    ok = torch.full((Q,), 7, dtype=torch.uint8, device=dev)
+    open_(mode, src2, off2, torch.tensor(lens2, dtype=torch.int32, device=dev), dst2, olen2, ok)
+    torch.cuda.synchronize()
+    g2, l2, k2 = dst2.cpu().numpy(), olen2.cpu().numpy(), ok.cpu().numpy()
+    n_bad = 0
+    for p, s in enumerate(rx):
+        exp = fo.open_(s, mode)
+        if exp is None:
+            assert l2[p] == 0 and k2[p] == 0
+            continue
+        body, good = exp
+        assert l2[p] == len(body) and k2[p] == int(good), p
+        assert g2[p, :len(body)].tobytes() == body, p
+        n4 = (len(body) + 3) // 4 * 4
+        assert not g2[p, len(body):n4].any() and (g2[p, n4:] == SENT).all()
+        n_bad += not good
+        if p < len(pk) and p % 3 != 0 and pk[p]:
+            assert good and body == pk[p]
+    assert n_bad > 100
