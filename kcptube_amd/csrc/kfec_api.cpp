@@ -48,7 +48,7 @@ int build_matrix(kfec_ctx *c)
     const size_t bytes = c->N * c->K;
     if (c->d_enc) (void)hipFree(c->d_enc);
     c->d_enc = nullptr;
-    if (hipMalloc(&c->d_enc, bytes) != hipSuccess) return KFEC_ENOMEM;
+    if (hipMalloc(&c->d_enc, kfec::enc_alloc_bytes(c->K, c->N)) != hipSuccess) return KFEC_ENOMEM;
     if (kfec::launch_build_matrix(c->d_enc, (int)c->K, (int)c->N, c->stream)) return KFEC_EHIP;
     c->h_enc.assign(bytes, 0);
     if (hipMemcpyAsync(c->h_enc.data(), c->d_enc, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess)

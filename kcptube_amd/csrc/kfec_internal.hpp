@@ -17,6 +17,13 @@ namespace kfec {
 inline size_t rec_k4(size_t K) { return (K + 3) & ~size_t(3); }
 inline size_t record_stride(size_t K, size_t R) { return (4 + rec_k4(K) + R * rec_k4(K) + 15) & ~size_t(15); }
 
+// The encoding matrix allocation also holds the perm-MAC tables of its parity rows (gf_perm_tables, 5 dwords
+// per coefficient) for the encode kernel, laid out [K][R + 8][5]: shard-major so that the rows of one shard
+// are contiguous (scalar loads), with 8 zero rows of slack for any row tile's overshoot.
+__host__ __device__ inline size_t enc_tab_rows(size_t R) { return R + 8; }
+__host__ __device__ inline size_t enc_tab_offset(size_t K, size_t N) { return (N * K + 255) & ~size_t(255); }
+inline size_t enc_alloc_bytes(size_t K, size_t N) { return enc_tab_offset(K, N) + K * enc_tab_rows(N - K) * 5 * 4; }
+
 struct DeviceInfo {
     int device = -1;
     int cus = 0;

@@ -66,6 +66,12 @@ static constexpr int kBlock = 256;
 #ifndef KFEC_MINW
 #define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the flattened kernel
 #endif
+#ifndef KFEC_SGPR_TABLES
+#define KFEC_SGPR_TABLES 0  // encode reads its perm tables with scalar loads instead of LDS (KFEC_SGPR_TABLES env)
+#endif
+#ifndef KFEC_XCD_REMAP
+#define KFEC_XCD_REMAP 0  // XCD-contiguous workgroup numbering in the flattened kernel (A/B knob)
+#endif
 #ifndef KFEC_NTSTORE
 #define KFEC_NTSTORE 1  // nontemporal output stores in the flattened kernel (+2.5% encode, measured)
 #endif
@@ -152,10 +158,28 @@ __global__ void __launch_bounds__(kBlock) build_matrix_kernel(uint8_t *enc, int 
     enc[idx] = s_exp[e];
 }
 
+// perm-MAC tables of the parity rows for the encode kernel: etab[j][r][0..5) = gf_perm_tables(enc[K + r][j])
+// (zero for the slack rows r >= R)
+__global__ void __launch_bounds__(kBlock) build_enc_tables_kernel(const uint8_t *enc, int K, int N, uint32_t *etab)
+{
+    const int R = N - K, rows = (int)enc_tab_rows(R);
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= K * rows) return;
+    const int j = idx / rows, r = idx - j * rows;
+    uint32_t t[5];
+    gf_perm_tables(r < R ? enc[(K + r) * K + j] : 0u, t);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) etab[(size_t)idx * 5 + i] = t[i];
+}
+
 int launch_build_matrix(uint8_t *d_enc, int K, int N, hipStream_t s)
 {
     const int total = N * K;
     hipLaunchKernelGGL(build_matrix_kernel, dim3((total + kBlock - 1) / kBlock), dim3(kBlock), 0, s, d_enc, K, N);
+    if (hipGetLastError() != hipSuccess) return -3;
+    const int nt = K * (int)enc_tab_rows(N - K);
+    uint32_t *etab = reinterpret_cast<uint32_t *>(d_enc + enc_tab_offset(K, N));
+    hipLaunchKernelGGL(build_enc_tables_kernel, dim3((nt + kBlock - 1) / kBlock), dim3(kBlock), 0, s, d_enc, K, N, etab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -666,6 +690,8 @@ struct MacArgs {
     uint32_t rec_stride;
     uint32_t JC;            // shards per LDS chunk
     uint32_t gmax;          // group slots per chunk
+    const uint32_t *etab;   // encode: perm tables [K][etab_rows][5] read with scalar loads (null: LDS path)
+    uint32_t etab_rows;
 };
 
 template <int VEC>
@@ -804,13 +830,24 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
 
     const uint32_t row0 = blockIdx.y * MT;
     const uint32_t K = a.K, cols = a.cpad;
-    const bool enc_once = !DEC && K <= a.JC;
-    if (enc_once) {
+    const bool gtab = !DEC && a.etab != nullptr;  // encode: wave-uniform tables straight from memory
+    const bool enc_once = !DEC && (gtab || K <= a.JC);
+    if (enc_once && !gtab) {
         mac_expand<MT, false>(a, s_ent, 0, 1, 0, K, row0);
         __syncthreads();
     }
     const uint32_t stride = gridDim.x * kBlock;
-    for (uint32_t base = blockIdx.x * kBlock; base < a.total; base += stride) {
+    // XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs, so workgroup b would run
+    // next to b+8, not b+1.  Re-numbering (bijective, MI355X guide T1) gives each XCD a contiguous run of
+    // items, so the 128-B lines that straddle two workgroups' columns are fetched by one L2, not two.
+    uint32_t wg = blockIdx.x;
+#if KFEC_XCD_REMAP
+    {
+        const uint32_t n = gridDim.x, q = n / 8, r = n % 8, x = wg % 8, i = wg / 8;
+        wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+    }
+#endif
+    for (uint32_t base = wg * kBlock; base < a.total; base += stride) {
         const uint32_t item = base + threadIdx.x;
         const uint32_t g = item < a.total ? item / cols : 0;
         const uint32_t col = item < a.total ? item - g * cols : 0;
@@ -879,11 +916,19 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
                                                     : load_gran<VEC>(share_ptr(jj + PD), col, a.B);
                         const uint8_t *ent = ent0 + sj(jj) * L::ENTRY;
                         uint32_t t[L::TBL_DW];
-                        const uint4 *tv = reinterpret_cast<const uint4 *>(ent + 16);
+                        if (gtab) {
+                            // uniform address in the constant address space: scalar loads into SGPRs, no LDS
+                            typedef const __attribute__((address_space(4))) uint32_t cu32;
+                            const cu32 *tg = (const cu32 *)(a.etab + ((size_t)(c0 + jj) * a.etab_rows + row0) * 5);
 #pragma unroll
-                        for (int i = 0; i < L::TBL_DW / 4; ++i) {
-                            const uint4 q = tv[i];
-                            t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+                            for (int i = 0; i < 5 * MT; ++i) t[i] = tg[i];
+                        } else {
+                            const uint4 *tv = reinterpret_cast<const uint4 *>(ent + 16);
+#pragma unroll
+                            for (int i = 0; i < L::TBL_DW / 4; ++i) {
+                                const uint4 q = tv[i];
+                                t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+                            }
                         }
 #pragma unroll
                         for (int w = 0; w < W; ++w) {
@@ -1704,7 +1749,7 @@ template <int VEC, int MT, bool DEC>
 static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
 {
     using L = MacLayout<MT>;
-    const size_t lds = (size_t)a.gmax * a.JC * L::ENTRY;
+    const size_t lds = a.etab ? 0 : (size_t)a.gmax * a.JC * L::ENTRY;
     // one workgroup per 256 items (non-persistent): the dispatcher refills each CU as workgroups retire.
     // Measured against a persistent grid sized to the resident workgroups (KFEC_GRID_PERSIST=1): encode
     // 6.90 -> 6.08 ms and decode 7.39 -> 6.75 ms at 20:3 B=1440 1M groups, 205 -> 173 ms encode at 200:55
@@ -2049,6 +2094,12 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.rec_stride = 0;
         a.JC = JC;
         a.gmax = 1;
+        static const int stab = env_int("KFEC_SGPR_TABLES", KFEC_SGPR_TABLES);
+        if (stab) {
+            a.etab = reinterpret_cast<const uint32_t *>(d_enc + enc_tab_offset(K, K + R));
+            a.etab_rows = (uint32_t)enc_tab_rows(R);
+            a.JC = K;
+        }
         return dispatch_mac<false>(di, vec, mt, a, tiles, s);
     });
 }
