@@ -183,9 +183,9 @@ int kfec_decode(const kfec_ctx *cctx, const size_t *share_ids, const uint8_t *co
     if (B == 0) return KFEC_OK;
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (set_dev(ctx)) return KFEC_EHIP;
-    const size_t rs = kfec::record_stride(K, R);
     const size_t o_data = 0, o_par = al256(K * B), o_out = o_par + al256(R * B), o_mask = o_out + al256(R * B);
-    const size_t o_idx = o_mask + 256, o_st = o_idx + al256(R + 1), o_rec = o_st + 256, total = o_rec + al256(rs);
+    const size_t o_idx = o_mask + 256, o_st = o_idx + al256(R + 1), o_rec = o_st + 256,
+                 total = o_rec + al256(kfec::decode_workspace_bytes(1, K, R));
     int rc = ensure_stage(ctx, total);
     if (rc) return rc;
     uint8_t *base = ctx->d_stage;
@@ -234,7 +234,7 @@ int kfec_encode_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, con
 
 size_t kfec_decode_workspace_size(const kfec_ctx *ctx, size_t G)
 {
-    return ctx ? G * kfec::record_stride(ctx->K, ctx->N - ctx->K) : 0;
+    return ctx ? kfec::decode_workspace_bytes(G, ctx->K, ctx->N - ctx->K) : 0;
 }
 
 int kfec_decode_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, const void *d_data,

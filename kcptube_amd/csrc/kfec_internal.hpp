@@ -16,6 +16,9 @@ namespace kfec {
 // with K4 = K rounded up to 4 so that the prep kernel writes whole dwords.
 inline size_t rec_k4(size_t K) { return (K + 3) & ~size_t(3); }
 inline size_t record_stride(size_t K, size_t R) { return (4 + rec_k4(K) + R * rec_k4(K) + 15) & ~size_t(15); }
+// after the G records: a uint32 count (+ 60 bytes of padding) and the uint32 work list of the decode MAC
+inline size_t decode_list_offset(size_t G, size_t K, size_t R) { return (G * record_stride(K, R) + 255) & ~size_t(255); }
+inline size_t decode_workspace_bytes(size_t G, size_t K, size_t R) { return decode_list_offset(G, K, R) + 64 + 4 * G; }
 
 // The encoding matrix allocation also holds the perm-MAC tables of its parity rows (gf_perm_tables, 5 dwords
 // per coefficient) for the encode kernel, laid out [K][R + 8][5]: shard-major so that the rows of one shard

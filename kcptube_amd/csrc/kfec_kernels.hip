@@ -692,6 +692,8 @@ struct MacArgs {
     uint32_t gmax;          // group slots per chunk
     const uint32_t *etab;   // encode: perm tables [K][etab_rows][5] read with scalar loads (null: LDS path)
     uint32_t etab_rows;
+    const uint32_t *list;   // decode: the groups with work (m > 0), ascending per wave; null = every group
+    const uint32_t *list_count;
 };
 
 template <int VEC>
@@ -794,7 +796,7 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
         uint32_t c = 0;
         if constexpr (DEC) {
             const uint32_t K4 = (a.K + 3) & ~3u;
-            const uint32_t g = gfirst + gs;
+            const uint32_t g = a.list ? a.list[gfirst + gs] : gfirst + gs;
             const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
             const uint32_t st = rec[0], m = rec[1];
             if (st == 0 && u < m) c = rec[4 + K4 + u * K4 + j];
@@ -847,18 +849,21 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
         wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
     }
 #endif
-    for (uint32_t base = wg * kBlock; base < a.total; base += stride) {
+    // decode with a work list: only the groups that lost data shards are visited (list index space)
+    const uint32_t total = (DEC && a.list) ? min(*a.list_count, a.G) * cols : a.total;
+    for (uint32_t base = wg * kBlock; base < total; base += stride) {
         const uint32_t item = base + threadIdx.x;
-        const uint32_t g = item < a.total ? item / cols : 0;
-        const uint32_t col = item < a.total ? item - g * cols : 0;
-        const bool in = item < a.total && col < a.cols;
+        const uint32_t gi = item < total ? item / cols : 0;  // list index (= group without a list)
+        const uint32_t col = item < total ? item - gi * cols : 0;
+        const bool in = item < total && col < a.cols;
+        const uint32_t g = (DEC && a.list) ? (item < total ? a.list[gi] : 0u) : gi;
         // dwords of this lane's granule below B: W except in the last granule of a row when VEC does not
         // divide B (VEC >= 4 only; the bytewise VEC = 1 path checks every byte itself)
         const uint32_t nd = (VEC >= 4 && (col + 1) * VB > a.B) ? (a.B - col * VB + 3) / 4 : (uint32_t)W;
         const uint32_t gfirst = base / cols;
-        const uint32_t glast = min(base + kBlock - 1, a.total - 1) / cols;
+        const uint32_t glast = min(base + kBlock - 1, total - 1) / cols;
         const uint32_t ng = glast - gfirst + 1;
-        const uint32_t gs = DEC ? g - gfirst : 0;
+        const uint32_t gs = DEC ? gi - gfirst : 0;
 
         uint32_t rows = 0;
         if (in) {
@@ -2104,6 +2109,23 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     });
 }
 
+// Work list of the decode MAC: the groups whose decode has work (status OK and at least one data shard
+// missing).  A group with nothing lost -- the common case on a live link, where fec_find_missings decodes
+// every group that reached K shares (client.cpp:924-925) -- then costs the MAC kernel nothing.  Ballot per
+// wave, one atomic per wave: groups are ascending within a wave, waves land in any order.
+__global__ void __launch_bounds__(kBlock) compact_kernel(uint64_t G, uint32_t R, const uint8_t *status,
+                                                         const uint8_t *out_idx, uint32_t *count, uint32_t *list)
+{
+    const uint64_t g = blockIdx.x * (uint64_t)kBlock + threadIdx.x;
+    const bool active = g < G && status[g] == 0 && out_idx[g * R] != 0xFF;
+    const uint64_t mask = __ballot(active);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t base = 0;
+    if (lane == 0 && mask) base = atomicAdd(count, (uint32_t)__popcll(mask));
+    base = __shfl(base, 0);
+    if (active) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)g;
+}
+
 int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, size_t B, size_t pitch,
                   const void *d_data, const void *d_parity, const uint64_t *d_present, void *d_out,
                   uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s)
@@ -2196,6 +2218,39 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
     const int tiles = (R + mt - 1) / mt;
     const size_t ent = entry_bytes(mt);
+    // Work-list mode (KFEC_DECODE_LIST=1) measured slower on the benchmark configs, where >= 91% of the groups
+    // lost data: 20:3 decode 6.84 -> 7.35 ms, 10:3 random 3.59 -> 3.75 ms (the list lookup is one more
+    // dependent load at the head of every workgroup, and wave-order compaction scatters neighbouring groups).
+    // It is kept for batches where most groups lost nothing.
+    static const int use_list = env_int("KFEC_DECODE_LIST", 0);
+    if (use_list && G * cpad <= kMaxItemsPerLaunch) {
+        uint32_t *count = reinterpret_cast<uint32_t *>(rec + decode_list_offset(G, K, R));
+        uint32_t *list = count + 16;
+        if (hipMemsetAsync(count, 0, sizeof(uint32_t), s) != hipSuccess) return -3;
+        hipLaunchKernelGGL(compact_kernel, dim3((uint32_t)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, (uint64_t)G,
+                           (uint32_t)R, d_status, d_out_idx, count, list);
+        if (hipGetLastError() != hipSuccess) return -3;
+        const uint32_t gmax = (uint32_t)std::min<size_t>(G, (kBlock - 1) / cpad + 2);
+        const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
+        MacArgs a{};
+        a.data = static_cast<const uint8_t *>(d_data);
+        a.parity = static_cast<const uint8_t *>(d_parity);
+        a.out = static_cast<uint8_t *>(d_out);
+        a.enc = d_enc;
+        a.rec = rec;
+        a.pitch = pitch;
+        a.total = (uint32_t)(G * cpad);  // grid size: every group could have work
+        a.cols = (uint32_t)cols;
+        a.cpad = (uint32_t)cpad;
+        a.G = (uint32_t)G;
+        a.K = K; a.R = R; a.B = (uint32_t)B;
+        a.rec_stride = (uint32_t)rs;
+        a.JC = JC;
+        a.gmax = gmax;
+        a.list = list;
+        a.list_count = count;
+        return dispatch_mac<true>(di, vec, mt, a, tiles, s);
+    }
     return for_group_ranges(G, cpad, [&](size_t g0, size_t gn) {
         const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kBlock - 1) / cpad + 2);
         const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
