@@ -52,6 +52,14 @@ int kfec_frame_data_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size
                           const uint64_t *d_off, const uint16_t *d_len, size_t B, size_t pitch, void *d_data,
                           uint16_t *d_align, void *stream);
 
+/* The fused form of kfec_frame_data_batch + kfec_encode_batch: the parity of G framed groups straight from
+ * the datagram arena, without writing the framed data slots (the encoder assembles each slot's bytes on the
+ * fly).  d_parity[g][r][0..B) and d_align[g] are exactly what the two-step path produces; the framed data
+ * slots themselves are not needed on the wire (the data packets carry the datagrams unframed). */
+int kfec_encode_framed_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size_t src_bytes,
+                             const uint64_t *d_off, const uint16_t *d_len, size_t B, size_t pitch, void *d_parity,
+                             uint16_t *d_align, void *stream);
+
 /* compact_into_container, receive variant (data_operations.cpp:633-667), for G cached groups.
  * Shard s < N of group g is present when bit s of d_present[g][4] is set; its bytes are
  * [d_off[g*N+s], +d_len[g*N+s]) of d_src.  Present data shards (s < K) are framed as on the send side into

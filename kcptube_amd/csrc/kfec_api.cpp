@@ -298,6 +298,34 @@ int kfec_frame_data_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size
                : KFEC_OK;
 }
 
+int kfec_encode_framed_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size_t src_bytes,
+                             const uint64_t *d_off, const uint16_t *d_len, size_t B, size_t pitch, void *d_parity,
+                             uint16_t *d_align, void *stream)
+{
+    if (!ctx || pitch < B || pitch % 4 || B > 0xFFFF) return KFEC_EINVAL;
+    if (G && (!d_src || !al4(d_src) || !d_off || !d_len || !d_align)) return KFEC_EINVAL;
+    if (G && ctx->N > ctx->K && (!d_parity || !al4(d_parity))) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    const int rc = kfec::launch_framed_encode(ctx->d_enc, (int)ctx->K, (int)ctx->N, G, d_src, src_bytes, d_off, d_len,
+                                              B, pitch, d_parity, d_align, as_stream(stream));
+    if (rc < 0) return KFEC_EHIP;
+    if (rc == 0) return KFEC_OK;
+    // shapes the fused kernel does not take (tiny slots with many groups per workgroup, R = 0, huge batches):
+    // frame into a scratch slot array, then encode
+    if (ctx->N == ctx->K) {
+        return kfec::launch_frame((int)ctx->K, (int)ctx->N, false, G, d_src, src_bytes, d_off, d_len, nullptr, B, pitch,
+                                  nullptr, nullptr, d_align, as_stream(stream)) == 0 ? KFEC_OK : KFEC_EHIP;
+    }
+    void *slots = nullptr;
+    if (hipMallocAsync(&slots, G * ctx->K * pitch, as_stream(stream)) != hipSuccess) return KFEC_ENOMEM;
+    int r = kfec::launch_frame((int)ctx->K, (int)ctx->N, false, G, d_src, src_bytes, d_off, d_len, nullptr, B, pitch,
+                               slots, nullptr, d_align, as_stream(stream));
+    if (!r) r = kfec::launch_encode(ctx->di, ctx->d_enc, (int)ctx->K, (int)ctx->N, G, B, pitch, slots, d_parity,
+                                    as_stream(stream));
+    (void)hipFreeAsync(slots, as_stream(stream));
+    return r ? KFEC_EHIP : KFEC_OK;
+}
+
 int kfec_frame_shards_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size_t src_bytes,
                             const uint64_t *d_off, const uint16_t *d_len, const uint64_t *d_present, size_t B,
                             size_t pitch, void *d_data, void *d_parity, uint16_t *d_align, void *stream)

@@ -14,6 +14,7 @@
 #include <algorithm>
 
 #include "../../include/kfec_frame.h"
+#include "kfec_gf.hpp"
 #include "kfec_internal.hpp"
 
 namespace kfec {
@@ -323,6 +324,118 @@ __global__ void __launch_bounds__(kFrameBlock) scatter_kernel(int pass, uint64_t
     }
 }
 
+// ---- fused compact_into_container + encode ---------------------------------------------------------------
+// Parity of framed groups without materialising the framed slots: lane (group, 32-byte column) assembles the
+// column of framed slot j -- [BE16 len][datagram][zeros] -- straight from the datagram arena (two 16-byte
+// re-based loads) and runs the same perm MAC as mac_kernel, with the coefficient tables of the encoding
+// matrix read by scalar loads.  Saves the slot write and re-read of frame_data + encode (2 x G*K*B bytes).
+// The workgroup stages the (offset, length) of its groups' datagrams in LDS.
+struct FramedArgs {
+    const uint32_t *src;
+    uint64_t src_dw;
+    const uint64_t *off;
+    const uint16_t *len;
+    const uint16_t *align;  // 0: the group holds a datagram too long for B (its slots, hence parity, are zero)
+    uint8_t *parity;
+    const uint32_t *etab;   // [K][etab_rows][5] perm tables (kfec_internal.hpp enc_tab_*)
+    uint64_t pitch;
+    uint32_t total, cols, K, R, B, etab_rows, gmax;
+};
+
+// framed bytes [32 col, 32 col + 32) of a slot holding an n-byte datagram at byte `off` of the arena
+__device__ __forceinline__ void framed_gran(const uint32_t *src, uint64_t lim, uint64_t off, uint32_t n, uint32_t col,
+                                            uint32_t (&x)[8])
+{
+    uint32_t lo[4], hi[4];
+    payload_quad(src, lim, off, n, (int64_t)(32 * col) - KFEC_FEC_CONTAINER_HEADER, lo);
+    payload_quad(src, lim, off, n, (int64_t)(32 * col) + 16 - KFEC_FEC_CONTAINER_HEADER, hi);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[i] = lo[i];
+        x[4 + i] = hi[i];
+    }
+    if (col == 0) x[0] |= (n >> 8) | ((n & 0xFFu) << 8);  // htons(length)
+}
+
+template <int MT>
+__global__ void __launch_bounds__(256) framed_encode_kernel(FramedArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_raw[];
+    uint64_t *s_off = reinterpret_cast<uint64_t *>(s_raw);
+    uint32_t *s_len = reinterpret_cast<uint32_t *>(s_raw + (size_t)a.gmax * a.K * 8);  // 0xFFFFFFFF: zero slot
+    const uint32_t K = a.K, cols = a.cols;
+    const uint32_t base = blockIdx.x * 256u, item = base + threadIdx.x;
+    const uint32_t gfirst = base / cols, glast = min(base + 255u, a.total - 1) / cols, ng = glast - gfirst + 1;
+    for (uint32_t e = threadIdx.x; e < ng * K; e += 256) {
+        const uint32_t gs = e / K, j = e - gs * K;
+        const uint64_t gj = (uint64_t)(gfirst + gs) * K + j;
+        const bool ok = a.align[gfirst + gs] != 0;
+        s_off[e] = ok ? a.off[gj] : 0;
+        s_len[e] = ok ? (uint32_t)a.len[gj] : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const uint32_t row0 = blockIdx.y * MT;
+    const uint32_t rows = a.R > row0 ? min((uint32_t)MT, a.R - row0) : 0u;
+    if (item >= a.total || rows == 0) return;
+    const uint32_t g = item / cols, col = item - g * cols, gs = g - gfirst;
+    uint32_t acc[MT][8];
+#pragma unroll
+    for (int r = 0; r < MT; ++r)
+#pragma unroll
+        for (int w = 0; w < 8; ++w) acc[r][w] = 0;
+    auto load = [&](uint32_t j, uint32_t (&x)[8]) {
+        const uint32_t n = s_len[gs * K + j];
+        if (n == 0xFFFFFFFFu) {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) x[w] = 0;
+        } else {
+            framed_gran(a.src, a.src_dw, s_off[gs * K + j], n, col, x);
+        }
+    };
+    uint32_t x0[8], x1[8];
+    load(0, x0);
+    if (K > 1) load(1, x1);
+    typedef const __attribute__((address_space(4))) uint32_t cu32;
+    // one shard: MAC the granule in x, then refill x with shard jj + 2 (two shards' loads in flight)
+    auto step = [&](uint32_t jj, uint32_t (&x)[8]) {
+        uint32_t cur[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) cur[w] = x[w];
+        if (jj + 2 < K) load(jj + 2, x);
+        const cu32 *tg = (const cu32 *)(a.etab + ((size_t)jj * a.etab_rows + row0) * 5);
+        uint32_t t[5 * MT];
+#pragma unroll
+        for (int i = 0; i < 5 * MT; ++i) t[i] = tg[i];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const uint32_t xv = cur[w];
+            const uint32_t s0 = xv & 0x07070707u, s1 = (xv >> 3) & 0x07070707u, s2 = (xv >> 6) & 0x03030303u;
+#pragma unroll
+            for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+        }
+    };
+    for (uint32_t j = 0; j < K; j += 2) {
+        step(j, x0);
+        if (j + 1 < K) step(j + 1, x1);
+    }
+    const uint32_t nd = (col + 1) * 32 > a.B ? (a.B - col * 32 + 3) / 4 : 8u;  // dwords of this column below B
+#pragma unroll
+    for (int r = 0; r < MT; ++r) {
+        if ((uint32_t)r >= rows) continue;
+        uint32_t *o = reinterpret_cast<uint32_t *>(a.parity + ((uint64_t)g * a.R + row0 + r) * a.pitch) + col * 8;
+        if (nd == 8) {
+            typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(u32x4_t{acc[r][0], acc[r][1], acc[r][2], acc[r][3]}, reinterpret_cast<u32x4_t *>(o));
+            __builtin_nontemporal_store(u32x4_t{acc[r][4], acc[r][5], acc[r][6], acc[r][7]},
+                                        reinterpret_cast<u32x4_t *>(o + 4));
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; ++w)
+                if ((uint32_t)w < nd) o[w] = acc[r][w];
+        }
+    }
+}
+
 uint32_t grid_for(uint64_t total)
 {
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((total + kFrameBlock - 1) / kFrameBlock, kMaxGrid));
@@ -336,6 +449,48 @@ uint32_t grid_rows(uint64_t rows)
 int launched() { return hipGetLastError() == hipSuccess ? 0 : -3; }
 
 }  // namespace
+
+// 0 on success, 1 when the fused kernel does not apply (the caller frames, then encodes), -3 on a HIP error
+int launch_framed_encode(const uint8_t *d_enc, int K, int N, size_t G, const void *src, size_t src_bytes,
+                         const uint64_t *off, const uint16_t *len, size_t B, size_t pitch, void *parity,
+                         uint16_t *align, hipStream_t s)
+{
+    const int R = N - K;
+    if (G == 0) return 0;
+    const uint32_t cols = (uint32_t)((B + 31) / 32);
+    const uint32_t gmax = (uint32_t)std::min<size_t>(G, 255 / cols + 2);
+    const size_t lds = (size_t)gmax * K * 12;
+    const int mt = R <= 4 ? std::max(R, 1) : 8;
+    if (R == 0 || lds > 32 * 1024 || (uint64_t)G * cols > 0x7FFFFFFFull || pitch % 4 || B > 0xFFFF) return 1;
+    hipLaunchKernelGGL(align_kernel, dim3(grid_for(G)), dim3(kFrameBlock), 0, s, (uint64_t)G, (uint32_t)K, (uint32_t)K,
+                       len, nullptr, (uint32_t)B, align);
+    if (launched()) return -3;
+    FramedArgs a{};
+    a.src = static_cast<const uint32_t *>(src);
+    a.src_dw = (src_bytes + 3) / 4;
+    a.off = off;
+    a.len = len;
+    a.align = align;
+    a.parity = static_cast<uint8_t *>(parity);
+    a.etab = reinterpret_cast<const uint32_t *>(d_enc + enc_tab_offset(K, N));
+    a.pitch = pitch;
+    a.total = (uint32_t)(G * cols);
+    a.cols = cols;
+    a.K = K;
+    a.R = R;
+    a.B = (uint32_t)B;
+    a.etab_rows = (uint32_t)enc_tab_rows(R);
+    a.gmax = gmax;
+    const dim3 grid((a.total + 255) / 256, (R + mt - 1) / mt);
+    switch (mt) {
+    case 1: hipLaunchKernelGGL(framed_encode_kernel<1>, grid, dim3(256), lds, s, a); break;
+    case 2: hipLaunchKernelGGL(framed_encode_kernel<2>, grid, dim3(256), lds, s, a); break;
+    case 3: hipLaunchKernelGGL(framed_encode_kernel<3>, grid, dim3(256), lds, s, a); break;
+    case 4: hipLaunchKernelGGL(framed_encode_kernel<4>, grid, dim3(256), lds, s, a); break;
+    default: hipLaunchKernelGGL(framed_encode_kernel<8>, grid, dim3(256), lds, s, a); break;
+    }
+    return launched();
+}
 
 int launch_frame(int K, int N, bool recv, size_t G, const void *src, size_t src_bytes, const uint64_t *off,
                  const uint16_t *len, const uint64_t *present, size_t B, size_t pitch, void *data, void *parity,

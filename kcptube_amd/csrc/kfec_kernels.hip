@@ -110,23 +110,6 @@ __device__ __forceinline__ uint64_t bits_below(int n, int q)
     return v <= 0 ? 0ull : (v >= 64 ? ~0ull : ((1ull << v) - 1ull));
 }
 
-// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor_b32 otherwise.
-// The builtin (not inline asm) leaves the scheduler free to interleave independent accumulator chains.
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
-{
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-// acc ^ c * x for 4 bytes, c given by its 5 permute tables (kfec_gf.hpp gf_perm_tables):
-// three v_perm_b32 lookups (bits 0-2, 3-5, 6-7 of every byte) and two XORs
-__device__ __forceinline__ uint32_t perm_mac(uint32_t acc, const uint32_t *t, uint32_t s0, uint32_t s1, uint32_t s2)
-{
-    const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], s0);
-    const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], s1);
-    const uint32_t p2 = __builtin_amdgcn_perm(t[4], t[4], s2);
-    return xor3(acc, p0, p1) ^ p2;
-}
-
 // ---------------------------------------------------------------------------------------------------
 // (A6) encoding matrix: Lagrange closed form of Vbot * Vtop^-1.
 // Evaluation points x_0 = 0, x_i = alpha^i (i >= 1) -- the rows of the reference's Vandermonde matrix

@@ -69,6 +69,15 @@ class FecFrame:
                                                B, pitch, _dptr(data), _dptr(align), _stream_handle(stream)),
                "kfec_frame_data_batch")
 
+    def encode_framed(self, src, off, length, parity, align, B: int, stream=None) -> None:
+        """frame_data + encode_batch fused: parity [G][R][pitch] and align [G] of the framed groups, without
+        materialising the framed data slots."""
+        G, r, pitch = parity.shape
+        assert off.numel() == G * self.K and align.numel() == G
+        _check(self._lib.kfec_encode_framed_batch(self.code._ctx, G, _dptr(src), src.numel(), _dptr(off),
+                                                  _dptr(length), B, pitch, _dptr(parity), _dptr(align),
+                                                  _stream_handle(stream)), "kfec_encode_framed_batch")
+
     def frame_shards(self, src, off, length, present, data, parity, align, B: int, stream=None) -> None:
         """Receive side: off/length [G*N] shard table, present int64 [G][4]; writes the present slots of
         data [G][K][pitch] / parity [G][R][pitch] and align [G]."""

@@ -438,3 +438,46 @@ def test_seal_open_match_oracle(dev, mode):
         if p < len(pk) and p % 3 != 0 and pk[p]:
             assert good and body == pk[p]
     assert n_bad > 100
+
+
+@pytest.mark.parametrize("K,N,B,pitch", [(20, 23, 1442, 1444), (10, 13, 1402, 1404), (200, 255, 1442, 1444),
+                                         (3, 5, 7, 8), (1, 2, 2, 4), (4, 6, 40, 64)])
+def test_encode_framed_matches_two_step_and_oracle(dev, oracle, K, N, B, pitch):
+    """kfec_encode_framed_batch == kfec_frame_data_batch + kfec_encode_batch, byte for byte, and == the oracle's
+    compact_into_container + fec_code::encode on the zero-padded slots (incl. an overflowing group)."""
+    c, fr = _coder(K, N)
+    R = N - K
+    rng = random.Random(K * 7 + B)
+    G = 23 if K < 100 else 5
+    dgs = []
+    for g in range(G):
+        for i in range(K):
+            n = rng.choice([0, 1, B - 2, rng.randint(0, B - 2)])
+            if g == 2 and i == 0:
+                n = B - 1  # too long: align 0 and zero parity
+            dgs.append(rng.randbytes(n))
+    src, off, lens = _arena(dgs, dev)
+    d_len = _i16(lens, dev)
+    par = torch.full((G, R, pitch), SENT, dtype=torch.uint8, device=dev)
+    al = torch.zeros(G, dtype=torch.int16, device=dev)
+    fr.encode_framed(src, off, d_len, par, al, B)
+    data = torch.empty((G, K, pitch), dtype=torch.uint8, device=dev)
+    al2 = torch.zeros(G, dtype=torch.int16, device=dev)
+    par2 = torch.full((G, R, pitch), SENT, dtype=torch.uint8, device=dev)
+    fr.frame_data(src, off, d_len, data, al2, B)
+    c.encode_batch(data, par2, B=B)
+    torch.cuda.synchronize()
+    gp, gp2 = par.cpu().numpy(), par2.cpu().numpy()
+    assert np.array_equal(_u16(al), _u16(al2))
+    Bp = (B + 3) // 4 * 4
+    assert np.array_equal(gp[:, :, :Bp], gp2[:, :, :Bp])
+    assert (gp[:, :, Bp:] == SENT).all()
+    for g in range(G):
+        cont, a, total = fo.compact_send(dgs[g * K:(g + 1) * K])
+        if a > B:
+            assert not gp[g, :, :Bp].any()
+            continue
+        exp = oracle.encode(K, N, cont, a)
+        for r in range(R):
+            assert gp[g, r, :a].tobytes() == exp[r], (g, r)
+            assert not gp[g, r, a:Bp].any()
