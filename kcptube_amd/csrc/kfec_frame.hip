@@ -54,17 +54,32 @@ __device__ __forceinline__ uint32_t payload_dword(const uint32_t *base32, uint64
 // 16 bytes [q0, q0 + 16) of the payload base[start, start + len) as 4 dwords, zero outside it: one 16-byte
 // load at the covering dword (dword aligned is enough on gfx950, as the MAC kernel's granules rely on) and
 // one more dword, re-based with v_alignbyte_b32.  Dwords at or beyond lim32 read as zero.
-__device__ __forceinline__ void payload_quad(const uint32_t *base32, uint64_t lim32, uint64_t start, uint32_t len,
-                                             int64_t q0, uint32_t (&o)[4])
+// bytes [a, b) of a dword (any a, b; clamped to [0, 4])
+__device__ __forceinline__ uint32_t range_mask(int a, int b)
 {
-    const uint64_t a4 = start + (uint64_t)(q0 + 16);  // first byte's address + 16 (q0 >= -15)
-    const uint64_t w4 = a4 >> 2;                       // its dword index + 4
+    const uint32_t hi = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : (1u << (8 * b)) - 1u);
+    const uint32_t lo = a >= 4 ? 0xFFFFFFFFu : (a <= 0 ? 0u : (1u << (8 * a)) - 1u);
+    return hi & ~lo;
+}
+
+__device__ __forceinline__ void payload_quad(const uint32_t *base32, uint64_t lim32, uint64_t start, uint32_t len,
+                                             int64_t q0l, uint32_t (&o)[4])
+{
+    const int32_t q0 = (int32_t)q0l;                     // |q0| < 2^17: slot and packet offsets
+    const int lo = max(0, -q0), hi = min(16, (int32_t)len - q0);  // payload bytes [lo, hi) of the chunk
+    if (hi <= lo) {  // nothing of the payload here (zero padding, headers): no loads
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = 0u;
+        return;
+    }
+    const uint64_t a4 = start + (uint64_t)(int64_t)(q0 + 16);  // first byte's address + 16 (q0 >= -15)
+    const uint64_t w4 = a4 >> 2;                                // its dword index + 4
     const uint32_t sh = (uint32_t)(a4 & 3u);
     uint32_t d[5];
     if (w4 >= 4 && w4 + 1 <= lim32) {
         const uint4 x = *reinterpret_cast<const uint4 *>(base32 + (w4 - 4));
         d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
-        d[4] = w4 < lim32 ? base32[w4] : 0u;
+        d[4] = (sh && w4 < lim32) ? base32[w4] : 0u;
     } else {
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
@@ -75,7 +90,7 @@ __device__ __forceinline__ void payload_quad(const uint32_t *base32, uint64_t li
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t v = sh ? __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) : d[i];
-        o[i] = v & byte_mask(q0 + 4 * i, len);
+        o[i] = v & range_mask(lo - 4 * i, hi - 4 * i);
     }
 }
 
