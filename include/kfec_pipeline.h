@@ -1,0 +1,105 @@
+/*
+ * kfec_pipeline.h -- the per-connection FEC bookkeeping of kcptube over batched GPU coding (libkfec.so),
+ * the callers of fec_code, restated so that many groups of many connections are
+ * coded in one device batch instead of one CPU call per group.
+ *
+ *   kfec_tx  = client_mode::fec_maker          (src/modes/client.cpp:797-840; server.cpp:932-975 is the same)
+ *   kfec_rx  = fec_unpack's cache insert + fec_find_missings
+ *                                              (client.cpp:842-938; server.cpp:977-1020; relay.cpp:1384-1428)
+ *   kfec_txq / kfec_rxq = the batched encode / decode queues shared by many kfec_tx / kfec_rx.
+ *
+ * What stays exactly as in the reference (host side, per packet, no GPU round trip on the latency path):
+ *   - every datagram leaves at once as a data packet (create_fec_data_packet: [LE32 ts][BE32 sn][u8 sub_sn]);
+ *   - sn / sub_sn numbering, including conv == 0 (no FEC group is built, sub_sn resets);
+ *   - the receive cache fec_rcv_cache[sn][sub_sn] (a duplicate overwrites), the fec_rcv_restored set, the
+ *     gbv_fec_waits = 3 expiry with uint32 wrap-around, and the rule that a group is decoded once, as soon
+ *     as it holds >= K shares (even when nothing is missing).
+ * What is batched: a group that becomes complete (send) or decodable (receive) is copied into the queue's
+ * pinned staging; kfec_txq_flush / kfec_rxq_flush code every queued group in one GPU batch
+ * (kfec_encode_framed_batch + kfec_pack_batch; kfec_frame_shards_batch + kfec_decode_batch +
+ * kfec_unframe_batch) and hand back redundant packets / recovered datagrams through a callback, in queue
+ * order.  The reference inputs a recovered datagram to KCP inside fec_find_missings; here that happens at the
+ * flush, which the caller schedules (e.g. once per event-loop turn) -- the latency / throughput trade the
+ * batching buys.  Shard padding is zero (include/kfec_frame.h).
+ *
+ * Threading: a kfec_tx / kfec_rx and its queue are used from one thread at a time (the reference serialises
+ * with mutex_fec_snd / mutex_fec_rcv, connections.hpp:609-611).
+ */
+#ifndef KFEC_PIPELINE_H_
+#define KFEC_PIPELINE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "kfec_frame.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct kfec_txq kfec_txq;
+typedef struct kfec_tx kfec_tx;
+typedef struct kfec_rxq kfec_rxq;
+typedef struct kfec_rx kfec_rx;
+
+/* ---- send -------------------------------------------------------------------------------------------- */
+
+/* A batched encode queue for the coder's fec=K:N-K: up to max_groups complete groups of datagrams of at most
+ * max_datagram bytes (kcp_mtu) between flushes.  Device buffers are allocated at the first flush. */
+int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram, kfec_txq **out);
+void kfec_txq_destroy(kfec_txq *q);
+size_t kfec_txq_pending(const kfec_txq *q);
+
+/* One connection direction's fec_maker state: conv is the KCP conversation id written into redundant
+ * packets (0: the reference builds no FEC groups for this connection). */
+int kfec_tx_create(kfec_txq *q, uint32_t conv, uint64_t tag, kfec_tx **out);
+void kfec_tx_destroy(kfec_tx *tx);
+
+/* fec_maker(input_data, data_size): writes the data packet to pkt[9 + len] (*pkt_len) and, when this
+ * datagram completes a group, queues the group (its redundant packets come from kfec_txq_flush).
+ * KFEC_EINVAL for a datagram longer than max_datagram; KFEC_ENOMEM, with nothing sent, when the datagram
+ * would complete a group and the queue is full (flush first). */
+int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t timestamp, uint8_t *pkt,
+                 size_t *pkt_len);
+
+/* Redundant packet callback: tag of the kfec_tx, the packet bytes (13-byte header + align bytes). */
+typedef void (*kfec_packet_cb)(void *user, uint64_t tag, uint32_t sn, uint8_t sub_sn, const uint8_t *pkt,
+                               size_t len);
+
+/* Encode every queued group on the GPU and emit its N-K redundant packets (queue order).  Synchronous. */
+int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *user, void *stream);
+
+/* ---- receive ----------------------------------------------------------------------------------------- */
+
+/* A batched decode queue: up to max_groups decodable groups whose shards are at most max_shard bytes
+ * (kcp_mtu + 2, the parity length) between flushes.  Device buffers are allocated at the first flush. */
+int kfec_rxq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_shard, kfec_rxq **out);
+void kfec_rxq_destroy(kfec_rxq *q);
+size_t kfec_rxq_pending(const kfec_rxq *q);
+
+int kfec_rx_create(kfec_rxq *q, uint64_t tag, kfec_rx **out);
+void kfec_rx_destroy(kfec_rx *rx);
+/* Groups currently held in the receive cache (fec_rcv_cache.size()). */
+size_t kfec_rx_cached(const kfec_rx *rx);
+
+/* fec_unpack for one received FEC packet: caches its payload under (sn, sub_sn), runs the fec_find_missings
+ * scan (expiry relative to this packet's sn; every group holding >= K shares and not yet restored is queued
+ * for decoding and marked restored).  For a data packet *datagram / *datagram_len point at its payload inside
+ * pkt (what fec_unpack returns to its caller for KCP::Input); NULL / 0 otherwise.  Returns the number of
+ * groups queued by this call, KFEC_EINVAL for a packet shorter than its header or a shard longer than
+ * max_shard, KFEC_ENOMEM when the decode queue might overflow (flush first; the packet is then not cached). */
+int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **datagram, size_t *datagram_len);
+
+/* Recovered datagram callback: tag of the kfec_rx, group sn, data index, bytes (what KCP::Input gets). */
+typedef void (*kfec_datagram_cb)(void *user, uint64_t tag, uint32_t sn, uint8_t index, const uint8_t *data,
+                                 size_t len);
+
+/* Decode every queued group on the GPU and emit the recovered datagrams (queue order, ascending index within
+ * a group), as fec_find_missings' extract_from_container + KCP::Input loop.  Synchronous. */
+int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KFEC_PIPELINE_H_ */

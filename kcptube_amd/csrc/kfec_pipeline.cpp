@@ -1,0 +1,414 @@
+// kfec_pipeline.cpp -- include/kfec_pipeline.h: kcptube's fec_maker / fec_unpack + fec_find_missings
+// bookkeeping on the host, feeding batched device coding through the public C ABI (kfec.h, kfec_frame.h).
+// Per-packet work here is bookkeeping and copies into pinned staging; every byte of parity, recovered data and
+// redundant packet is computed by the GPU kernels at flush time.
+#include "../../include/kfec_pipeline.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <new>
+#include <set>
+#include <vector>
+
+namespace {
+
+constexpr uint32_t kFecWaits = KFEC_FEC_WAITS;
+
+size_t round4(size_t x) { return (x + 3) & ~size_t(3); }
+
+// pinned host and device buffers, grown on demand
+struct Pinned {
+    void *p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes)
+    {
+        if (bytes <= n) return KFEC_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipHostMalloc(&p, std::max<size_t>(bytes, 256), hipHostMallocDefault) != hipSuccess) return KFEC_ENOMEM;
+        n = std::max<size_t>(bytes, 256);
+        return KFEC_OK;
+    }
+    template <typename T> T *as() const { return static_cast<T *>(p); }
+    ~Pinned() { if (p) (void)hipHostFree(p); }
+};
+
+struct Device {
+    void *p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes)
+    {
+        if (bytes <= n) return KFEC_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipMalloc(&p, std::max<size_t>(bytes, 256)) != hipSuccess) return KFEC_ENOMEM;
+        n = std::max<size_t>(bytes, 256);
+        return KFEC_OK;
+    }
+    template <typename T> T *as() const { return static_cast<T *>(p); }
+    ~Device() { if (p) (void)hipFree(p); }
+};
+
+inline void put_le32(uint8_t *p, uint32_t v)
+{
+    p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+}
+inline void put_be32(uint8_t *p, uint32_t v)
+{
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+inline uint32_t get_be32(const uint8_t *p)
+{
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+
+}  // namespace
+
+// ---- send ------------------------------------------------------------------------------------------------
+struct kfec_txq {
+    const kfec_ctx *ctx = nullptr;
+    size_t K = 0, N = 0, R = 0, G = 0, mtu = 0, slot = 0;  // slot: datagram stride in the staging arena
+    size_t n = 0;                                          // complete groups queued
+    Pinned h_dg, h_off, h_len, h_sn, h_conv, h_pkt, h_pkt_len;
+    std::vector<uint64_t> tags;
+    Device d_dg, d_off, d_len, d_sn, d_conv, d_par, d_align, d_pkt, d_pkt_len;
+};
+
+struct kfec_tx {
+    kfec_txq *q = nullptr;
+    uint32_t conv = 0;
+    uint64_t tag = 0;
+    uint32_t sn = 0;      // fec_snd_sn
+    uint8_t sub_sn = 0;   // fec_snd_sub_sn
+    std::vector<std::vector<uint8_t>> cache;  // fec_snd_cache
+};
+
+extern "C" {
+
+int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram, kfec_txq **out)
+{
+    if (!out) return KFEC_EINVAL;
+    *out = nullptr;
+    if (!ctx || !max_groups || max_datagram + KFEC_FEC_CONTAINER_HEADER > 0xFFFF) return KFEC_EINVAL;
+    kfec_txq *q = new (std::nothrow) kfec_txq;
+    if (!q) return KFEC_ENOMEM;
+    q->ctx = ctx;
+    q->K = kfec_get_K(ctx);
+    q->N = kfec_get_N(ctx);
+    q->R = q->N - q->K;
+    q->G = max_groups;
+    q->mtu = max_datagram;
+    q->slot = std::max<size_t>(round4(max_datagram), 4);
+    const size_t GK = q->G * q->K;
+    if (q->h_dg.ensure(GK * q->slot) || q->h_off.ensure(GK * 8) || q->h_len.ensure(GK * 2) ||
+        q->h_sn.ensure(q->G * 4) || q->h_conv.ensure(q->G * 4)) {
+        delete q;
+        return KFEC_ENOMEM;
+    }
+    q->tags.resize(q->G);
+    *out = q;
+    return KFEC_OK;
+}
+
+void kfec_txq_destroy(kfec_txq *q) { delete q; }
+
+size_t kfec_txq_pending(const kfec_txq *q) { return q ? q->n : 0; }
+
+int kfec_tx_create(kfec_txq *q, uint32_t conv, uint64_t tag, kfec_tx **out)
+{
+    if (!out) return KFEC_EINVAL;
+    *out = nullptr;
+    if (!q) return KFEC_EINVAL;
+    kfec_tx *tx = new (std::nothrow) kfec_tx;
+    if (!tx) return KFEC_ENOMEM;
+    tx->q = q;
+    tx->conv = conv;
+    tx->tag = tag;
+    *out = tx;
+    return KFEC_OK;
+}
+
+void kfec_tx_destroy(kfec_tx *tx) { delete tx; }
+
+int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t timestamp, uint8_t *pkt, size_t *pkt_len)
+{
+    if (!tx || !pkt || !pkt_len || (len && !datagram)) return KFEC_EINVAL;
+    kfec_txq *q = tx->q;
+    if (len > q->mtu) return KFEC_EINVAL;
+    const bool completes = tx->conv != 0 && tx->cache.size() + 1 == q->K;
+    if (completes && q->n == q->G) return KFEC_ENOMEM;
+    // create_fec_data_packet (connections.cpp:395-411), sub_sn = fec_snd_sub_sn++ (client.cpp:805-806)
+    put_le32(pkt, timestamp);
+    put_be32(pkt + 4, tx->sn);
+    pkt[8] = tx->sub_sn++;
+    if (len) std::memcpy(pkt + KFEC_PKT_DATA_HEADER, datagram, len);
+    *pkt_len = KFEC_PKT_DATA_HEADER + len;
+    if (tx->conv == 0) {  // client.cpp:811-815
+        tx->sub_sn = 0;
+        return KFEC_OK;
+    }
+    tx->cache.emplace_back(datagram, datagram + len);
+    if (!completes) return KFEC_OK;
+    // the group is complete: copy it into queue slot n (compact_into_container + encode run at the flush)
+    const size_t g = q->n;
+    for (size_t i = 0; i < q->K; ++i) {
+        const size_t e = g * q->K + i;
+        if (!tx->cache[i].empty()) std::memcpy(q->h_dg.as<uint8_t>() + e * q->slot, tx->cache[i].data(), tx->cache[i].size());
+        q->h_off.as<uint64_t>()[e] = e * q->slot;
+        q->h_len.as<uint16_t>()[e] = (uint16_t)tx->cache[i].size();
+    }
+    q->h_sn.as<uint32_t>()[g] = tx->sn;
+    q->h_conv.as<uint32_t>()[g] = tx->conv;
+    q->tags[g] = tx->tag;
+    q->n = g + 1;
+    tx->cache.clear();  // client.cpp:830-832
+    tx->sub_sn = 0;
+    tx->sn++;
+    return KFEC_OK;
+}
+
+int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *user, void *stream)
+{
+    if (!q) return KFEC_EINVAL;
+    const size_t n = q->n;
+    if (n == 0) return KFEC_OK;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t K = q->K, N = q->N, R = q->R, G = q->G;
+    const size_t B = q->mtu + KFEC_FEC_CONTAINER_HEADER, pitch = round4(B);
+    const size_t pkt_pitch = round4(KFEC_PKT_REDUNDANT_HEADER + B);
+    if (q->d_dg.ensure(G * K * q->slot) || q->d_off.ensure(G * K * 8) || q->d_len.ensure(G * K * 2) ||
+        q->d_sn.ensure(G * 4) || q->d_conv.ensure(G * 4) || q->d_par.ensure(G * std::max<size_t>(R, 1) * pitch) ||
+        q->d_align.ensure(G * 2) || q->d_pkt.ensure(G * N * pkt_pitch) || q->d_pkt_len.ensure(G * N * 2) ||
+        q->h_pkt.ensure(G * std::max<size_t>(R, 1) * pkt_pitch) || q->h_pkt_len.ensure(G * std::max<size_t>(R, 1) * 2))
+        return KFEC_ENOMEM;
+    const size_t nk = n * K;
+    if (hipMemcpyAsync(q->d_dg.p, q->h_dg.p, nk * q->slot, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(q->d_off.p, q->h_off.p, nk * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(q->d_len.p, q->h_len.p, nk * 2, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(q->d_sn.p, q->h_sn.p, n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(q->d_conv.p, q->h_conv.p, n * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+        return KFEC_EHIP;
+    const size_t arena = nk * q->slot;
+    int rc = kfec_encode_framed_batch(q->ctx, n, q->d_dg.p, arena, q->d_off.as<uint64_t>(), q->d_len.as<uint16_t>(), B,
+                                      pitch, q->d_par.p, q->d_align.as<uint16_t>(), stream);
+    if (rc) return rc;
+    if (R) {
+        rc = kfec_pack_batch(q->ctx, n, KFEC_PACK_REDUNDANT, q->d_dg.p, arena, q->d_off.as<uint64_t>(),
+                             q->d_len.as<uint16_t>(), pitch, q->d_par.p, q->d_align.as<uint16_t>(),
+                             q->d_sn.as<uint32_t>(), q->d_conv.as<uint32_t>(), timestamp, q->d_pkt.p, pkt_pitch,
+                             q->d_pkt_len.as<uint16_t>(), stream);
+        if (rc) return rc;
+        // the R redundant packets of each group: rows of R * pkt_pitch bytes, N * pkt_pitch apart
+        if (hipMemcpy2DAsync(q->h_pkt.p, R * pkt_pitch, q->d_pkt.as<uint8_t>() + K * pkt_pitch, N * pkt_pitch,
+                             R * pkt_pitch, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpy2DAsync(q->h_pkt_len.p, R * 2, q->d_pkt_len.as<uint8_t>() + K * 2, N * 2, R * 2, n,
+                             hipMemcpyDeviceToHost, s) != hipSuccess)
+            return KFEC_EHIP;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
+    const uint32_t *sn = q->h_sn.as<uint32_t>();
+    for (size_t g = 0; g < n && cb; ++g)
+        for (size_t r = 0; r < R; ++r) {
+            const uint16_t len = q->h_pkt_len.as<uint16_t>()[g * R + r];
+            if (len) cb(user, q->tags[g], sn[g], (uint8_t)(K + r), q->h_pkt.as<uint8_t>() + (g * R + r) * pkt_pitch, len);
+        }
+    q->n = 0;
+    return KFEC_OK;
+}
+
+}  // extern "C"
+
+// ---- receive ---------------------------------------------------------------------------------------------
+struct kfec_rxq {
+    const kfec_ctx *ctx = nullptr;
+    size_t K = 0, N = 0, R = 0, G = 0, max_shard = 0, slot = 0;
+    size_t n = 0;  // groups queued for decoding
+    Pinned h_arena, h_off, h_len, h_present, h_idx, h_rec_len, h_dst;
+    std::vector<uint64_t> tags;
+    std::vector<uint32_t> sns;
+    Device d_arena, d_off, d_len, d_present, d_data, d_par, d_align, d_out, d_idx, d_st, d_ws, d_rec_len, d_dst;
+};
+
+struct kfec_rx {
+    kfec_rxq *q = nullptr;
+    uint64_t tag = 0;
+    std::map<uint32_t, std::map<uint8_t, std::vector<uint8_t>>> cache;  // fec_rcv_cache
+    std::set<uint32_t> restored;                                          // fec_rcv_restored
+};
+
+namespace {
+
+// copy a decodable group into queue slot q->n
+void rx_enqueue(kfec_rxq *q, uint64_t tag, uint32_t sn, const std::map<uint8_t, std::vector<uint8_t>> &shards)
+{
+    const size_t g = q->n;
+    uint64_t *present = q->h_present.as<uint64_t>() + g * 4;
+    present[0] = present[1] = present[2] = present[3] = 0;
+    for (const auto &[s, bytes] : shards) {
+        if (s >= q->N) continue;  // a sub_sn beyond N is cached by the reference but never selected usefully
+        const size_t e = g * q->N + s;
+        if (!bytes.empty()) std::memcpy(q->h_arena.as<uint8_t>() + e * q->slot, bytes.data(), bytes.size());
+        q->h_off.as<uint64_t>()[e] = e * q->slot;
+        q->h_len.as<uint16_t>()[e] = (uint16_t)bytes.size();
+        present[s >> 6] |= 1ull << (s & 63);
+    }
+    q->tags[g] = tag;
+    q->sns[g] = sn;
+    q->n = g + 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kfec_rxq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_shard, kfec_rxq **out)
+{
+    if (!out) return KFEC_EINVAL;
+    *out = nullptr;
+    if (!ctx || !max_groups || max_shard < KFEC_FEC_CONTAINER_HEADER || max_shard > 0xFFFF) return KFEC_EINVAL;
+    kfec_rxq *q = new (std::nothrow) kfec_rxq;
+    if (!q) return KFEC_ENOMEM;
+    q->ctx = ctx;
+    q->K = kfec_get_K(ctx);
+    q->N = kfec_get_N(ctx);
+    q->R = q->N - q->K;
+    q->G = max_groups;
+    q->max_shard = max_shard;
+    q->slot = round4(max_shard);
+    const size_t GN = q->G * q->N;
+    if (q->h_arena.ensure(GN * q->slot) || q->h_off.ensure(GN * 8) || q->h_len.ensure(GN * 2) ||
+        q->h_present.ensure(q->G * 32)) {
+        delete q;
+        return KFEC_ENOMEM;
+    }
+    q->tags.resize(q->G);
+    q->sns.resize(q->G);
+    *out = q;
+    return KFEC_OK;
+}
+
+void kfec_rxq_destroy(kfec_rxq *q) { delete q; }
+
+size_t kfec_rxq_pending(const kfec_rxq *q) { return q ? q->n : 0; }
+
+int kfec_rx_create(kfec_rxq *q, uint64_t tag, kfec_rx **out)
+{
+    if (!out) return KFEC_EINVAL;
+    *out = nullptr;
+    if (!q) return KFEC_EINVAL;
+    kfec_rx *rx = new (std::nothrow) kfec_rx;
+    if (!rx) return KFEC_ENOMEM;
+    rx->q = q;
+    rx->tag = tag;
+    *out = rx;
+    return KFEC_OK;
+}
+
+void kfec_rx_destroy(kfec_rx *rx) { delete rx; }
+
+size_t kfec_rx_cached(const kfec_rx *rx) { return rx ? rx->cache.size() : 0; }
+
+int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **datagram, size_t *datagram_len)
+{
+    if (!rx || !pkt) return KFEC_EINVAL;
+    if (datagram) *datagram = nullptr;
+    if (datagram_len) *datagram_len = 0;
+    kfec_rxq *q = rx->q;
+    // unpack_fec / unpack_fec_redundant (connections.cpp:488-511), dispatched on sub_sn as fec_unpack
+    if (len < KFEC_PKT_DATA_HEADER) return KFEC_EINVAL;
+    const uint8_t sub = pkt[8];
+    const bool red = sub >= q->K;
+    const size_t H = red ? KFEC_PKT_REDUNDANT_HEADER : KFEC_PKT_DATA_HEADER;
+    if (len < H) return KFEC_EINVAL;
+    const uint8_t *payload = pkt + H;
+    const size_t plen = len - H;
+    if (plen + (red ? 0 : KFEC_FEC_CONTAINER_HEADER) > q->max_shard) return KFEC_EINVAL;
+    const uint32_t fec_sn = get_be32(pkt + 4);
+    // capacity: this push can queue at most every not-yet-restored cached group plus a new one
+    size_t could = rx->cache.count(fec_sn) ? 0 : 1;
+    for (const auto &kv : rx->cache)
+        if (!rx->restored.count(kv.first)) ++could;
+    if (q->n + could > q->G) return KFEC_ENOMEM;
+    rx->cache[fec_sn][sub].assign(payload, payload + plen);  // fec_rcv_cache[sn][sub_sn] = ... (client.cpp:869,887)
+    if (!red) {
+        if (datagram) *datagram = payload;
+        if (datagram_len) *datagram_len = plen;
+    }
+    // fec_find_missings (client.cpp:895-938)
+    int queued = 0;
+    for (auto it = rx->cache.begin(); it != rx->cache.end();) {
+        const uint32_t sn = it->first;
+        const bool stale = (uint32_t)(fec_sn - sn) > kFecWaits;
+        if (it->second.size() < q->K || rx->restored.count(sn)) {
+            if (stale) {
+                rx->restored.erase(sn);
+                it = rx->cache.erase(it);
+            } else {
+                ++it;
+            }
+            continue;
+        }
+        rx_enqueue(q, rx->tag, sn, it->second);
+        rx->restored.insert(sn);
+        ++queued;
+        ++it;
+    }
+    return queued;
+}
+
+int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
+{
+    if (!q) return KFEC_EINVAL;
+    const size_t n = q->n;
+    if (n == 0) return KFEC_OK;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t K = q->K, N = q->N, R = q->R, G = q->G;
+    const size_t B = q->max_shard, pitch = round4(B), dst_pitch = round4(B);
+    const size_t R1 = std::max<size_t>(R, 1);
+    if (q->d_arena.ensure(G * N * q->slot) || q->d_off.ensure(G * N * 8) || q->d_len.ensure(G * N * 2) ||
+        q->d_present.ensure(G * 32) || q->d_data.ensure(G * K * pitch) || q->d_par.ensure(G * R1 * pitch) ||
+        q->d_align.ensure(G * 2) || q->d_out.ensure(G * R1 * pitch) || q->d_idx.ensure(G * R1) ||
+        q->d_st.ensure(G) || q->d_ws.ensure(kfec_decode_workspace_size(q->ctx, G)) ||
+        q->d_rec_len.ensure(G * R1 * 2) || q->d_dst.ensure(G * R1 * dst_pitch) || q->h_idx.ensure(G * R1) ||
+        q->h_rec_len.ensure(G * R1 * 2) || q->h_dst.ensure(G * R1 * dst_pitch))
+        return KFEC_ENOMEM;
+    const size_t nn = n * N;
+    if (hipMemcpyAsync(q->d_arena.p, q->h_arena.p, nn * q->slot, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(q->d_off.p, q->h_off.p, nn * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(q->d_len.p, q->h_len.p, nn * 2, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(q->d_present.p, q->h_present.p, n * 32, hipMemcpyHostToDevice, s) != hipSuccess)
+        return KFEC_EHIP;
+    int rc = kfec_frame_shards_batch(q->ctx, n, q->d_arena.p, nn * q->slot, q->d_off.as<uint64_t>(),
+                                     q->d_len.as<uint16_t>(), q->d_present.as<uint64_t>(), B, pitch, q->d_data.p,
+                                     q->d_par.p, q->d_align.as<uint16_t>(), stream);
+    if (rc) return rc;
+    rc = kfec_decode_batch(q->ctx, n, B, pitch, q->d_data.p, q->d_par.p, q->d_present.as<uint64_t>(), q->d_out.p,
+                           q->d_idx.as<uint8_t>(), q->d_st.as<uint8_t>(), q->d_ws.p, stream);
+    if (rc) return rc;
+    if (R) {
+        rc = kfec_unframe_batch(q->ctx, n, B, pitch, q->d_out.p, q->d_idx.as<uint8_t>(), q->d_rec_len.as<uint16_t>(),
+                                q->d_dst.p, dst_pitch, stream);
+        if (rc) return rc;
+        if (hipMemcpyAsync(q->h_idx.p, q->d_idx.p, n * R, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(q->h_rec_len.p, q->d_rec_len.p, n * R * 2, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(q->h_dst.p, q->d_dst.p, n * R * dst_pitch, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return KFEC_EHIP;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
+    for (size_t g = 0; g < n && cb && R; ++g)
+        for (size_t t = 0; t < R; ++t) {
+            const uint8_t idx = q->h_idx.as<uint8_t>()[g * R + t];
+            const uint16_t len = q->h_rec_len.as<uint16_t>()[g * R + t];
+            if (idx == 0xFF || len == 0xFFFF) continue;
+            cb(user, q->tags[g], q->sns[g], idx, q->h_dst.as<uint8_t>() + (g * R + t) * dst_pitch, len);
+        }
+    q->n = 0;
+    return KFEC_OK;
+}
+
+}  // extern "C"

@@ -39,7 +39,7 @@ _szp = C.POINTER(C.c_size_t)
 _vp = C.c_void_p
 
 
-HEADERS = [HEADER, os.path.join(os.path.dirname(PKG), "include", "kfec_frame.h")]
+HEADERS = [HEADER] + [os.path.join(os.path.dirname(PKG), "include", h) for h in ("kfec_frame.h", "kfec_pipeline.h")]
 
 
 def header_functions() -> list[str]:
@@ -88,6 +88,22 @@ def load_library():
                                       _vp, sz, _vp, _vp]),
         "kfec_unpack_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, _vp, _vp]),
         "kfec_group_scatter": (C.c_int, [_vp, sz, _vp, _vp, C.c_uint32, sz, _vp, _vp, _vp, _vp]),
+        # include/kfec_pipeline.h
+        "kfec_txq_create": (C.c_int, [_vp, sz, sz, C.POINTER(_vp)]),
+        "kfec_txq_destroy": (None, [_vp]),
+        "kfec_txq_pending": (sz, [_vp]),
+        "kfec_tx_create": (C.c_int, [_vp, C.c_uint32, C.c_uint64, C.POINTER(_vp)]),
+        "kfec_tx_destroy": (None, [_vp]),
+        "kfec_tx_send": (C.c_int, [_vp, _u8p, sz, C.c_uint32, _u8p, _szp]),
+        "kfec_txq_flush": (C.c_int, [_vp, C.c_uint32, _vp, _vp, _vp]),
+        "kfec_rxq_create": (C.c_int, [_vp, sz, sz, C.POINTER(_vp)]),
+        "kfec_rxq_destroy": (None, [_vp]),
+        "kfec_rxq_pending": (sz, [_vp]),
+        "kfec_rx_create": (C.c_int, [_vp, C.c_uint64, C.POINTER(_vp)]),
+        "kfec_rx_destroy": (None, [_vp]),
+        "kfec_rx_cached": (sz, [_vp]),
+        "kfec_rx_push": (C.c_int, [_vp, _u8p, sz, C.POINTER(_u8p), _szp]),
+        "kfec_rxq_flush": (C.c_int, [_vp, _vp, _vp, _vp]),
         "kfec_seal_batch": (C.c_int, [C.c_int, sz, _vp, sz, _vp, _vp, _vp, sz, _vp, _vp]),
         "kfec_open_batch": (C.c_int, [C.c_int, sz, _vp, sz, _vp, _vp, _vp, sz, _vp, _vp, _vp]),
     }

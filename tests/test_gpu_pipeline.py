@@ -1,0 +1,132 @@
+"""GPU tests of the batched fec_maker / fec_find_missings pipeline (include/kfec_pipeline.h) against the
+oracle's restatement of the same reference functions (oracle/frame_oracle.py FecTx / FecRx).
+
+Bar: the data packets are byte-identical to create_fec_data_packet's, the redundant packets to
+create_fec_redundant_packet's over the oracle encoder's parity, and through a lossy multi-connection channel
+the receiver hands KCP exactly the datagrams the oracle's fec_unpack / fec_find_missings hands it (same set,
+same per-group recovered datagrams), with the same cache expiry.
+"""
+from __future__ import annotations
+
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import frame_oracle as fo  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from kcptube_amd import load_library
+    load_library()
+    return torch.device("cuda:0")
+
+
+def _coder(K, N):
+    from kcptube_amd import FecCode
+    return FecCode(K, N)
+
+
+@pytest.mark.parametrize("K,N,mtu", [(20, 23, 1440), (10, 13, 1400), (4, 6, 100)])
+def test_sender_packets_match_oracle(dev, oracle, K, N, mtu):
+    from kcptube_amd.pipeline import FecSender, TxQueue
+    c = _coder(K, N)
+    q = TxQueue(c, max_groups=64, max_datagram=mtu)
+    rng = random.Random(K)
+    conns = [(FecSender(q, conv=0x1000 + i, tag=i), fo.FecTx(K, N, lambda d, t, a: oracle.encode(K, N, d, a, t),
+                                                             conv=0x1000 + i)) for i in range(3)]
+    exp_red = []
+    for step in range(K * 7 + 3):
+        for tag, (tx, ref) in enumerate(conns):
+            d = rng.randbytes(rng.choice([0, 1, mtu, rng.randint(0, mtu)]))
+            pkt = tx.send(d, timestamp=1234)
+            ref_pkts = ref.send(d, timestamp=1234)
+            assert pkt == ref_pkts[0]
+            exp_red += [(tag, p) for p in ref_pkts[1:]]
+    assert q.pending() == 3 * 7
+    got = q.flush(timestamp=1234)
+    assert q.pending() == 0
+    assert sorted((t, p) for t, _, _, p in got) == sorted(exp_red)
+    for t, sn, sub, p in got:
+        assert p[8] == sub and int.from_bytes(p[4:8], "big") == sn
+
+
+def test_sender_conv_zero_builds_no_groups(dev):
+    from kcptube_amd.pipeline import FecSender, TxQueue
+    c = _coder(3, 5)
+    q = TxQueue(c, 4, 64)
+    tx = FecSender(q, conv=0)
+    for i in range(10):
+        p = tx.send(b"x" * i)
+        assert p[8] == 0 and int.from_bytes(p[4:8], "big") == 0  # sub_sn reset, sn never advances
+    assert q.pending() == 0
+
+
+def test_queue_full_is_reported_without_side_effects(dev):
+    from kcptube_amd.fec import KfecError
+    from kcptube_amd.pipeline import FecSender, TxQueue
+    c = _coder(2, 3)
+    q = TxQueue(c, 1, 16)
+    tx = FecSender(q, conv=5)
+    tx.send(b"a"), tx.send(b"b")
+    tx.send(b"c")
+    with pytest.raises(KfecError):
+        tx.send(b"d")  # would complete a second group
+    assert q.pending() == 1
+    assert len(q.flush()) == 1
+    assert tx.send(b"d")[8] == 1  # the refused datagram was not counted
+
+
+@pytest.mark.parametrize("K,N,mtu", [(20, 23, 1440), (6, 9, 300)])
+def test_receiver_matches_oracle_through_lossy_channel(dev, oracle, K, N, mtu):
+    from kcptube_amd.pipeline import FecReceiver, RxQueue
+    c = _coder(K, N)
+    rq = RxQueue(c, max_groups=256, max_shard=mtu + 2)
+    rng = random.Random(N)
+    conns = 3
+    streams = []
+    for i in range(conns):
+        tx = fo.FecTx(K, N, lambda d, t, a: oracle.encode(K, N, d, a, t), conv=77 + i)
+        pkts = []
+        for _ in range(K * 25):
+            pkts += tx.send(rng.randbytes(rng.randint(0, mtu)))
+        streams.append(pkts)
+    # per connection: drop ~8% of packets, interleave the connections, reorder slightly within a connection
+    rx = [FecReceiver(rq, tag=i) for i in range(conns)]
+    ref = [fo.FecRx(K, N, lambda s, a: oracle.decode(K, N, s, a)) for _ in range(conns)]
+    got = [[] for _ in range(conns)]
+    exp = [[] for _ in range(conns)]
+    order = []
+    for i, pkts in enumerate(streams):
+        kept = [p for p in pkts if rng.random() >= 0.08]
+        for j in range(0, len(kept) - 1, 7):
+            kept[j], kept[j + 1] = kept[j + 1], kept[j]
+        order.append(kept)
+    pos = [0] * conns
+    while any(pos[i] < len(order[i]) for i in range(conns)):
+        i = rng.randrange(conns)
+        if pos[i] >= len(order[i]):
+            continue
+        p = order[i][pos[i]]
+        pos[i] += 1
+        own, _ = rx[i].push(p)
+        if own is not None:
+            got[i].append(own)
+        exp[i] += ref[i].push(p)
+        if rq.pending() > 200:
+            for tag, sn, idx, d in rq.flush():
+                got[tag].append(d)
+    for tag, sn, idx, d in rq.flush():
+        got[tag].append(d)
+    n_rec = 0
+    for i in range(conns):
+        assert sorted(got[i]) == sorted(exp[i]), i
+        assert rx[i].cached() == len(ref[i].cache)
+        n_rec += ref[i].recovered
+    assert n_rec > 20
