@@ -84,6 +84,7 @@ int kfec_unframe_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, co
 
 #define KFEC_PACK_DATA 1u       /* emit the K data packets of each group */
 #define KFEC_PACK_REDUNDANT 2u  /* emit the R redundant packets of each group */
+#define KFEC_PACK_COMPACT 4u    /* lay out only the emitted kinds: [G][K] data, [G][R] redundant, or [G][N] */
 
 /* create_fec_data_packet / create_fec_redundant_packet (connections.cpp:395-430) for G encoded groups.
  * Packet s of group g goes to d_pkt + (g*N + s) * pkt_pitch with its length in d_pkt_len[g*N + s]:
@@ -91,7 +92,8 @@ int kfec_unframe_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, co
  *   s >= K: [LE32 timestamp][BE32 d_sn[g]][u8 s][BE32 d_conv[g]][parity s-K, d_align[g] bytes] 13 + align
  * (sub_sn numbering as fec_maker, client.cpp:797-840: data 0..K-1, redundant K..N-1).  Bytes of the
  * packet slot past the packet's length, up to the next multiple of 4, are written as zero.  Groups with
- * d_align[g] == 0 get length-0 redundant packets. */
+ * d_align[g] == 0 get length-0 redundant packets.  With KFEC_PACK_COMPACT in `which`, slot (g, s) is
+ * instead g * n_kinds + (s - first emitted s), e.g. [G][R] for the redundant packets alone. */
 int kfec_pack_batch(const kfec_ctx *ctx, size_t G, unsigned which, const void *d_src, size_t src_bytes,
                     const uint64_t *d_off, const uint16_t *d_len, size_t pitch, const void *d_parity,
                     const uint16_t *d_align, const uint32_t *d_sn, const uint32_t *d_conv, uint32_t timestamp,

@@ -45,7 +45,7 @@ typedef struct kfec_rx kfec_rx;
 /* ---- send -------------------------------------------------------------------------------------------- */
 
 /* A batched encode queue for the coder's fec=K:N-K: up to max_groups complete groups of datagrams of at most
- * max_datagram bytes (kcp_mtu) between flushes.  Device buffers are allocated at the first flush. */
+ * max_datagram bytes (kcp_mtu) between flushes.  Pinned host and device buffers are allocated here. */
 int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram, kfec_txq **out);
 void kfec_txq_destroy(kfec_txq *q);
 size_t kfec_txq_pending(const kfec_txq *q);
@@ -72,7 +72,7 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
 /* ---- receive ----------------------------------------------------------------------------------------- */
 
 /* A batched decode queue: up to max_groups decodable groups whose shards are at most max_shard bytes
- * (kcp_mtu + 2, the parity length) between flushes.  Device buffers are allocated at the first flush. */
+ * (kcp_mtu + 2, the parity length) between flushes.  Pinned host and device buffers are allocated here. */
 int kfec_rxq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_shard, kfec_rxq **out);
 void kfec_rxq_destroy(kfec_rxq *q);
 size_t kfec_rxq_pending(const kfec_rxq *q);

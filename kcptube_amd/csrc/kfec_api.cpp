@@ -359,7 +359,7 @@ int kfec_pack_batch(const kfec_ctx *ctx, size_t G, unsigned which, const void *d
                     const uint16_t *d_align, const uint32_t *d_sn, const uint32_t *d_conv, uint32_t timestamp,
                     void *d_pkt, size_t pkt_pitch, uint16_t *d_pkt_len, void *stream)
 {
-    if (!ctx || pkt_pitch % 4 || (which & ~(KFEC_PACK_DATA | KFEC_PACK_REDUNDANT))) return KFEC_EINVAL;
+    if (!ctx || pkt_pitch % 4 || (which & ~(KFEC_PACK_DATA | KFEC_PACK_REDUNDANT | KFEC_PACK_COMPACT))) return KFEC_EINVAL;
     if (G && (!d_sn || !d_pkt || !al4(d_pkt) || !d_pkt_len)) return KFEC_EINVAL;
     if (G && (which & KFEC_PACK_DATA) && (!d_src || !al4(d_src) || !d_off || !d_len)) return KFEC_EINVAL;
     if (G && (which & KFEC_PACK_REDUNDANT) && ctx->N > ctx->K &&

@@ -232,7 +232,7 @@ struct PackArgs {
     uint8_t *pkt;
     uint16_t *pkt_len;
     uint64_t pitch, pkt_pitch, rows;
-    uint32_t K, N, which, timestamp;
+    uint32_t K, N, which, timestamp, nsel, s0;
 };
 
 __global__ void __launch_bounds__(kFrameBlock) pack_kernel(PackArgs a)
@@ -244,10 +244,12 @@ __global__ void __launch_bounds__(kFrameBlock) pack_kernel(PackArgs a)
         const uint32_t s = (uint32_t)(pk - g * a.N);
         const bool red = s >= a.K;
         if (!(a.which & (red ? KFEC_PACK_REDUNDANT : KFEC_PACK_DATA))) continue;
+        // output slot: (g, s) of [G][N], or of [G][emitted kinds] with KFEC_PACK_COMPACT
+        const uint64_t slot = (a.which & KFEC_PACK_COMPACT) ? g * a.nsel + (s - a.s0) : pk;
         const uint32_t H = red ? KFEC_PKT_REDUNDANT_HEADER : KFEC_PKT_DATA_HEADER;
         const uint32_t n = red ? a.align[g] : a.len[g * a.K + s];
         const bool fits = H + n <= a.pkt_pitch && !(red && n == 0);
-        if (lane == 0) a.pkt_len[pk] = fits ? (uint16_t)(H + n) : (uint16_t)0;
+        if (lane == 0) a.pkt_len[slot] = fits ? (uint16_t)(H + n) : (uint16_t)0;
         if (!fits) continue;
         uint32_t h[4];
         h[0] = a.timestamp;      // host_to_little_endian
@@ -266,7 +268,7 @@ __global__ void __launch_bounds__(kFrameBlock) pack_kernel(PackArgs a)
             lim = a.src_dw;
             off = a.off[g * a.K + s];
         }
-        uint32_t *dst = reinterpret_cast<uint32_t *>(a.pkt + pk * a.pkt_pitch);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(a.pkt + slot * a.pkt_pitch);
         store_quads(dst, (H + n + 3) / 4, h, H, base, lim, off, n, lane);
     }
 }
@@ -577,6 +579,8 @@ int launch_pack(int K, int N, size_t G, unsigned which, const void *src, size_t 
     a.N = N;
     a.which = which;
     a.timestamp = timestamp;
+    a.nsel = ((which & KFEC_PACK_DATA) ? K : 0) + ((which & KFEC_PACK_REDUNDANT) ? N - K : 0);
+    a.s0 = (which & KFEC_PACK_DATA) ? 0 : K;
     a.rows = (uint64_t)G * N;
     hipLaunchKernelGGL(pack_kernel, dim3(grid_rows(a.rows)), dim3(kFrameBlock), 0, s, a);
     return launched();

@@ -52,6 +52,10 @@ uint32_t engine_error_word()
 }
 
 static constexpr int kBlock = 256;
+#ifndef KFEC_MAC_BLOCK
+#define KFEC_MAC_BLOCK 256
+#endif
+static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened MAC kernel
 
 // build-time tuning knobs (tools/ab.py builds variants; the shipped library uses the defaults)
 #ifndef KFEC_PD
@@ -805,7 +809,7 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
 }
 
 template <int VEC, int MT, bool DEC>
-__global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
+__global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
 {
     using L = MacLayout<MT>;
     constexpr int W = Gran<VEC>::W;
@@ -821,7 +825,7 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
         mac_expand<MT, false>(a, s_ent, 0, 1, 0, K, row0);
         __syncthreads();
     }
-    const uint32_t stride = gridDim.x * kBlock;
+    const uint32_t stride = gridDim.x * kMacBlock;
     // XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs, so workgroup b would run
     // next to b+8, not b+1.  Re-numbering (bijective, MI355X guide T1) gives each XCD a contiguous run of
     // items, so the 128-B lines that straddle two workgroups' columns are fetched by one L2, not two.
@@ -834,7 +838,7 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
 #endif
     // decode with a work list: only the groups that lost data shards are visited (list index space)
     const uint32_t total = (DEC && a.list) ? min(*a.list_count, a.G) * cols : a.total;
-    for (uint32_t base = wg * kBlock; base < total; base += stride) {
+    for (uint32_t base = wg * kMacBlock; base < total; base += stride) {
         const uint32_t item = base + threadIdx.x;
         const uint32_t gi = item < total ? item / cols : 0;  // list index (= group without a list)
         const uint32_t col = item < total ? item - gi * cols : 0;
@@ -844,7 +848,7 @@ __global__ void __launch_bounds__(kBlock, KFEC_MINW) mac_kernel(MacArgs a)
         // divide B (VEC >= 4 only; the bytewise VEC = 1 path checks every byte itself)
         const uint32_t nd = (VEC >= 4 && (col + 1) * VB > a.B) ? (a.B - col * VB + 3) / 4 : (uint32_t)W;
         const uint32_t gfirst = base / cols;
-        const uint32_t glast = min(base + kBlock - 1, total - 1) / cols;
+        const uint32_t glast = min(base + kMacBlock - 1, total - 1) / cols;
         const uint32_t ng = glast - gfirst + 1;
         const uint32_t gs = DEC ? gi - gfirst : 0;
 
@@ -1743,7 +1747,7 @@ static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
     // 6.90 -> 6.08 ms and decode 7.39 -> 6.75 ms at 20:3 B=1440 1M groups, 205 -> 173 ms encode at 200:55
     // (DESIGN.md 5).  With several row tiles the grid's x extent stays a multiple of the 8 XCDs, so
     // workgroups (x, y) and (x, y') share an XCD and the tiles' re-reads of the same shard bytes hit its L2.
-    const uint32_t want = (a.total + kBlock - 1) / kBlock;
+    const uint32_t want = (a.total + kMacBlock - 1) / kMacBlock;
     static const int persist = env_int("KFEC_GRID_PERSIST", 0);
     uint32_t gx = want;
     if (persist) {
@@ -1755,7 +1759,7 @@ static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
         gx = (want + 7) & ~7u;
     }
     gx = std::max(1u, gx);
-    hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC>), dim3(gx, tiles), dim3(kBlock), lds, s, a);
+    hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC>), dim3(gx, tiles), dim3(kMacBlock), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -2213,7 +2217,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         hipLaunchKernelGGL(compact_kernel, dim3((uint32_t)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, (uint64_t)G,
                            (uint32_t)R, d_status, d_out_idx, count, list);
         if (hipGetLastError() != hipSuccess) return -3;
-        const uint32_t gmax = (uint32_t)std::min<size_t>(G, (kBlock - 1) / cpad + 2);
+        const uint32_t gmax = (uint32_t)std::min<size_t>(G, (kMacBlock - 1) / cpad + 2);
         const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
         MacArgs a{};
         a.data = static_cast<const uint8_t *>(d_data);
@@ -2235,7 +2239,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         return dispatch_mac<true>(di, vec, mt, a, tiles, s);
     }
     return for_group_ranges(G, cpad, [&](size_t g0, size_t gn) {
-        const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kBlock - 1) / cpad + 2);
+        const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kMacBlock - 1) / cpad + 2);
         const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
         MacArgs a{};
         a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;

@@ -1,0 +1,139 @@
+// pipeline_bench.cpp -- host-memory end to end of the batched FEC path (include/kfec_pipeline.h):
+// C connections, each sending datagrams through kfec_tx (data packets built on the host at once, complete
+// groups coded on the GPU at each flush), then the packets of every group minus `loss` of them per group
+// pushed through kfec_rx (receive cache + fec_find_missings scan on the host, decodable groups decoded on the
+// GPU at each flush).  Reports host-side per-packet cost, GPU flush time (including the pinned H2D / D2H
+// copies) and the datagram payload rate of each direction, on ONE host thread, and checks every recovered
+// datagram.
+// Build: g++ -O2 -std=c++17 -I include tools/pipeline_bench.cpp -o tools/pipeline_bench -L kcptube_amd -lkfec
+//        -Wl,-rpath,$PWD/kcptube_amd
+// Usage: tools/pipeline_bench [K N mtu groups_per_flush flushes loss]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "kfec_pipeline.h"
+
+using clk = std::chrono::steady_clock;
+
+struct Sink {
+    std::vector<std::vector<uint8_t>> pkts;
+    size_t bytes = 0, n = 0;
+};
+
+static void on_pkt(void *u, uint64_t, uint32_t, uint8_t, const uint8_t *p, size_t len)
+{
+    auto *s = static_cast<Sink *>(u);
+    s->pkts.emplace_back(p, p + len);
+}
+
+struct Rec {
+    size_t n = 0, bytes = 0, bad = 0;
+    const std::vector<std::vector<uint8_t>> *orig;
+    size_t K;
+};
+
+static void on_dg(void *u, uint64_t tag, uint32_t sn, uint8_t idx, const uint8_t *d, size_t len)
+{
+    auto *r = static_cast<Rec *>(u);
+    r->n++;
+    r->bytes += len;
+    (void)tag;
+    const auto &o = (*r->orig)[(size_t)sn * r->K + idx];
+    if (o.size() != len || std::memcmp(o.data(), d, len)) r->bad++;
+}
+
+int main(int argc, char **argv)
+{
+    const size_t K = argc > 1 ? atoi(argv[1]) : 20, N = argc > 2 ? atoi(argv[2]) : 23;
+    const size_t mtu = argc > 3 ? atoi(argv[3]) : 1440, G = argc > 4 ? atoi(argv[4]) : 16384;
+    const int flushes = argc > 5 ? atoi(argv[5]) : 4;
+    const size_t loss = argc > 6 ? atoi(argv[6]) : 3;
+    const size_t R = N - K;
+    kfec_ctx *ctx = nullptr;
+    if (kfec_create(K, N, &ctx)) { printf("no GPU\n"); return 1; }
+    kfec_txq *tq;
+    kfec_rxq *rq;
+    kfec_txq_create(ctx, G, mtu, &tq);
+    kfec_rxq_create(ctx, G, mtu + 2, &rq);
+    kfec_tx *tx;
+    kfec_rx *rx;
+    kfec_tx_create(tq, 0x4B435054, 1, &tx);
+    kfec_rx_create(rq, 1, &rx);
+    std::mt19937_64 rng(7);
+    const size_t total_groups = G * flushes;
+    std::vector<std::vector<uint8_t>> dg(total_groups * K);
+    for (auto &d : dg) {
+        d.resize(mtu);
+        for (size_t i = 0; i < mtu; i += 8) {
+            const uint64_t v = rng();
+            std::memcpy(d.data() + i, &v, std::min<size_t>(8, mtu - i));
+        }
+    }
+    std::vector<std::vector<uint8_t>> data_pkts(total_groups * K);
+    Sink red;
+    double t_tx_host = 0, t_tx_flush = 0, t_rx_host = 0, t_rx_flush = 0;
+    std::vector<uint8_t> pkt(mtu + 16);
+    for (int f = 0; f < flushes; ++f) {
+        auto t0 = clk::now();
+        for (size_t g = f * G; g < (f + 1) * G; ++g)
+            for (size_t i = 0; i < K; ++i) {
+                size_t n = 0;
+                if (kfec_tx_send(tx, dg[g * K + i].data(), mtu, 1, pkt.data(), &n)) { printf("send failed\n"); return 1; }
+                data_pkts[g * K + i].assign(pkt.data(), pkt.data() + n);
+            }
+        auto t1 = clk::now();
+        if (kfec_txq_flush(tq, 1, on_pkt, &red, nullptr)) { printf("tx flush failed\n"); return 1; }
+        auto t2 = clk::now();
+        t_tx_host += std::chrono::duration<double>(t1 - t0).count();
+        t_tx_flush += std::chrono::duration<double>(t2 - t1).count();
+    }
+    // receive: every group loses `loss` data packets (worst case for the decoder)
+    Rec rec;
+    rec.orig = &dg;
+    rec.K = K;
+    size_t own = 0;
+    for (int f = 0; f < flushes; ++f) {
+        auto t0 = clk::now();
+        for (size_t g = f * G; g < (f + 1) * G; ++g) {
+            for (size_t i = loss; i < K; ++i) {
+                const uint8_t *d;
+                size_t dn;
+                if (kfec_rx_push(rx, data_pkts[g * K + i].data(), data_pkts[g * K + i].size(), &d, &dn) < 0) {
+                    printf("push failed\n");
+                    return 1;
+                }
+                own += dn;
+            }
+            for (size_t r = 0; r < R; ++r) {
+                const auto &p = red.pkts[g * R + r];
+                if (kfec_rx_push(rx, p.data(), p.size(), nullptr, nullptr) < 0) { printf("push failed\n"); return 1; }
+            }
+        }
+        auto t1 = clk::now();
+        if (kfec_rxq_flush(rq, on_dg, &rec, nullptr)) { printf("rx flush failed\n"); return 1; }
+        auto t2 = clk::now();
+        t_rx_host += std::chrono::duration<double>(t1 - t0).count();
+        t_rx_flush += std::chrono::duration<double>(t2 - t1).count();
+    }
+    const double payload = (double)total_groups * K * mtu;
+    const double npk_tx = (double)total_groups * K, npk_rx = (double)total_groups * (K - loss + R);
+    printf("{\"metric\": \"batched FEC pipeline, host memory in and out (1 host thread)\", \"fec\": \"%zu:%zu\", "
+           "\"kcp_mtu\": %zu, \"groups_per_flush\": %zu, \"flushes\": %d, \"loss_per_group\": %zu, "
+           "\"tx_host_ns_per_packet\": %.1f, \"tx_flush_ms\": %.3f, \"tx_GiBps\": %.3f, \"tx_flush_only_GiBps\": %.2f, "
+           "\"rx_host_ns_per_packet\": %.1f, \"rx_flush_ms\": %.3f, \"rx_GiBps\": %.3f, \"rx_flush_only_GiBps\": %.2f, "
+           "\"recovered\": %zu, \"recovered_expected\": %zu, \"bad\": %zu}\n",
+           K, R, mtu, G, flushes, loss, t_tx_host / npk_tx * 1e9, t_tx_flush / flushes * 1e3,
+           payload / (t_tx_host + t_tx_flush) / (1 << 30), payload / t_tx_flush / (1 << 30), t_rx_host / npk_rx * 1e9,
+           t_rx_flush / flushes * 1e3, payload / (t_rx_host + t_rx_flush) / (1 << 30), payload / t_rx_flush / (1 << 30),
+           rec.n, total_groups * loss, rec.bad);
+    kfec_tx_destroy(tx);
+    kfec_rx_destroy(rx);
+    kfec_txq_destroy(tq);
+    kfec_rxq_destroy(rq);
+    kfec_destroy(ctx);
+    return (rec.bad == 0 && rec.n == total_groups * loss) ? 0 : 3;
+}
