@@ -23,7 +23,11 @@
  * batching buys.  Shard padding is zero (include/kfec_frame.h).
  *
  * Threading: a kfec_tx / kfec_rx and its queue are used from one thread at a time (the reference serialises
- * with mutex_fec_snd / mutex_fec_rcv, connections.hpp:609-611).
+ * with mutex_fec_snd / mutex_fec_rcv, connections.hpp:609-611).  Destroy the kfec_tx / kfec_rx of a queue
+ * before the queue.
+ * Staging: datagrams and shards are copied once, into the queue's pinned arena, when they arrive; finished
+ * 8 MiB stretches of it go H2D on the queue's own copy stream while the host keeps filling it, so a flush
+ * waits only for the tail, the kernels and the D2H of its results.
  */
 #ifndef KFEC_PIPELINE_H_
 #define KFEC_PIPELINE_H_
@@ -57,8 +61,11 @@ void kfec_tx_destroy(kfec_tx *tx);
 
 /* fec_maker(input_data, data_size): writes the data packet to pkt[9 + len] (*pkt_len) and, when this
  * datagram completes a group, queues the group (its redundant packets come from kfec_txq_flush).
- * KFEC_EINVAL for a datagram longer than max_datagram; KFEC_ENOMEM, with nothing sent, when the datagram
- * would complete a group and the queue is full (flush first). */
+ * The datagram is stored once, in the queue's staging arena (max_groups x K datagram slots, shared by the
+ * complete groups and every sender's partial group; a flush keeps the partial groups).  KFEC_EINVAL for a
+ * datagram longer than max_datagram; KFEC_ENOMEM, with nothing sent, when the datagram would complete a
+ * group and the queue is full, or the arena is full (flush first; size max_groups above the number of
+ * senders so that their partial groups alone never fill it). */
 int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t timestamp, uint8_t *pkt,
                  size_t *pkt_len);
 
@@ -87,7 +94,9 @@ size_t kfec_rx_cached(const kfec_rx *rx);
  * for decoding and marked restored).  For a data packet *datagram / *datagram_len point at its payload inside
  * pkt (what fec_unpack returns to its caller for KCP::Input); NULL / 0 otherwise.  Returns the number of
  * groups queued by this call, KFEC_EINVAL for a packet shorter than its header or a shard longer than
- * max_shard, KFEC_ENOMEM when the decode queue might overflow (flush first; the packet is then not cached). */
+ * max_shard, KFEC_ENOMEM when the decode queue might overflow or the staging arena (max_groups x N shard
+ * slots, which also holds the shards of groups still waiting for K shares) is full (flush first; the packet
+ * is then not cached).  The payload is stored once, in that arena; a flush keeps the waiting groups' shards. */
 int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **datagram, size_t *datagram_len);
 
 /* Recovered datagram callback: tag of the kfec_rx, group sn, data index, bytes (what KCP::Input gets). */

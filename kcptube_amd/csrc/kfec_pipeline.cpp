@@ -9,8 +9,8 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <new>
-#include <set>
 #include <vector>
 
 namespace {
@@ -54,6 +54,48 @@ struct Device {
     ~Device() { if (p) (void)hipFree(p); }
 };
 
+// Append-only staging uploaded while the host is still filling it: every kUploadChunk bytes of finished
+// groups go H2D on the queue's own copy stream, so the PCIe transfer overlaps the per-packet host work and a
+// flush only copies the tail.  Bytes already queued for DMA are never written again before the flush has
+// synchronised (the arena is append-only between flushes).
+struct Upload {
+    static constexpr size_t kUploadChunk = size_t(8) << 20;
+    hipStream_t cs = nullptr;
+    hipEvent_t ev = nullptr;
+    size_t issued = 0;
+    int init(int device)
+    {
+        if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+            return KFEC_EHIP;
+        return KFEC_OK;
+    }
+    // called after the arena grew to `used` bytes: start the copy of the finished bytes once a chunk is ready
+    void grow(const Pinned &h, const Device &d, size_t used)
+    {
+        if (used - issued < kUploadChunk) return;
+        if (hipMemcpyAsync(static_cast<uint8_t *>(d.p) + issued, static_cast<const uint8_t *>(h.p) + issued,
+                           used - issued, hipMemcpyHostToDevice, cs) == hipSuccess)
+            issued = used;  // on failure the bytes are simply copied again by finish()
+    }
+    // copy the tail and make `s` wait for every upload
+    int finish(const Pinned &h, const Device &d, size_t used, hipStream_t s)
+    {
+        if (used > issued && hipMemcpyAsync(static_cast<uint8_t *>(d.p) + issued, static_cast<const uint8_t *>(h.p) + issued,
+                                            used - issued, hipMemcpyHostToDevice, cs) != hipSuccess)
+            return KFEC_EHIP;
+        issued = 0;
+        if (hipEventRecord(ev, cs) != hipSuccess || hipStreamWaitEvent(s, ev, 0) != hipSuccess) return KFEC_EHIP;
+        return KFEC_OK;
+    }
+    ~Upload()
+    {
+        if (cs) (void)hipStreamSynchronize(cs);
+        if (ev) (void)hipEventDestroy(ev);
+        if (cs) (void)hipStreamDestroy(cs);
+    }
+};
+
 inline void put_le32(uint8_t *p, uint32_t v)
 {
     p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
@@ -72,11 +114,15 @@ inline uint32_t get_be32(const uint8_t *p)
 // ---- send ------------------------------------------------------------------------------------------------
 struct kfec_txq {
     const kfec_ctx *ctx = nullptr;
-    size_t K = 0, N = 0, R = 0, G = 0, mtu = 0, slot = 0;  // slot: datagram stride in the staging arena
+    size_t K = 0, N = 0, R = 0, G = 0, mtu = 0, slot = 0;  // slot: datagram stride of a kfec_tx group cache
     size_t n = 0;                                          // complete groups queued
+    size_t used = 0;  // staged datagram bytes (packed back to back at 4-byte offsets: one H2D of these)
+    size_t cap = 0;   // staging arena bytes
+    std::vector<kfec_tx *> txs;  // the senders whose partial groups live in the arena
     Pinned h_dg, h_off, h_len, h_sn, h_conv, h_pkt, h_pkt_len;
     std::vector<uint64_t> tags;
     Device d_dg, d_off, d_len, d_sn, d_conv, d_par, d_align, d_pkt, d_pkt_len;
+    Upload up;  // declared after the buffers: destroyed (and drained) before them
 };
 
 struct kfec_tx {
@@ -85,8 +131,8 @@ struct kfec_tx {
     uint64_t tag = 0;
     uint32_t sn = 0;      // fec_snd_sn
     uint8_t sub_sn = 0;   // fec_snd_sub_sn
-    // fec_snd_cache: the group's datagrams so far, in one preallocated K x max_datagram buffer
-    std::vector<uint8_t> cache;
+    // fec_snd_cache: the group's datagrams so far, stored once, straight into the queue's staging arena
+    std::vector<uint64_t> cache_off;
     std::vector<uint16_t> cache_len;
     size_t cached = 0;
 };
@@ -120,6 +166,11 @@ int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram,
         delete q;
         return KFEC_ENOMEM;
     }
+    if (q->up.init(kfec_device(ctx))) {
+        delete q;
+        return KFEC_EHIP;
+    }
+    q->cap = GK * q->slot;
     q->tags.resize(q->G);
     *out = q;
     return KFEC_OK;
@@ -140,8 +191,9 @@ int kfec_tx_create(kfec_txq *q, uint32_t conv, uint64_t tag, kfec_tx **out)
     tx->conv = conv;
     tx->tag = tag;
     try {
-        tx->cache.resize(q->K * q->slot);
+        tx->cache_off.resize(q->K);
         tx->cache_len.resize(q->K);
+        q->txs.push_back(tx);
     } catch (...) {
         delete tx;
         return KFEC_ENOMEM;
@@ -150,7 +202,13 @@ int kfec_tx_create(kfec_txq *q, uint32_t conv, uint64_t tag, kfec_tx **out)
     return KFEC_OK;
 }
 
-void kfec_tx_destroy(kfec_tx *tx) { delete tx; }
+void kfec_tx_destroy(kfec_tx *tx)
+{
+    if (!tx) return;
+    auto &v = tx->q->txs;
+    v.erase(std::remove(v.begin(), v.end(), tx), v.end());
+    delete tx;
+}
 
 int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t timestamp, uint8_t *pkt, size_t *pkt_len)
 {
@@ -159,6 +217,7 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
     if (len > q->mtu) return KFEC_EINVAL;
     const bool completes = tx->conv != 0 && tx->cached + 1 == q->K;
     if (completes && q->n == q->G) return KFEC_ENOMEM;
+    if (tx->conv != 0 && q->used + round4(len) > q->cap) return KFEC_ENOMEM;
     // create_fec_data_packet (connections.cpp:395-411), sub_sn = fec_snd_sub_sn++ (client.cpp:805-806)
     put_le32(pkt, timestamp);
     put_be32(pkt + 4, tx->sn);
@@ -169,17 +228,18 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
         tx->sub_sn = 0;
         return KFEC_OK;
     }
-    if (len) std::memcpy(tx->cache.data() + tx->cached * q->slot, datagram, len);
+    if (len) std::memcpy(q->h_dg.as<uint8_t>() + q->used, datagram, len);
+    tx->cache_off[tx->cached] = q->used;
     tx->cache_len[tx->cached++] = (uint16_t)len;
+    q->used += round4(len);
     if (!completes) return KFEC_OK;
-    // the group is complete: copy it into queue slot n (compact_into_container + encode run at the flush)
+    // the group is complete: it takes queue slot n (compact_into_container + encode run at the flush)
     const size_t g = q->n;
-    std::memcpy(q->h_dg.as<uint8_t>() + g * q->K * q->slot, tx->cache.data(), q->K * q->slot);
     for (size_t i = 0; i < q->K; ++i) {
-        const size_t e = g * q->K + i;
-        q->h_off.as<uint64_t>()[e] = e * q->slot;
-        q->h_len.as<uint16_t>()[e] = tx->cache_len[i];
+        q->h_off.as<uint64_t>()[g * q->K + i] = tx->cache_off[i];
+        q->h_len.as<uint16_t>()[g * q->K + i] = tx->cache_len[i];
     }
+    q->up.grow(q->h_dg, q->d_dg, q->used);
     q->h_sn.as<uint32_t>()[g] = tx->sn;
     q->h_conv.as<uint32_t>()[g] = tx->conv;
     q->tags[g] = tx->tag;
@@ -200,13 +260,13 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
     const size_t B = q->mtu + KFEC_FEC_CONTAINER_HEADER, pitch = round4(B);
     const size_t pkt_pitch = round4(KFEC_PKT_REDUNDANT_HEADER + B);
     const size_t nk = n * K;
-    if (hipMemcpyAsync(q->d_dg.p, q->h_dg.p, nk * q->slot, hipMemcpyHostToDevice, s) != hipSuccess ||
+    if (q->up.finish(q->h_dg, q->d_dg, q->used, s) ||
         hipMemcpyAsync(q->d_off.p, q->h_off.p, nk * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(q->d_len.p, q->h_len.p, nk * 2, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(q->d_sn.p, q->h_sn.p, n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(q->d_conv.p, q->h_conv.p, n * 4, hipMemcpyHostToDevice, s) != hipSuccess)
         return KFEC_EHIP;
-    const size_t arena = nk * q->slot;
+    const size_t arena = std::max<size_t>(q->used, 4);
     int rc = kfec_encode_framed_batch(q->ctx, n, q->d_dg.p, arena, q->d_off.as<uint64_t>(), q->d_len.as<uint16_t>(), B,
                                       pitch, q->d_par.p, q->d_align.as<uint16_t>(), stream);
     if (rc) return rc;
@@ -229,6 +289,25 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
             if (len) cb(user, q->tags[g], sn[g], (uint8_t)(K + r), q->h_pkt.as<uint8_t>() + (g * R + r) * pkt_pitch, len);
         }
     q->n = 0;
+    // keep the partial groups: move their datagrams to the front of the arena, in arena order (every
+    // destination lies at or below its source, so memmove in that order never overwrites unread bytes)
+    struct Part {
+        uint64_t off;
+        size_t len;
+        uint64_t *rec;  // where the offset is recorded
+        bool operator<(const Part &o) const { return off < o.off; }
+    };
+    std::vector<Part> part;
+    for (kfec_tx *tx : q->txs)
+        for (size_t i = 0; i < tx->cached; ++i) part.push_back({tx->cache_off[i], tx->cache_len[i], &tx->cache_off[i]});
+    std::sort(part.begin(), part.end());
+    size_t at = 0;
+    for (const Part &p : part) {
+        if (p.len && at != p.off) std::memmove(q->h_dg.as<uint8_t>() + at, q->h_dg.as<uint8_t>() + p.off, p.len);
+        *p.rec = at;
+        at += round4(p.len);
+    }
+    q->used = at;
     return KFEC_OK;
 }
 
@@ -238,34 +317,63 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
 struct kfec_rxq {
     const kfec_ctx *ctx = nullptr;
     size_t K = 0, N = 0, R = 0, G = 0, max_shard = 0, slot = 0;
-    size_t n = 0;  // groups queued for decoding
+    size_t n = 0;     // groups queued for decoding
+    size_t used = 0;  // arena bytes staged (shards packed back to back at 4-byte offsets: one H2D of these)
+    size_t cap = 0;   // staging arena bytes
+    std::vector<kfec_rx *> rxs;  // the receivers whose cached shards live in the arena
     Pinned h_arena, h_off, h_len, h_present, h_idx, h_rec_len, h_dst;
     std::vector<uint64_t> tags;
     std::vector<uint32_t> sns;
     Device d_arena, d_off, d_len, d_present, d_data, d_par, d_align, d_out, d_idx, d_st, d_ws, d_rec_len, d_dst;
+    Upload up;
+};
+
+// fec_rcv_cache[sn]: the shards of one group, by sub_sn.  The bytes live in the queue's staging arena (stored
+// once, at push); a restored group keeps only its membership (the reference never reads it again).
+struct RxGroup {
+    uint64_t off[256];
+    uint16_t len[256];
+    uint64_t has[4];
+    uint32_t count;  // distinct sub_sn cached: fec_rcv_cache[sn].size()
+    bool restored;   // sn in fec_rcv_restored (restored is always a subset of the cache's keys)
+    bool test(unsigned s) const { return (has[s >> 6] >> (s & 63)) & 1; }
 };
 
 struct kfec_rx {
     kfec_rxq *q = nullptr;
     uint64_t tag = 0;
-    std::map<uint32_t, std::map<uint8_t, std::vector<uint8_t>>> cache;  // fec_rcv_cache
-    std::set<uint32_t> restored;                                          // fec_rcv_restored
+    std::map<uint32_t, RxGroup *> cache;  // fec_rcv_cache + fec_rcv_restored
+    std::vector<std::unique_ptr<RxGroup>> pool;
+    std::vector<RxGroup *> free_groups;
+    RxGroup *get()
+    {
+        if (free_groups.empty()) {
+            pool.push_back(std::make_unique<RxGroup>());
+            free_groups.push_back(pool.back().get());
+        }
+        RxGroup *x = free_groups.back();
+        free_groups.pop_back();
+        x->has[0] = x->has[1] = x->has[2] = x->has[3] = 0;
+        x->count = 0;
+        x->restored = false;
+        return x;
+    }
 };
 
 namespace {
 
-// copy a decodable group into queue slot q->n
-void rx_enqueue(kfec_rxq *q, uint64_t tag, uint32_t sn, const std::map<uint8_t, std::vector<uint8_t>> &shards)
+// a decodable group takes queue slot q->n: its shards are already in the arena
+void rx_enqueue(kfec_rxq *q, uint64_t tag, uint32_t sn, const RxGroup &grp)
 {
     const size_t g = q->n;
     uint64_t *present = q->h_present.as<uint64_t>() + g * 4;
     present[0] = present[1] = present[2] = present[3] = 0;
-    for (const auto &[s, bytes] : shards) {
-        if (s >= q->N) continue;  // a sub_sn beyond N is cached by the reference but never selected usefully
+    // a sub_sn beyond N is cached by the reference (it counts towards size()) but never selected usefully
+    for (unsigned s = 0; s < q->N; ++s) {
+        if (!grp.test(s)) continue;
         const size_t e = g * q->N + s;
-        if (!bytes.empty()) std::memcpy(q->h_arena.as<uint8_t>() + e * q->slot, bytes.data(), bytes.size());
-        q->h_off.as<uint64_t>()[e] = e * q->slot;
-        q->h_len.as<uint16_t>()[e] = (uint16_t)bytes.size();
+        q->h_off.as<uint64_t>()[e] = grp.off[s];
+        q->h_len.as<uint16_t>()[e] = grp.len[s];
         present[s >> 6] |= 1ull << (s & 63);
     }
     q->tags[g] = tag;
@@ -303,6 +411,11 @@ int kfec_rxq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_shard, kf
         delete q;
         return KFEC_ENOMEM;
     }
+    if (q->up.init(kfec_device(ctx))) {
+        delete q;
+        return KFEC_EHIP;
+    }
+    q->cap = GN * q->slot;
     q->tags.resize(q->G);
     q->sns.resize(q->G);
     *out = q;
@@ -322,11 +435,23 @@ int kfec_rx_create(kfec_rxq *q, uint64_t tag, kfec_rx **out)
     if (!rx) return KFEC_ENOMEM;
     rx->q = q;
     rx->tag = tag;
+    try {
+        q->rxs.push_back(rx);
+    } catch (...) {
+        delete rx;
+        return KFEC_ENOMEM;
+    }
     *out = rx;
     return KFEC_OK;
 }
 
-void kfec_rx_destroy(kfec_rx *rx) { delete rx; }
+void kfec_rx_destroy(kfec_rx *rx)
+{
+    if (!rx) return;
+    auto &v = rx->q->rxs;
+    v.erase(std::remove(v.begin(), v.end(), rx), v.end());
+    delete rx;
+}
 
 size_t kfec_rx_cached(const kfec_rx *rx) { return rx ? rx->cache.size() : 0; }
 
@@ -347,11 +472,26 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
     if (plen + (red ? 0 : KFEC_FEC_CONTAINER_HEADER) > q->max_shard) return KFEC_EINVAL;
     const uint32_t fec_sn = get_be32(pkt + 4);
     // capacity: this push can queue at most every not-yet-restored cached group plus a new one
-    size_t could = rx->cache.count(fec_sn) ? 0 : 1;
+    auto found = rx->cache.find(fec_sn);
+    size_t could = found == rx->cache.end() ? 1 : 0;
     for (const auto &kv : rx->cache)
-        if (!rx->restored.count(kv.first)) ++could;
+        if (!kv.second->restored) ++could;
     if (q->n + could > q->G) return KFEC_ENOMEM;
-    rx->cache[fec_sn][sub].assign(payload, payload + plen);  // fec_rcv_cache[sn][sub_sn] = ... (client.cpp:869,887)
+    const bool store = found == rx->cache.end() || !found->second->restored;
+    if (store && q->used + round4(plen) > q->cap) return KFEC_ENOMEM;
+    // fec_rcv_cache[sn][sub_sn] = ... (client.cpp:869,887): a duplicate overwrites
+    RxGroup *grp = found != rx->cache.end() ? found->second : (rx->cache[fec_sn] = rx->get());
+    if (!grp->test(sub)) {
+        grp->has[sub >> 6] |= 1ull << (sub & 63);
+        grp->count++;
+    }
+    if (store) {
+        if (plen) std::memcpy(q->h_arena.as<uint8_t>() + q->used, payload, plen);
+        grp->off[sub] = q->used;
+        grp->len[sub] = (uint16_t)plen;
+        q->used += round4(plen);
+        q->up.grow(q->h_arena, q->d_arena, q->used);
+    }
     if (!red) {
         if (datagram) *datagram = payload;
         if (datagram_len) *datagram_len = plen;
@@ -360,18 +500,19 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
     int queued = 0;
     for (auto it = rx->cache.begin(); it != rx->cache.end();) {
         const uint32_t sn = it->first;
+        RxGroup *x = it->second;
         const bool stale = (uint32_t)(fec_sn - sn) > kFecWaits;
-        if (it->second.size() < q->K || rx->restored.count(sn)) {
-            if (stale) {
-                rx->restored.erase(sn);
+        if (x->count < q->K || x->restored) {
+            if (stale) {  // fec_rcv_restored.erase(sn) + fec_rcv_cache.erase(sn)
+                rx->free_groups.push_back(x);
                 it = rx->cache.erase(it);
             } else {
                 ++it;
             }
             continue;
         }
-        rx_enqueue(q, rx->tag, sn, it->second);
-        rx->restored.insert(sn);
+        rx_enqueue(q, rx->tag, sn, *x);
+        x->restored = true;
         ++queued;
         ++it;
     }
@@ -387,12 +528,12 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
     const size_t N = q->N, R = q->R;
     const size_t B = q->max_shard, pitch = round4(B), dst_pitch = round4(B);
     const size_t nn = n * N;
-    if (hipMemcpyAsync(q->d_arena.p, q->h_arena.p, nn * q->slot, hipMemcpyHostToDevice, s) != hipSuccess ||
+    if (q->up.finish(q->h_arena, q->d_arena, q->used, s) ||
         hipMemcpyAsync(q->d_off.p, q->h_off.p, nn * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(q->d_len.p, q->h_len.p, nn * 2, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(q->d_present.p, q->h_present.p, n * 32, hipMemcpyHostToDevice, s) != hipSuccess)
         return KFEC_EHIP;
-    int rc = kfec_frame_shards_batch(q->ctx, n, q->d_arena.p, nn * q->slot, q->d_off.as<uint64_t>(),
+    int rc = kfec_frame_shards_batch(q->ctx, n, q->d_arena.p, std::max<size_t>(q->used, 4), q->d_off.as<uint64_t>(),
                                      q->d_len.as<uint16_t>(), q->d_present.as<uint64_t>(), B, pitch, q->d_data.p,
                                      q->d_par.p, q->d_align.as<uint16_t>(), stream);
     if (rc) return rc;
@@ -417,6 +558,32 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
             cb(user, q->tags[g], q->sns[g], idx, q->h_dst.as<uint8_t>() + (g * R + t) * dst_pitch, len);
         }
     q->n = 0;
+    // keep the shards of the groups still waiting for K shares: move them to the front of the arena, in arena
+    // order (every destination lies at or below its source, so memmove in that order overwrites nothing unread)
+    struct Part {
+        uint64_t *off;
+        size_t len;
+        bool operator<(const Part &o) const { return *off < *o.off; }
+    };
+    std::vector<Part> part;
+    for (kfec_rx *rx : q->rxs)
+        for (auto &kv : rx->cache) {
+            RxGroup *x = kv.second;
+            if (x->restored) continue;
+            for (unsigned w = 0; w < 4; ++w)
+                for (uint64_t m = x->has[w]; m; m &= m - 1) {
+                    const unsigned sub = w * 64 + (unsigned)__builtin_ctzll(m);
+                    part.push_back({&x->off[sub], x->len[sub]});
+                }
+        }
+    std::sort(part.begin(), part.end());
+    size_t at = 0;
+    for (const Part &p : part) {
+        if (p.len && at != *p.off) std::memmove(q->h_arena.as<uint8_t>() + at, q->h_arena.as<uint8_t>() + *p.off, p.len);
+        *p.off = at;
+        at += round4(p.len);
+    }
+    q->used = at;
     return KFEC_OK;
 }
 

@@ -19,15 +19,20 @@
 
 using clk = std::chrono::steady_clock;
 
+// redundant packets land in one preallocated buffer (stride = max packet), so the flush time is the
+// library's, not the allocator's
 struct Sink {
-    std::vector<std::vector<uint8_t>> pkts;
-    size_t bytes = 0, n = 0;
+    std::vector<uint8_t> buf;
+    std::vector<uint16_t> len;
+    size_t stride = 0, n = 0;
+    const uint8_t *pkt(size_t i) const { return buf.data() + i * stride; }
 };
 
 static void on_pkt(void *u, uint64_t, uint32_t, uint8_t, const uint8_t *p, size_t len)
 {
     auto *s = static_cast<Sink *>(u);
-    s->pkts.emplace_back(p, p + len);
+    std::memcpy(s->buf.data() + s->n * s->stride, p, len);
+    s->len[s->n++] = (uint16_t)len;
 }
 
 struct Rec {
@@ -73,17 +78,25 @@ int main(int argc, char **argv)
             std::memcpy(d.data() + i, &v, std::min<size_t>(8, mtu - i));
         }
     }
-    std::vector<std::vector<uint8_t>> data_pkts(total_groups * K);
+    // data packets land in one preallocated buffer too (stride mtu + 16)
+    const size_t dstride = mtu + 16;
+    std::vector<uint8_t> data_pkts(total_groups * K * dstride);
+    std::vector<uint16_t> data_len(total_groups * K);
     Sink red;
+    red.stride = mtu + 16;
+    red.buf.resize(total_groups * R * red.stride);
+    red.len.resize(total_groups * R);
     double t_tx_host = 0, t_tx_flush = 0, t_rx_host = 0, t_rx_flush = 0;
-    std::vector<uint8_t> pkt(mtu + 16);
     for (int f = 0; f < flushes; ++f) {
         auto t0 = clk::now();
         for (size_t g = f * G; g < (f + 1) * G; ++g)
             for (size_t i = 0; i < K; ++i) {
                 size_t n = 0;
-                if (kfec_tx_send(tx, dg[g * K + i].data(), mtu, 1, pkt.data(), &n)) { printf("send failed\n"); return 1; }
-                data_pkts[g * K + i].assign(pkt.data(), pkt.data() + n);
+                if (kfec_tx_send(tx, dg[g * K + i].data(), mtu, 1, data_pkts.data() + (g * K + i) * dstride, &n)) {
+                    printf("send failed\n");
+                    return 1;
+                }
+                data_len[g * K + i] = (uint16_t)n;
             }
         auto t1 = clk::now();
         if (kfec_txq_flush(tq, 1, on_pkt, &red, nullptr)) { printf("tx flush failed\n"); return 1; }
@@ -102,15 +115,17 @@ int main(int argc, char **argv)
             for (size_t i = loss; i < K; ++i) {
                 const uint8_t *d;
                 size_t dn;
-                if (kfec_rx_push(rx, data_pkts[g * K + i].data(), data_pkts[g * K + i].size(), &d, &dn) < 0) {
+                if (kfec_rx_push(rx, data_pkts.data() + (g * K + i) * dstride, data_len[g * K + i], &d, &dn) < 0) {
                     printf("push failed\n");
                     return 1;
                 }
                 own += dn;
             }
             for (size_t r = 0; r < R; ++r) {
-                const auto &p = red.pkts[g * R + r];
-                if (kfec_rx_push(rx, p.data(), p.size(), nullptr, nullptr) < 0) { printf("push failed\n"); return 1; }
+                if (kfec_rx_push(rx, red.pkt(g * R + r), red.len[g * R + r], nullptr, nullptr) < 0) {
+                    printf("push failed\n");
+                    return 1;
+                }
             }
         }
         auto t1 = clk::now();
