@@ -71,6 +71,16 @@ int kfec_frame_shards_batch(const kfec_ctx *ctx, size_t G, const void *d_src, si
                             const uint64_t *d_off, const uint16_t *d_len, const uint64_t *d_present, size_t B,
                             size_t pitch, void *d_data, void *d_parity, uint16_t *d_align, void *stream);
 
+/* The fused form of kfec_frame_shards_batch + kfec_decode_batch: the missing data shards of G cached groups
+ * straight from the packet arena, without writing the framed shards (the decoder assembles the columns of the
+ * K shares it selected on the fly).  Inputs as kfec_frame_shards_batch; d_out / d_out_idx / d_status /
+ * d_workspace as kfec_decode_batch (workspace of kfec_decode_workspace_size(ctx, G) bytes); d_align as
+ * kfec_frame_shards_batch.  Every output is byte-identical to the two-step path. */
+int kfec_decode_framed_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size_t src_bytes,
+                             const uint64_t *d_off, const uint16_t *d_len, const uint64_t *d_present, size_t B,
+                             size_t pitch, void *d_out, uint8_t *d_out_idx, uint8_t *d_status, uint16_t *d_align,
+                             void *d_workspace, void *stream);
+
 /* extract_from_container (data_operations.cpp:697-704) on kfec_decode_batch's output.  For every used
  * recovered slot t of group g (d_out_idx[g][t] != 0xFF), d_rec_len[g*R+t] = the slot's BE16 length;
  * 0xFFFF when the slot is unused or the length does not fit in B - 2 (an inconsistent group: the reference

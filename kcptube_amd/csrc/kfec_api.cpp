@@ -341,6 +341,40 @@ int kfec_frame_shards_batch(const kfec_ctx *ctx, size_t G, const void *d_src, si
                : KFEC_OK;
 }
 
+int kfec_decode_framed_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size_t src_bytes,
+                             const uint64_t *d_off, const uint16_t *d_len, const uint64_t *d_present, size_t B,
+                             size_t pitch, void *d_out, uint8_t *d_out_idx, uint8_t *d_status, uint16_t *d_align,
+                             void *d_workspace, void *stream)
+{
+    if (!ctx || pitch < B || pitch % 4 || B > 0xFFFF) return KFEC_EINVAL;
+    if (G && (!d_src || !al4(d_src) || !d_off || !d_len || !d_present || !d_status || !d_workspace || !d_align))
+        return KFEC_EINVAL;
+    if (G && ctx->N > ctx->K && (!d_out || !al4(d_out) || !d_out_idx)) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    const hipStream_t s = as_stream(stream);
+    const int rc = kfec::launch_framed_decode(ctx->di, ctx->d_enc, (int)ctx->K, (int)ctx->N, G, d_src, src_bytes, d_off,
+                                              d_len, d_present, B, pitch, d_out, d_out_idx, d_status, d_align,
+                                              d_workspace, s);
+    if (rc < 0) return KFEC_EHIP;
+    if (rc == 0) return KFEC_OK;
+    // shapes the fused kernel does not take (R = 0, K x row tile too large for its LDS staging, huge batches):
+    // frame into scratch shard arrays, then decode
+    const size_t R = ctx->N - ctx->K;
+    void *data = nullptr, *par = nullptr;
+    if (hipMallocAsync(&data, std::max<size_t>(G * ctx->K * pitch, 4), s) != hipSuccess) return KFEC_ENOMEM;
+    if (hipMallocAsync(&par, std::max<size_t>(G * R * pitch, 4), s) != hipSuccess) {
+        (void)hipFreeAsync(data, s);
+        return KFEC_ENOMEM;
+    }
+    int r = kfec::launch_frame((int)ctx->K, (int)ctx->N, true, G, d_src, src_bytes, d_off, d_len, d_present, B, pitch,
+                               data, par, d_align, s);
+    if (!r) r = kfec::launch_decode(ctx->di, ctx->d_enc, (int)ctx->K, (int)ctx->N, G, B, pitch, data, par, d_present,
+                                    d_out, d_out_idx, d_status, d_workspace, s);
+    (void)hipFreeAsync(data, s);
+    (void)hipFreeAsync(par, s);
+    return r ? KFEC_EHIP : KFEC_OK;
+}
+
 int kfec_unframe_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, const void *d_out,
                        const uint8_t *d_out_idx, uint16_t *d_rec_len, void *d_dst, size_t dst_pitch, void *stream)
 {

@@ -453,6 +453,140 @@ __global__ void __launch_bounds__(256) framed_encode_kernel(FramedArgs a)
     }
 }
 
+// ---- fused receive compact_into_container + decode ---------------------------------------------------------
+// The recovered data shards of G cached groups straight from the packet arena: decode_prep_* has chosen each
+// group's K shares and written the coefficient rows of its missing data shards (decode records, as for
+// kfec_decode_batch); lane (group, 32-byte column) assembles column `col` of each chosen share on the fly --
+// a data shard framed as [BE16 len][payload][zeros], a parity shard raw and zero-padded -- and runs the perm
+// MAC.  Saves frame_shards' write of every present shard and the decoder's re-read of it.  The workgroup stages
+// its groups' (offset, length, kind) of the chosen shares and their perm tables in LDS.
+struct FramedDecArgs {
+    const uint32_t *src;
+    uint64_t src_dw;
+    const uint64_t *off;    // [G][N]
+    const uint16_t *len;    // [G][N]
+    const uint16_t *align;  // 0: a present shard does not fit in B (the group's shards read as zeros)
+    const uint8_t *rec;     // decode records (kfec_internal.hpp record_stride)
+    uint8_t *out;           // [G][R][pitch]
+    uint64_t pitch;
+    uint32_t total, cols, K, N, R, B, gmax, rec_stride;
+};
+
+constexpr uint32_t kDecData = 0x80000000u;  // s_len flag: a data shard (framed on the fly)
+constexpr uint32_t kDecZero = 0xFFFFFFFFu;  // s_len: reads as zeros
+
+template <int MT>
+__global__ void __launch_bounds__(256) framed_decode_kernel(FramedDecArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_raw[];
+    const uint32_t K = a.K, cols = a.cols, K4 = (K + 3) & ~3u;
+    const uint32_t base = blockIdx.x * 256u, item = base + threadIdx.x;
+    const uint32_t gfirst = base / cols, glast = min(base + 255u, a.total - 1) / cols, ng = glast - gfirst + 1;
+    uint32_t *s_tab = reinterpret_cast<uint32_t *>(s_raw);                              // [ng][K][MT][5]
+    uint64_t *s_off = reinterpret_cast<uint64_t *>(s_raw + (size_t)a.gmax * K * MT * 20);  // [ng][K]
+    uint32_t *s_len = reinterpret_cast<uint32_t *>(s_off + (size_t)a.gmax * K);           // [ng][K]
+    const uint32_t row0 = blockIdx.y * MT;
+    for (uint32_t e = threadIdx.x; e < ng * K; e += 256) {
+        const uint32_t gs = e / K, j = e - gs * K, g = gfirst + gs;
+        const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
+        const uint32_t st = rec[0], m = rec[1];
+        const bool work = st == 0 && m > row0;
+        uint32_t n = kDecZero;
+        uint64_t o = 0;
+        if (work && a.align[g] != 0) {
+            const uint32_t src = rec[4 + j];
+            const uint64_t idx = (uint64_t)g * a.N + src;
+            o = a.off[idx];
+            n = (uint32_t)a.len[idx] | (src < K ? kDecData : 0u);
+        }
+        s_off[e] = o;
+        s_len[e] = n;
+#pragma unroll
+        for (int r = 0; r < MT; ++r) {
+            const uint32_t u = row0 + r;
+            const uint32_t c = (work && u < m) ? rec[4 + K4 + u * K4 + j] : 0u;
+            uint32_t t[5];
+            gf_perm_tables(c, t);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) s_tab[((size_t)e * MT + r) * 5 + i] = t[i];
+        }
+    }
+    __syncthreads();
+    if (item >= a.total) return;
+    const uint32_t g = item / cols, col = item - g * cols, gs = g - gfirst;
+    uint32_t rows = 0;
+    {
+        const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
+        const uint32_t st = rec[0], m = rec[1];
+        rows = (st == 0 && m > row0) ? min((uint32_t)MT, m - row0) : 0u;
+    }
+    if (rows == 0) return;
+    uint32_t acc[MT][8];
+#pragma unroll
+    for (int r = 0; r < MT; ++r)
+#pragma unroll
+        for (int w = 0; w < 8; ++w) acc[r][w] = 0;
+    auto load = [&](uint32_t j, uint32_t (&x)[8]) {
+        const uint32_t n = s_len[gs * K + j];
+        const uint64_t o = s_off[gs * K + j];
+        if (n == kDecZero) {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) x[w] = 0;
+        } else if (n & kDecData) {
+            framed_gran(a.src, a.src_dw, o, n & 0xFFFFu, col, x);
+        } else {
+            uint32_t lo[4], hi[4];
+            payload_quad(a.src, a.src_dw, o, n, (int64_t)(32 * col), lo);
+            payload_quad(a.src, a.src_dw, o, n, (int64_t)(32 * col) + 16, hi);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                x[i] = lo[i];
+                x[4 + i] = hi[i];
+            }
+        }
+    };
+    uint32_t x0[8], x1[8];
+    load(0, x0);
+    if (K > 1) load(1, x1);
+    auto step = [&](uint32_t jj, uint32_t (&x)[8]) {
+        uint32_t cur[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) cur[w] = x[w];
+        if (jj + 2 < K) load(jj + 2, x);
+        const uint32_t *tp = s_tab + ((size_t)(gs * K + jj) * MT) * 5;
+        uint32_t t[5 * MT];
+#pragma unroll
+        for (int i = 0; i < 5 * MT; ++i) t[i] = tp[i];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const uint32_t xv = cur[w];
+            const uint32_t s0 = xv & 0x07070707u, s1 = (xv >> 3) & 0x07070707u, s2 = (xv >> 6) & 0x03030303u;
+#pragma unroll
+            for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+        }
+    };
+    for (uint32_t j = 0; j < K; j += 2) {
+        step(j, x0);
+        if (j + 1 < K) step(j + 1, x1);
+    }
+    const uint32_t nd = (col + 1) * 32 > a.B ? (a.B - col * 32 + 3) / 4 : 8u;  // dwords of this column below B
+#pragma unroll
+    for (int r = 0; r < MT; ++r) {
+        if ((uint32_t)r >= rows) continue;
+        uint32_t *o = reinterpret_cast<uint32_t *>(a.out + ((uint64_t)g * a.R + row0 + r) * a.pitch) + col * 8;
+        if (nd == 8) {
+            typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(u32x4_t{acc[r][0], acc[r][1], acc[r][2], acc[r][3]}, reinterpret_cast<u32x4_t *>(o));
+            __builtin_nontemporal_store(u32x4_t{acc[r][4], acc[r][5], acc[r][6], acc[r][7]},
+                                        reinterpret_cast<u32x4_t *>(o + 4));
+        } else {
+#pragma unroll
+            for (int w = 0; w < 8; ++w)
+                if ((uint32_t)w < nd) o[w] = acc[r][w];
+        }
+    }
+}
+
 uint32_t grid_for(uint64_t total)
 {
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((total + kFrameBlock - 1) / kFrameBlock, kMaxGrid));
@@ -505,6 +639,50 @@ int launch_framed_encode(const uint8_t *d_enc, int K, int N, size_t G, const voi
     case 3: hipLaunchKernelGGL(framed_encode_kernel<3>, grid, dim3(256), lds, s, a); break;
     case 4: hipLaunchKernelGGL(framed_encode_kernel<4>, grid, dim3(256), lds, s, a); break;
     default: hipLaunchKernelGGL(framed_encode_kernel<8>, grid, dim3(256), lds, s, a); break;
+    }
+    return launched();
+}
+
+int launch_framed_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, const void *src,
+                         size_t src_bytes, const uint64_t *off, const uint16_t *len, const uint64_t *present, size_t B,
+                         size_t pitch, void *out, uint8_t *out_idx, uint8_t *status, uint16_t *align,
+                         void *workspace, hipStream_t s)
+{
+    const int R = N - K;
+    if (G == 0) return 0;
+    const uint32_t cols = (uint32_t)((B + 31) / 32);
+    const uint32_t gmax = (uint32_t)std::min<size_t>(G, 255 / std::max<uint32_t>(cols, 1) + 2);
+    const int mt = R <= 4 ? std::max(R, 1) : 8;
+    const size_t lds = (size_t)gmax * K * ((size_t)mt * 20 + 12);
+    if (R == 0 || B == 0 || lds > 64 * 1024 || (uint64_t)G * cols > 0x7FFFFFFFull || pitch % 4 || B > 0xFFFF) return 1;
+    hipLaunchKernelGGL(align_kernel, dim3(grid_for(G)), dim3(kFrameBlock), 0, s, (uint64_t)G, (uint32_t)N, (uint32_t)K,
+                       len, present, (uint32_t)B, align);
+    if (launched()) return -3;
+    if (launch_decode_prep(di, d_enc, K, N, G, present, out_idx, status, workspace, s)) return -3;
+    FramedDecArgs a{};
+    a.src = static_cast<const uint32_t *>(src);
+    a.src_dw = (src_bytes + 3) / 4;
+    a.off = off;
+    a.len = len;
+    a.align = align;
+    a.rec = static_cast<const uint8_t *>(workspace);
+    a.out = static_cast<uint8_t *>(out);
+    a.pitch = pitch;
+    a.total = (uint32_t)(G * cols);
+    a.cols = cols;
+    a.K = K;
+    a.N = N;
+    a.R = R;
+    a.B = (uint32_t)B;
+    a.gmax = gmax;
+    a.rec_stride = (uint32_t)record_stride(K, R);
+    const dim3 grid((a.total + 255) / 256, (R + mt - 1) / mt);
+    switch (mt) {
+    case 1: hipLaunchKernelGGL(framed_decode_kernel<1>, grid, dim3(256), lds, s, a); break;
+    case 2: hipLaunchKernelGGL(framed_decode_kernel<2>, grid, dim3(256), lds, s, a); break;
+    case 3: hipLaunchKernelGGL(framed_decode_kernel<3>, grid, dim3(256), lds, s, a); break;
+    case 4: hipLaunchKernelGGL(framed_decode_kernel<4>, grid, dim3(256), lds, s, a); break;
+    default: hipLaunchKernelGGL(framed_decode_kernel<8>, grid, dim3(256), lds, s, a); break;
     }
     return launched();
 }

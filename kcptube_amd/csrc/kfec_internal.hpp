@@ -39,6 +39,8 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
 int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, size_t B, size_t pitch,
                   const void *d_data, const void *d_parity, const uint64_t *d_present, void *d_out,
                   uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s);
+int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, const uint64_t *d_present,
+                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s);
 int launch_synth(uint64_t seed, int N, size_t g0, size_t G, size_t s0, size_t ns, size_t B, size_t pitch,
                  void *d_out, hipStream_t s);
 int launch_erasure_masks(uint64_t seed, int N, size_t g0, size_t G, size_t pool, size_t count_max,
@@ -52,6 +54,11 @@ uint32_t engine_error_word();
 int launch_frame(int K, int N, bool recv, size_t G, const void *src, size_t src_bytes, const uint64_t *off,
                  const uint16_t *len, const uint64_t *present, size_t B, size_t pitch, void *data, void *parity,
                  uint16_t *align, hipStream_t s);
+// frame_shards + decode fused: 1 when the shape is not taken (the caller falls back to the two-step path)
+int launch_framed_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, const void *src,
+                         size_t src_bytes, const uint64_t *off, const uint16_t *len, const uint64_t *present, size_t B,
+                         size_t pitch, void *out, uint8_t *out_idx, uint8_t *status, uint16_t *align,
+                         void *workspace, hipStream_t s);
 int launch_unframe(int K, int N, size_t G, size_t B, size_t pitch, const void *out, const uint8_t *out_idx,
                    uint16_t *rec_len, void *dst, size_t dst_pitch, hipStream_t s);
 int launch_pack(int K, int N, size_t G, unsigned which, const void *src, size_t src_bytes, const uint64_t *off,

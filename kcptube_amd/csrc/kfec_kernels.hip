@@ -2113,9 +2113,10 @@ __global__ void __launch_bounds__(kBlock) compact_kernel(uint64_t G, uint32_t R,
     if (active) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)g;
 }
 
-int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, size_t B, size_t pitch,
-                  const void *d_data, const void *d_parity, const uint64_t *d_present, void *d_out,
-                  uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s)
+// decode_prep_*: share selection, the m x m solve and the coefficient rows of every group into the decode
+// records of d_workspace (+ d_out_idx, d_status).  The MAC kernels (here and kfec_frame.hip) consume them.
+int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, const uint64_t *d_present,
+                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s)
 {
     const int R = N - K;
     if (G == 0) return 0;
@@ -2151,7 +2152,18 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>(G, (size_t)std::max(di.cus, 1) * occ));
         hipLaunchKernelGGL(decode_prep_lagrange, dim3(blocks), dim3(kPrepThreads), 0, s, p);
     }
-    if (hipGetLastError() != hipSuccess) return -3;
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, size_t B, size_t pitch,
+                  const void *d_data, const void *d_parity, const uint64_t *d_present, void *d_out,
+                  uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s)
+{
+    const int R = N - K;
+    if (G == 0) return 0;
+    uint8_t *rec = static_cast<uint8_t *>(d_workspace);
+    const size_t rs = record_stride(K, R);
+    if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s)) return -3;
     if (R == 0 || B == 0) return 0;
     if (use_tile_path(G, B)) {
         LdsArgs a{};

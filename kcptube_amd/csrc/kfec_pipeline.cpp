@@ -324,7 +324,7 @@ struct kfec_rxq {
     Pinned h_arena, h_off, h_len, h_present, h_idx, h_rec_len, h_dst;
     std::vector<uint64_t> tags;
     std::vector<uint32_t> sns;
-    Device d_arena, d_off, d_len, d_present, d_data, d_par, d_align, d_out, d_idx, d_st, d_ws, d_rec_len, d_dst;
+    Device d_arena, d_off, d_len, d_present, d_align, d_out, d_idx, d_st, d_ws, d_rec_len, d_dst;
     Upload up;
 };
 
@@ -403,8 +403,7 @@ int kfec_rxq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_shard, kf
     const size_t pitch = round4(max_shard);
     if (q->h_arena.ensure(GN * q->slot) || q->h_off.ensure(GN * 8) || q->h_len.ensure(GN * 2) ||
         q->h_present.ensure(G * 32) || q->d_arena.ensure(GN * q->slot) || q->d_off.ensure(GN * 8) ||
-        q->d_len.ensure(GN * 2) || q->d_present.ensure(G * 32) || q->d_data.ensure(G * q->K * pitch) ||
-        q->d_par.ensure(G * R1 * pitch) || q->d_align.ensure(G * 2) || q->d_out.ensure(G * R1 * pitch) ||
+        q->d_len.ensure(GN * 2) || q->d_present.ensure(G * 32) || q->d_align.ensure(G * 2) || q->d_out.ensure(G * R1 * pitch) ||
         q->d_idx.ensure(G * R1) || q->d_st.ensure(G) || q->d_ws.ensure(kfec_decode_workspace_size(ctx, G)) ||
         q->d_rec_len.ensure(G * R1 * 2) || q->d_dst.ensure(G * R1 * pitch) || q->h_idx.ensure(G * R1) ||
         q->h_rec_len.ensure(G * R1 * 2) || q->h_dst.ensure(G * R1 * pitch)) {
@@ -533,12 +532,11 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
         hipMemcpyAsync(q->d_len.p, q->h_len.p, nn * 2, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(q->d_present.p, q->h_present.p, n * 32, hipMemcpyHostToDevice, s) != hipSuccess)
         return KFEC_EHIP;
-    int rc = kfec_frame_shards_batch(q->ctx, n, q->d_arena.p, std::max<size_t>(q->used, 4), q->d_off.as<uint64_t>(),
-                                     q->d_len.as<uint16_t>(), q->d_present.as<uint64_t>(), B, pitch, q->d_data.p,
-                                     q->d_par.p, q->d_align.as<uint16_t>(), stream);
-    if (rc) return rc;
-    rc = kfec_decode_batch(q->ctx, n, B, pitch, q->d_data.p, q->d_par.p, q->d_present.as<uint64_t>(), q->d_out.p,
-                           q->d_idx.as<uint8_t>(), q->d_st.as<uint8_t>(), q->d_ws.p, stream);
+    // recv compact_into_container + decode fused: the chosen shares are framed on the fly from the arena
+    int rc = kfec_decode_framed_batch(q->ctx, n, q->d_arena.p, std::max<size_t>(q->used, 4), q->d_off.as<uint64_t>(),
+                                      q->d_len.as<uint16_t>(), q->d_present.as<uint64_t>(), B, pitch, q->d_out.p,
+                                      q->d_idx.as<uint8_t>(), q->d_st.as<uint8_t>(), q->d_align.as<uint16_t>(),
+                                      q->d_ws.p, stream);
     if (rc) return rc;
     if (R) {
         rc = kfec_unframe_batch(q->ctx, n, B, pitch, q->d_out.p, q->d_idx.as<uint8_t>(), q->d_rec_len.as<uint16_t>(),

@@ -87,6 +87,17 @@ class FecFrame:
                                                  _dptr(length), _dptr(present), B, pitch, _dptr(data), _dptr(parity),
                                                  _dptr(align), _stream_handle(stream)), "kfec_frame_shards_batch")
 
+    def decode_framed(self, src, off, length, present, out, out_idx, status, align, workspace, B: int,
+                      stream=None) -> None:
+        """frame_shards + decode_batch fused: the missing data shards out [G][R][pitch] (+ out_idx, status,
+        align) straight from the shard table, without materialising the framed shards."""
+        G, r, pitch = out.shape
+        assert off.numel() == G * self.N and present.shape == (G, 4) and align.numel() == G
+        _check(self._lib.kfec_decode_framed_batch(self.code._ctx, G, _dptr(src), src.numel(), _dptr(off),
+                                                  _dptr(length), _dptr(present), B, pitch, _dptr(out),
+                                                  _dptr(out_idx), _dptr(status), _dptr(align), _dptr(workspace),
+                                                  _stream_handle(stream)), "kfec_decode_framed_batch")
+
     def unframe(self, out, out_idx, rec_len, B: int, dst=None, stream=None) -> None:
         """out [G][R][pitch] from decode_batch; rec_len int16 [G][R] (written; 0xFFFF = no datagram);
         dst [G][R][dst_pitch] (optional) receives the datagram bytes."""

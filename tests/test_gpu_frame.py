@@ -481,3 +481,93 @@ def test_encode_framed_matches_two_step_and_oracle(dev, oracle, K, N, B, pitch):
         for r in range(R):
             assert gp[g, r, :a].tobytes() == exp[r], (g, r)
             assert not gp[g, r, a:Bp].any()
+
+
+def _ws(c, G, dev):
+    return c.decode_workspace(G, device=dev)
+
+
+@pytest.mark.parametrize("K,N,B,pitch", [(20, 23, 1442, 1444), (10, 13, 1402, 1404), (3, 5, 7, 8), (1, 2, 2, 4),
+                                         (4, 6, 40, 64), (200, 255, 1442, 1444)])
+def test_decode_framed_matches_two_step(dev, K, N, B, pitch):
+    """kfec_decode_framed_batch == kfec_frame_shards_batch + kfec_decode_batch, byte for byte, on arbitrary
+    shard bytes: random present sets (some below K), ragged lengths, a group whose data shard does not fit."""
+    c, fr = _coder(K, N)
+    R = N - K
+    rng = random.Random(K * 31 + B)
+    G = 37 if K < 100 else 4
+    chunks, present = [], np.zeros((G, 4), np.uint64)
+    for g in range(G):
+        pal = rng.randint(0, B)
+        nh = N if g == 0 else rng.choice([K, K, N - 1, rng.randint(max(0, K - 1), N)])
+        have = rng.sample(range(N), nh)
+        for s in range(N):
+            n = rng.choice([0, B - 2, rng.randint(0, B - 2)]) if s < K else pal
+            if g == 1 and s == 0 and B > 2:
+                n = B - 1  # cannot be framed in B: the group reads as zeros on both paths
+            chunks.append(rng.randbytes(n))
+        for s in have:
+            present[g, s >> 6] |= np.uint64(1 << (s & 63))
+    src, off, lens = _arena(chunks, dev)
+    d_len = _i16(lens, dev)
+    pres = torch.tensor(present.view(np.int64), device=dev)
+    out = torch.full((G, R, pitch), SENT, dtype=torch.uint8, device=dev)
+    idx = torch.full((G, R), 0x5A, dtype=torch.uint8, device=dev)
+    st = torch.full((G,), 0x5A, dtype=torch.uint8, device=dev)
+    al = torch.zeros(G, dtype=torch.int16, device=dev)
+    fr.decode_framed(src, off, d_len, pres, out, idx, st, al, _ws(c, G, dev), B)
+    data = torch.full((G, K, pitch), SENT, dtype=torch.uint8, device=dev)
+    par = torch.full((G, R, pitch), SENT, dtype=torch.uint8, device=dev)
+    al2 = torch.zeros(G, dtype=torch.int16, device=dev)
+    fr.frame_shards(src, off, d_len, pres, data, par, al2, B)
+    out2 = torch.full((G, R, pitch), SENT, dtype=torch.uint8, device=dev)
+    idx2 = torch.full((G, R), 0x5A, dtype=torch.uint8, device=dev)
+    st2 = torch.full((G,), 0x5A, dtype=torch.uint8, device=dev)
+    c.decode_batch(data, par, pres, out2, idx2, st2, _ws(c, G, dev), B=B)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u16(al), _u16(al2))
+    assert np.array_equal(st.cpu().numpy(), st2.cpu().numpy())
+    assert np.array_equal(idx.cpu().numpy(), idx2.cpu().numpy())
+    assert np.array_equal(out.cpu().numpy(), out2.cpu().numpy())
+    assert (st.cpu().numpy() == 0).sum() >= G // 3
+
+
+@pytest.mark.parametrize("K,N,B", [(20, 23, 1442), (10, 13, 1402), (5, 8, 300)])
+def test_decode_framed_recovers_datagrams(dev, oracle, K, N, B):
+    """Real groups (oracle compact_into_container + fec_code::encode), up to N-K packets lost per group:
+    decode_framed + unframe hand back exactly the lost datagrams."""
+    c, fr = _coder(K, N)
+    R = N - K
+    pitch = (B + 3) // 4 * 4
+    rng = random.Random(K + N)
+    G = 29
+    chunks, present, lost = [], np.zeros((G, 4), np.uint64), []
+    for g in range(G):
+        dgs = [rng.randbytes(rng.choice([0, 1, B - 2, rng.randint(0, B - 2)])) for _ in range(K)]
+        cont, a, _ = fo.compact_send(dgs)
+        par = oracle.encode(K, N, cont, a)
+        chunks += dgs + list(par)
+        gone = set(rng.sample(range(N), rng.randint(0, R)))
+        for s in range(N):
+            if s not in gone:
+                present[g, s >> 6] |= np.uint64(1 << (s & 63))
+        lost.append({s: dgs[s] for s in gone if s < K})
+    src, off, lens = _arena(chunks, dev)
+    pres = torch.tensor(present.view(np.int64), device=dev)
+    out = torch.zeros((G, R, pitch), dtype=torch.uint8, device=dev)
+    idx = torch.zeros((G, R), dtype=torch.uint8, device=dev)
+    st = torch.zeros((G,), dtype=torch.uint8, device=dev)
+    al = torch.zeros(G, dtype=torch.int16, device=dev)
+    fr.decode_framed(src, off, _i16(lens, dev), pres, out, idx, st, al, _ws(c, G, dev), B)
+    rec_len = torch.zeros((G, R), dtype=torch.int16, device=dev)
+    dst = torch.zeros((G, R, pitch), dtype=torch.uint8, device=dev)
+    fr.unframe(out, idx, rec_len, B, dst=dst)
+    torch.cuda.synchronize()
+    gi, gl, gd = idx.cpu().numpy(), _u16(rec_len), dst.cpu().numpy()
+    assert (st.cpu().numpy() == 0).all()
+    n = 0
+    for g in range(G):
+        got = {int(gi[g, t]): gd[g, t, :gl[g, t]].tobytes() for t in range(R) if gi[g, t] != 0xFF}
+        assert got == lost[g], g
+        n += len(got)
+    assert n > G // 3

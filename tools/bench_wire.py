@@ -6,7 +6,8 @@
 fec=20:3, kcp_mtu=1440.  Send step: frame_data -> encode_batch -> pack (data + redundant packets), and the
 fused form encode_framed (frame + encode in one kernel, checked equal) -> pack.
 Receive step (every group lost 3 data packets, worst case): unpack -> scatter -> frame_shards -> decode_batch
--> unframe.  Datagrams are 1440 B (bulk traffic) or, with --ragged, uniform 0..1440 B.  Prints one JSON line:
+-> unframe, and the fused form unpack -> scatter -> decode_framed (frame_shards + decode in one kernel, checked
+equal) -> unframe.  Datagrams are 1440 B (bulk traffic) or, with --ragged, uniform 0..1440 B.  Prints one JSON line:
 payload GiB/s of each direction and per-kernel times / HBM GB/s (algorithmic bytes per launch / HIP-event
 time on the launch stream).
 """
@@ -80,9 +81,12 @@ def main():
     flat = pkt.view(-1)
     parity2 = torch.empty_like(parity)
     align2 = torch.empty_like(align)
+    out2, idx2, st2, ralign2 = torch.empty_like(out), torch.empty_like(idx), torch.empty_like(st), torch.empty_like(ralign)
+    ws2 = c.decode_workspace(G)
 
     s = torch.cuda.current_stream()
-    names = ["frame_data", "encode", "pack", "unpack", "scatter", "frame_shards", "decode", "unframe", "encode_framed"]
+    names = ["frame_data", "encode", "pack", "unpack", "scatter", "frame_shards", "decode", "unframe", "encode_framed",
+             "decode_framed"]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
     times = {n: [] for n in names}
 
@@ -117,6 +121,9 @@ def main():
         fr.encode_framed(arena, off, d_len, parity2, align2, B)  # fused frame_data + encode (same parity)
         if timed:
             ev[9].record(s)
+        fr.decode_framed(flat, toff, tlen, present, out2, idx2, st2, ralign2, ws2, B)  # fused frame_shards + decode
+        if timed:
+            ev[10].record(s)
 
     # received packet lengths (what recvmmsg reports) -- identical every step, so taken once up front
     fr.frame_data(arena, off, d_len, data, align, B)
@@ -164,17 +171,24 @@ def main():
         "decode": G * K * B + G * R * B,
         "unframe": lost_bytes * 2,
         "encode_framed": payload + G * R * B,
+        "decode_framed": (kept_pkt_bytes - P * 9 - G * R * 4) + G * R * B,
     }
     send_ms = med["frame_data"] + med["encode"] + med["pack"]
     send_fused_ms = med["encode_framed"] + med["pack"]
     recv_ms = sum(med[n] for n in names[3:8])
+    recv_fused_ms = med["unpack"] + med["scatter"] + med["decode_framed"] + med["unframe"]
     ok = ok and torch.equal(parity2, parity) and torch.equal(align2, align)
+    ok = ok and torch.equal(idx2, idx) and torch.equal(st2, st) and torch.equal(ralign2, ralign)
+    B4 = (B + 3) // 4 * 4
+    ok = ok and torch.equal(out2[:, :, :B4], out[:, :, :B4])
     res = {
         "metric": "FEC wire path payload GiB/s (device-resident, packet-in/packet-out), fec=20:3 kcp_mtu=1440",
         "groups": G, "ragged": args.ragged, "steps": args.steps,
         "send_GiBps": round(payload / (send_ms * 1e-3) / 2**30, 2),
         "recv_GiBps": round(payload / (recv_ms * 1e-3) / 2**30, 2),
         "send_fused_GiBps": round(payload / (send_fused_ms * 1e-3) / 2**30, 2),
+        "recv_fused_GiBps": round(payload / (recv_fused_ms * 1e-3) / 2**30, 2),
+        "recv_fused_ms": round(recv_fused_ms, 4),
         "send_ms": round(send_ms, 4), "send_fused_ms": round(send_fused_ms, 4), "recv_ms": round(recv_ms, 4),
         "kernels": {n: {"ms": round(med[n], 4), "alg_GBps": round(alg[n] / (med[n] * 1e-3) / 1e9, 1)} for n in names},
         "verified_bit_exact": ok,
