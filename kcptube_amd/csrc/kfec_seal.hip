@@ -96,14 +96,6 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t (*t)[256], uint32_t
     return t[0][r & 0xFFu] ^ t[1][(r >> 8) & 0xFFu] ^ t[2][(r >> 16) & 0xFFu] ^ t[3][r >> 24];
 }
 
-// bytes [a, b) of a dword (0 <= a, b <= 4)
-__device__ __forceinline__ uint32_t range_mask(int a, int b)
-{
-    const uint32_t hi = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : (1u << (8 * b)) - 1u);
-    const uint32_t lo = a >= 4 ? 0xFFFFFFFFu : (a <= 0 ? 0u : (1u << (8 * a)) - 1u);
-    return hi & ~lo;
-}
-
 // 16 bytes [q0, q0 + 16) of base[start, start + len), zero outside (dword-aligned base, dwords < lim32):
 // one 16-byte load at the covering dword (dword alignment suffices on gfx950) and one more dword
 __device__ __forceinline__ void chunk16(const uint32_t *base32, uint64_t lim32, uint64_t start, uint32_t len,
@@ -128,10 +120,12 @@ __device__ __forceinline__ void chunk16(const uint32_t *base32, uint64_t lim32, 
         }
     }
     const int lo = max(0, -q0), hi = min(16, (int32_t)len - q0);  // valid bytes [lo, hi) of the chunk
+    const uint32_t M = ((1u << hi) - 1u) & ~((1u << lo) - 1u);    // one bit per valid byte (branch-free masks)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const uint32_t v = sh ? __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) : d[i];
-        o[i] = v & range_mask(lo - 4 * i, hi - 4 * i);
+        const uint32_t nib = (M >> (4 * i)) & 0xFu;
+        const uint32_t bm = ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;  // bit b of nib -> byte b
+        o[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) & bm;
     }
 }
 
