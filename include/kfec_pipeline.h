@@ -60,11 +60,11 @@ void kfec_tx_destroy(kfec_tx *tx);
 
 /* fec_maker(input_data, data_size): writes the data packet to pkt[9 + len] (*pkt_len) and, when this
  * datagram completes a group, queues the group (its redundant packets come from kfec_txq_flush).
- * The datagram is stored once, in the queue's staging arena (max_groups x K datagram slots, shared by the
- * complete groups and every sender's partial group; a flush keeps the partial groups).  KFEC_EINVAL for a
- * datagram longer than max_datagram; KFEC_ENOMEM, with nothing sent, when the datagram would complete a
- * group and the queue is full, or the arena is full (flush first; size max_groups above the number of
- * senders so that their partial groups alone never fill it). */
+ * The datagram is stored once, in the queue's staging arena (initially max_groups x K datagram slots, shared
+ * by the complete groups and every sender's partial group; a flush keeps the partial groups, and the arena
+ * doubles when the partial groups alone fill it).  KFEC_EINVAL for a datagram longer than max_datagram;
+ * KFEC_ENOMEM, with nothing sent, when the datagram would complete a group and the queue is full, or the
+ * arena is full while groups are queued (flush, then retry). */
 int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t timestamp, uint8_t *pkt,
                  size_t *pkt_len);
 
@@ -92,10 +92,12 @@ size_t kfec_rx_cached(const kfec_rx *rx);
  * scan (expiry relative to this packet's sn; every group holding >= K shares and not yet restored is queued
  * for decoding and marked restored).  For a data packet *datagram / *datagram_len point at its payload inside
  * pkt (what fec_unpack returns to its caller for KCP::Input); NULL / 0 otherwise.  Returns the number of
- * groups queued by this call, KFEC_EINVAL for a packet shorter than its header or a shard longer than
- * max_shard, KFEC_ENOMEM when the decode queue might overflow or the staging arena (max_groups x N shard
- * slots, which also holds the shards of groups still waiting for K shares) is full (flush first; the packet
- * is then not cached).  The payload is stored once, in that arena; a flush keeps the waiting groups' shards. */
+ * groups queued by this call (0 or 1: only the packet's own group can reach K shares), KFEC_EINVAL for a
+ * packet shorter than its header or a shard longer than max_shard, KFEC_ENOMEM when that group would be
+ * queued and the queue is full, or the staging arena is full while groups are queued (flush, then retry; the
+ * packet is then not cached).  The payload is stored once, in that arena (initially max_groups x N shard
+ * slots, also holding the shards of groups still waiting for K shares: a flush keeps them, and the arena
+ * doubles when they alone fill it). */
 int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **datagram, size_t *datagram_len);
 
 /* Recovered datagram callback: tag of the kfec_rx, group sn, data index, bytes (what KCP::Input gets). */

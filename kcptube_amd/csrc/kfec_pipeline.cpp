@@ -96,6 +96,27 @@ struct Upload {
     }
 };
 
+// Make room for `need` more bytes in a staging arena holding `used` bytes when nothing is queued (so a flush
+// cannot free anything): the partial / waiting groups of many connections can outgrow the initial
+// max_groups-sized arena.  Doubles the pinned and the device arena; the upload restarts from byte 0.
+int grow_arena(Pinned &h, Device &d, Upload &up, size_t used, size_t need, size_t &cap)
+{
+    size_t ncap = std::max<size_t>(cap, 4096);
+    while (used + need > ncap) ncap *= 2;
+    if (up.cs && hipStreamSynchronize(up.cs) != hipSuccess) return KFEC_EHIP;
+    Pinned nh;
+    Device nd;
+    if (nh.ensure(ncap) || nd.ensure(ncap)) return KFEC_ENOMEM;
+    if (used) std::memcpy(nh.p, h.p, used);
+    std::swap(h.p, nh.p);
+    std::swap(h.n, nh.n);
+    std::swap(d.p, nd.p);
+    std::swap(d.n, nd.n);
+    up.issued = 0;
+    cap = ncap;
+    return KFEC_OK;
+}
+
 inline void put_le32(uint8_t *p, uint32_t v)
 {
     p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
@@ -217,7 +238,11 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
     if (len > q->mtu) return KFEC_EINVAL;
     const bool completes = tx->conv != 0 && tx->cached + 1 == q->K;
     if (completes && q->n == q->G) return KFEC_ENOMEM;
-    if (tx->conv != 0 && q->used + round4(len) > q->cap) return KFEC_ENOMEM;
+    if (tx->conv != 0 && q->used + round4(len) > q->cap) {
+        if (q->n) return KFEC_ENOMEM;  // a flush frees the queued groups' bytes
+        const int rc = grow_arena(q->h_dg, q->d_dg, q->up, q->used, round4(len), q->cap);
+        if (rc) return rc;
+    }
     // create_fec_data_packet (connections.cpp:395-411), sub_sn = fec_snd_sub_sn++ (client.cpp:805-806)
     put_le32(pkt, timestamp);
     put_be32(pkt + 4, tx->sn);
@@ -472,12 +497,18 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
     const uint32_t fec_sn = get_be32(pkt + 4);
     // capacity: this push can queue at most every not-yet-restored cached group plus a new one
     auto found = rx->cache.find(fec_sn);
-    size_t could = found == rx->cache.end() ? 1 : 0;
-    for (const auto &kv : rx->cache)
-        if (!kv.second->restored) ++could;
-    if (q->n + could > q->G) return KFEC_ENOMEM;
-    const bool store = found == rx->cache.end() || !found->second->restored;
-    if (store && q->used + round4(plen) > q->cap) return KFEC_ENOMEM;
+    // capacity: only this packet's group can become decodable on this push (every other cached group either
+    // reached K shares on an earlier push, and was queued and restored then, or still lacks shares)
+    const bool fresh = found == rx->cache.end();
+    const bool store = fresh || !found->second->restored;
+    const uint32_t have = fresh ? 0u : found->second->count + (found->second->test(sub) ? 0u : 1u);
+    const bool completes = store && (fresh ? 1u : have) >= q->K;
+    if (completes && q->n >= q->G) return KFEC_ENOMEM;
+    if (store && q->used + round4(plen) > q->cap) {
+        if (q->n) return KFEC_ENOMEM;  // a flush frees the queued groups' bytes
+        const int rc = grow_arena(q->h_arena, q->d_arena, q->up, q->used, round4(plen), q->cap);
+        if (rc) return rc;
+    }
     // fec_rcv_cache[sn][sub_sn] = ... (client.cpp:869,887): a duplicate overwrites
     RxGroup *grp = found != rx->cache.end() ? found->second : (rx->cache[fec_sn] = rx->get());
     if (!grp->test(sub)) {

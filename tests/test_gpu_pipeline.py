@@ -154,3 +154,68 @@ def test_receiver_matches_oracle_through_lossy_channel(dev, oracle, K, N, mtu):
         assert rx[i].cached() == len(ref[i].cache)
         n_rec += ref[i].recovered
     assert n_rec > 20
+
+
+@pytest.mark.parametrize("K,N,mtu,max_groups", [(20, 23, 1440, 4), (6, 9, 300, 2)])
+def test_receiver_frequent_flushes_and_duplicates(dev, oracle, K, N, mtu, max_groups):
+    """Flushes at random points (groups still waiting for K shares keep their shards across each flush, moved
+    to the front of the staging arena), a tiny queue (KFEC_ENOMEM -> flush and retry), duplicated packets
+    (the later copy wins, as the reference's map assignment): same datagrams as the oracle."""
+    from kcptube_amd.fec import KfecError
+    from kcptube_amd.pipeline import FecReceiver, RxQueue
+    c = _coder(K, N)
+    rq = RxQueue(c, max_groups=max_groups, max_shard=mtu + 2)
+    rng = random.Random(K * 1000 + N)
+    conns = 3
+    streams = []
+    for i in range(conns):
+        tx = fo.FecTx(K, N, lambda d, t, a: oracle.encode(K, N, d, a, t), conv=900 + i)
+        pkts = []
+        for _ in range(K * 12):
+            pkts += tx.send(rng.randbytes(rng.randint(0, mtu)))
+        kept = []
+        for p in pkts:
+            r = rng.random()
+            if r < 0.10:
+                continue  # lost
+            kept.append(p)
+            if r > 0.95:
+                kept.append(p)  # duplicated on the wire
+        for j in range(0, len(kept) - 2, 5):
+            kept[j], kept[j + 2] = kept[j + 2], kept[j]
+        streams.append(kept)
+    rx = [FecReceiver(rq, tag=i) for i in range(conns)]
+    ref = [fo.FecRx(K, N, lambda s, a: oracle.decode(K, N, s, a)) for _ in range(conns)]
+    got = [[] for _ in range(conns)]
+    exp = [[] for _ in range(conns)]
+    pos = [0] * conns
+    n_full = 0
+    while any(pos[i] < len(streams[i]) for i in range(conns)):
+        i = rng.randrange(conns)
+        if pos[i] >= len(streams[i]):
+            continue
+        p = streams[i][pos[i]]
+        try:
+            own, _ = rx[i].push(p)
+        except KfecError:
+            n_full += 1
+            for tag, sn, idx, d in rq.flush():
+                got[tag].append(d)
+            own, _ = rx[i].push(p)
+        pos[i] += 1
+        if own is not None:
+            got[i].append(own)
+        exp[i] += ref[i].push(p)
+        if rng.random() < 0.1:
+            for tag, sn, idx, d in rq.flush():
+                got[tag].append(d)
+    for tag, sn, idx, d in rq.flush():
+        got[tag].append(d)
+    n_rec = 0
+    for i in range(conns):
+        assert sorted(got[i]) == sorted(exp[i]), i
+        assert rx[i].cached() == len(ref[i].cache)
+        n_rec += ref[i].recovered
+    assert n_rec > 5
+    if max_groups <= 2:
+        assert n_full > 0  # the KFEC_ENOMEM -> flush -> retry path ran
