@@ -57,24 +57,32 @@ def test_sender_packets_match_oracle(dev, oracle, K, N, mtu):
         assert p[8] == sub and int.from_bytes(p[4:8], "big") == sn
 
 
-def test_sender_flushes_between_partial_groups(dev, oracle):
+@pytest.mark.parametrize("max_groups,senders", [(8, 4), (1, 9)])
+def test_sender_flushes_between_partial_groups(dev, oracle, max_groups, senders):
     """Flushes at random points: the partial groups of every sender survive each flush (their datagrams are
-    moved to the front of the staging arena) and complete later with the right bytes."""
+    moved to the front of the staging arena) and complete later with the right bytes.  With 9 senders and a
+    one-group queue the partial groups alone outgrow the arena, which then grows."""
+    from kcptube_amd.fec import KfecError
     from kcptube_amd.pipeline import FecSender, TxQueue
     K, N, mtu = 5, 7, 200
     c = _coder(K, N)
-    q = TxQueue(c, max_groups=8, max_datagram=mtu)
+    q = TxQueue(c, max_groups=max_groups, max_datagram=mtu)
     rng = random.Random(99)
     conns = [(FecSender(q, conv=0x2000 + i, tag=i), fo.FecTx(K, N, lambda d, t, a: oracle.encode(K, N, d, a, t),
-                                                             conv=0x2000 + i)) for i in range(4)]
+                                                             conv=0x2000 + i)) for i in range(senders)]
     exp_red, got = [], []
     for step in range(400):
         tag = rng.randrange(len(conns))
         tx, ref = conns[tag]
         d = rng.randbytes(rng.choice([0, 3, mtu, rng.randint(0, mtu)]))
-        if q.pending() == 8 or rng.random() < 0.05:
+        if q.pending() == max_groups or rng.random() < 0.05:
             got += q.flush(timestamp=7)
-        assert tx.send(d, timestamp=7) == (ref_pkts := ref.send(d, timestamp=7))[0]
+        try:
+            pkt = tx.send(d, timestamp=7)
+        except KfecError:  # arena full while groups are queued: flush, then retry
+            got += q.flush(timestamp=7)
+            pkt = tx.send(d, timestamp=7)
+        assert pkt == (ref_pkts := ref.send(d, timestamp=7))[0]
         exp_red += [(tag, p) for p in ref_pkts[1:]]
     got += q.flush(timestamp=7)
     assert len(exp_red) > 100
