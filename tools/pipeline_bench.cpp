@@ -5,15 +5,22 @@
 // GPU at each flush).  Reports host-side per-packet cost, GPU flush time (including the pinned H2D / D2H
 // copies) and the datagram payload rate of each direction, on ONE host thread, and checks every recovered
 // datagram.
-// Build: g++ -O2 -std=c++17 -I include tools/pipeline_bench.cpp -o tools/pipeline_bench -L kcptube_amd -lkfec
-//        -Wl,-rpath,$PWD/kcptube_amd
-// Usage: tools/pipeline_bench [K N mtu groups_per_flush flushes loss]
+// Build: g++ -O2 -std=c++17 -D__HIP_PLATFORM_AMD__ -I include -I /opt/rocm/include tools/pipeline_bench.cpp
+//        -o tools/pipeline_bench -L kcptube_amd -lkfec -L /opt/rocm/lib -lamdhip64 -pthread
+//        -Wl,-rpath,'$ORIGIN/../kcptube_amd'
+// Usage: tools/pipeline_bench [K N mtu groups_per_flush flushes loss threads]
+// With threads > 1 every thread runs its own sender + receiver over its own queues and HIP stream (one
+// context shared); all_threads_tx_plus_rx_GiBps = the payload every thread sent and received / the slowest
+// thread's wall time (its data generation excluded).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <thread>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "kfec_pipeline.h"
 
@@ -51,24 +58,30 @@ static void on_dg(void *u, uint64_t tag, uint32_t sn, uint8_t idx, const uint8_t
     if (o.size() != len || std::memcmp(o.data(), d, len)) r->bad++;
 }
 
-int main(int argc, char **argv)
+struct Params {
+    size_t K, N, mtu, G, loss;
+    int flushes;
+};
+
+struct Result {
+    double t_tx_host = 0, t_tx_flush = 0, t_rx_host = 0, t_rx_flush = 0, wall = 0;
+    size_t recovered = 0, bad = 0;
+    int rc = 0;
+};
+
+// One host thread's sender + receiver over its own queues and HIP stream.
+static void run(kfec_ctx *ctx, const Params &pa, uint64_t seed, hipStream_t stream, Result &res)
 {
-    const size_t K = argc > 1 ? atoi(argv[1]) : 20, N = argc > 2 ? atoi(argv[2]) : 23;
-    const size_t mtu = argc > 3 ? atoi(argv[3]) : 1440, G = argc > 4 ? atoi(argv[4]) : 16384;
-    const int flushes = argc > 5 ? atoi(argv[5]) : 4;
-    const size_t loss = argc > 6 ? atoi(argv[6]) : 3;
-    const size_t R = N - K;
-    kfec_ctx *ctx = nullptr;
-    if (kfec_create(K, N, &ctx)) { printf("no GPU\n"); return 1; }
+    const size_t K = pa.K, N = pa.N, mtu = pa.mtu, G = pa.G, loss = pa.loss, R = N - K;
+    const int flushes = pa.flushes;
     kfec_txq *tq;
     kfec_rxq *rq;
-    kfec_txq_create(ctx, G, mtu, &tq);
-    kfec_rxq_create(ctx, G, mtu + 2, &rq);
+    if (kfec_txq_create(ctx, G, mtu, &tq) || kfec_rxq_create(ctx, G, mtu + 2, &rq)) { res.rc = 1; return; }
     kfec_tx *tx;
     kfec_rx *rx;
     kfec_tx_create(tq, 0x4B435054, 1, &tx);
     kfec_rx_create(rq, 1, &rx);
-    std::mt19937_64 rng(7);
+    std::mt19937_64 rng(seed);
     const size_t total_groups = G * flushes;
     std::vector<std::vector<uint8_t>> dg(total_groups * K);
     for (auto &d : dg) {
@@ -86,23 +99,23 @@ int main(int argc, char **argv)
     red.stride = mtu + 16;
     red.buf.resize(total_groups * R * red.stride);
     red.len.resize(total_groups * R);
-    double t_tx_host = 0, t_tx_flush = 0, t_rx_host = 0, t_rx_flush = 0;
+    const auto w0 = clk::now();
     for (int f = 0; f < flushes; ++f) {
         auto t0 = clk::now();
         for (size_t g = f * G; g < (f + 1) * G; ++g)
             for (size_t i = 0; i < K; ++i) {
                 size_t n = 0;
                 if (kfec_tx_send(tx, dg[g * K + i].data(), mtu, 1, data_pkts.data() + (g * K + i) * dstride, &n)) {
-                    printf("send failed\n");
-                    return 1;
+                    res.rc = 1;
+                    return;
                 }
                 data_len[g * K + i] = (uint16_t)n;
             }
         auto t1 = clk::now();
-        if (kfec_txq_flush(tq, 1, on_pkt, &red, nullptr)) { printf("tx flush failed\n"); return 1; }
+        if (kfec_txq_flush(tq, 1, on_pkt, &red, stream)) { res.rc = 1; return; }
         auto t2 = clk::now();
-        t_tx_host += std::chrono::duration<double>(t1 - t0).count();
-        t_tx_flush += std::chrono::duration<double>(t2 - t1).count();
+        res.t_tx_host += std::chrono::duration<double>(t1 - t0).count();
+        res.t_tx_flush += std::chrono::duration<double>(t2 - t1).count();
     }
     // receive: every group loses `loss` data packets (worst case for the decoder)
     Rec rec;
@@ -116,39 +129,83 @@ int main(int argc, char **argv)
                 const uint8_t *d;
                 size_t dn;
                 if (kfec_rx_push(rx, data_pkts.data() + (g * K + i) * dstride, data_len[g * K + i], &d, &dn) < 0) {
-                    printf("push failed\n");
-                    return 1;
+                    res.rc = 1;
+                    return;
                 }
                 own += dn;
             }
             for (size_t r = 0; r < R; ++r) {
                 if (kfec_rx_push(rx, red.pkt(g * R + r), red.len[g * R + r], nullptr, nullptr) < 0) {
-                    printf("push failed\n");
-                    return 1;
+                    res.rc = 1;
+                    return;
                 }
             }
         }
         auto t1 = clk::now();
-        if (kfec_rxq_flush(rq, on_dg, &rec, nullptr)) { printf("rx flush failed\n"); return 1; }
+        if (kfec_rxq_flush(rq, on_dg, &rec, stream)) { res.rc = 1; return; }
         auto t2 = clk::now();
-        t_rx_host += std::chrono::duration<double>(t1 - t0).count();
-        t_rx_flush += std::chrono::duration<double>(t2 - t1).count();
+        res.t_rx_host += std::chrono::duration<double>(t1 - t0).count();
+        res.t_rx_flush += std::chrono::duration<double>(t2 - t1).count();
     }
-    const double payload = (double)total_groups * K * mtu;
-    const double npk_tx = (double)total_groups * K, npk_rx = (double)total_groups * (K - loss + R);
-    printf("{\"metric\": \"batched FEC pipeline, host memory in and out (1 host thread)\", \"fec\": \"%zu:%zu\", "
-           "\"kcp_mtu\": %zu, \"groups_per_flush\": %zu, \"flushes\": %d, \"loss_per_group\": %zu, "
-           "\"tx_host_ns_per_packet\": %.1f, \"tx_flush_ms\": %.3f, \"tx_GiBps\": %.3f, \"tx_flush_only_GiBps\": %.2f, "
-           "\"rx_host_ns_per_packet\": %.1f, \"rx_flush_ms\": %.3f, \"rx_GiBps\": %.3f, \"rx_flush_only_GiBps\": %.2f, "
-           "\"recovered\": %zu, \"recovered_expected\": %zu, \"bad\": %zu}\n",
-           K, R, mtu, G, flushes, loss, t_tx_host / npk_tx * 1e9, t_tx_flush / flushes * 1e3,
-           payload / (t_tx_host + t_tx_flush) / (1 << 30), payload / t_tx_flush / (1 << 30), t_rx_host / npk_rx * 1e9,
-           t_rx_flush / flushes * 1e3, payload / (t_rx_host + t_rx_flush) / (1 << 30), payload / t_rx_flush / (1 << 30),
-           rec.n, total_groups * loss, rec.bad);
+    res.wall = std::chrono::duration<double>(clk::now() - w0).count();
+    res.recovered = rec.n;
+    res.bad = rec.bad;
+    if (rec.bad != 0 || rec.n != total_groups * loss) res.rc = 3;
     kfec_tx_destroy(tx);
     kfec_rx_destroy(rx);
     kfec_txq_destroy(tq);
     kfec_rxq_destroy(rq);
+}
+
+int main(int argc, char **argv)
+{
+    Params pa;
+    pa.K = argc > 1 ? atoi(argv[1]) : 20;
+    pa.N = argc > 2 ? atoi(argv[2]) : 23;
+    pa.mtu = argc > 3 ? atoi(argv[3]) : 1440;
+    pa.G = argc > 4 ? atoi(argv[4]) : 16384;
+    pa.flushes = argc > 5 ? atoi(argv[5]) : 4;
+    pa.loss = argc > 6 ? atoi(argv[6]) : 3;
+    const int T = argc > 7 ? std::max(1, atoi(argv[7])) : 1;
+    const size_t K = pa.K, R = pa.N - pa.K;
+    kfec_ctx *ctx = nullptr;
+    if (kfec_create(pa.K, pa.N, &ctx)) { printf("no GPU\n"); return 1; }
+    std::vector<Result> res(T);
+    std::vector<hipStream_t> streams(T, nullptr);
+    for (int t = 0; t < T; ++t)
+        if (T > 1 && hipStreamCreateWithFlags(&streams[t], hipStreamNonBlocking) != hipSuccess) return 1;
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t) th.emplace_back(run, ctx, std::cref(pa), 7 + t, streams[t], std::ref(res[t]));
+        for (auto &x : th) x.join();
+    }
+    Result a;  // per-thread averages of the phase times; wall = the slowest thread
+    size_t recovered = 0, bad = 0;
+    int rc = 0;
+    for (const Result &r : res) {
+        a.t_tx_host += r.t_tx_host / T; a.t_tx_flush += r.t_tx_flush / T;
+        a.t_rx_host += r.t_rx_host / T; a.t_rx_flush += r.t_rx_flush / T;
+        a.wall = std::max(a.wall, r.wall);
+        recovered += r.recovered;
+        bad += r.bad;
+        rc = rc ? rc : r.rc;
+    }
+    const size_t total_groups = pa.G * pa.flushes;
+    const double payload = (double)total_groups * K * pa.mtu;  // per thread and direction
+    const double npk_tx = (double)total_groups * K, npk_rx = (double)total_groups * (K - pa.loss + R);
+    printf("{\"metric\": \"batched FEC pipeline, host memory in and out\", \"threads\": %d, \"fec\": \"%zu:%zu\", "
+           "\"kcp_mtu\": %zu, \"groups_per_flush\": %zu, \"flushes\": %d, \"loss_per_group\": %zu, "
+           "\"tx_host_ns_per_packet\": %.1f, \"tx_flush_ms\": %.3f, \"tx_GiBps\": %.3f, \"tx_flush_only_GiBps\": %.2f, "
+           "\"rx_host_ns_per_packet\": %.1f, \"rx_flush_ms\": %.3f, \"rx_GiBps\": %.3f, \"rx_flush_only_GiBps\": %.2f, "
+           "\"all_threads_tx_plus_rx_GiBps\": %.2f, "
+           "\"recovered\": %zu, \"recovered_expected\": %zu, \"bad\": %zu}\n",
+           T, K, R, pa.mtu, pa.G, pa.flushes, pa.loss, a.t_tx_host / npk_tx * 1e9, a.t_tx_flush / pa.flushes * 1e3,
+           payload / (a.t_tx_host + a.t_tx_flush) / (1 << 30), payload / a.t_tx_flush / (1 << 30),
+           a.t_rx_host / npk_rx * 1e9, a.t_rx_flush / pa.flushes * 1e3, payload / (a.t_rx_host + a.t_rx_flush) / (1 << 30),
+           payload / a.t_rx_flush / (1 << 30), 2.0 * T * payload / a.wall / (1 << 30),
+           recovered, total_groups * pa.loss * T, bad);
+    for (hipStream_t st : streams)
+        if (st) (void)hipStreamDestroy(st);
     kfec_destroy(ctx);
-    return (rec.bad == 0 && rec.n == total_groups * loss) ? 0 : 3;
+    return rc;
 }
