@@ -7,9 +7,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "kfec_internal.hpp"
@@ -23,6 +25,8 @@ struct kfec_ctx {
     std::mutex mu;                 // single-group staging is shared by encode and decode callers
     uint8_t *d_stage = nullptr;
     size_t stage_cap = 0;
+    uint8_t *h_stage = nullptr;  // fine-grained pinned host staging the kernels read and write in place
+    size_t h_stage_cap = 0;
 };
 
 namespace {
@@ -70,6 +74,33 @@ int ensure_stage(kfec_ctx *c, size_t bytes)
 }
 
 inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// Single-group calls (the drop-in's per-call path) are latency-bound: a DMA copy costs ~10 us to set up, more
+// than a 29 KB group's whole encode.  So the shares are gathered on the host into fine-grained (coherent)
+// pinned memory, and the kernels read the shares and write the recovered / parity blocks there directly over
+// PCIe; the decode records stay in device memory.  KFEC_ZERO_COPY=0 restores the copy-based path (A/B).
+bool zero_copy()
+{
+    static const bool on = [] {
+        const char *e = getenv("KFEC_ZERO_COPY");
+        return !(e && std::string(e) == "0");
+    }();
+    return on;
+}
+
+int ensure_host_stage(kfec_ctx *c, size_t bytes)
+{
+    if (bytes <= c->h_stage_cap) return KFEC_OK;
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    c->h_stage = nullptr;
+    c->h_stage_cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 64 * 1024);
+    void *p = nullptr;
+    if (hipHostMalloc(&p, cap, hipHostMallocCoherent) != hipSuccess) return KFEC_ENOMEM;
+    c->h_stage = static_cast<uint8_t *>(p);
+    c->h_stage_cap = cap;
+    return KFEC_OK;
+}
 
 inline hipStream_t as_stream(void *s) { return static_cast<hipStream_t>(s); }
 
@@ -128,6 +159,7 @@ void kfec_destroy(kfec_ctx *ctx)
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->d_enc) (void)hipFree(ctx->d_enc);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -157,6 +189,17 @@ int kfec_encode(const kfec_ctx *cctx, const uint8_t *input, size_t data_length, 
     const size_t off_par = al256(K * B);
     int rc = ensure_stage(ctx, off_par + al256(R * B));
     if (rc) return rc;
+    if (zero_copy()) {
+        rc = ensure_host_stage(ctx, off_par + al256(R * B));
+        if (rc) return rc;
+        uint8_t *h_data = ctx->h_stage, *h_par = ctx->h_stage + off_par;
+        std::memcpy(h_data, input, K * B);
+        if (kfec::launch_encode(ctx->di, ctx->d_enc, (int)K, (int)N, 1, B, B, h_data, h_par, ctx->stream))
+            return KFEC_EHIP;
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess) return KFEC_EHIP;
+        std::memcpy(parity_out, h_par, R * B);
+        return KFEC_OK;
+    }
     uint8_t *d_data = ctx->d_stage, *d_par = ctx->d_stage + off_par;
     if (hipMemcpyAsync(d_data, input, K * B, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) return KFEC_EHIP;
     rc = kfec::launch_encode(ctx->di, ctx->d_enc, (int)K, (int)N, 1, B, B, d_data, d_par, ctx->stream);
@@ -188,6 +231,34 @@ int kfec_decode(const kfec_ctx *cctx, const size_t *share_ids, const uint8_t *co
                  total = o_rec + al256(kfec::decode_workspace_bytes(1, K, R));
     int rc = ensure_stage(ctx, total);
     if (rc) return rc;
+    if (zero_copy()) {
+        rc = ensure_host_stage(ctx, o_rec);
+        if (rc) return rc;
+        uint8_t *h = ctx->h_stage;
+        uint64_t *mask = reinterpret_cast<uint64_t *>(h + o_mask);
+        mask[0] = mask[1] = mask[2] = mask[3] = 0;
+        for (size_t i = 0; i < n_shares; ++i) {
+            const size_t s = share_ids[i];
+            mask[s >> 6] |= 1ull << (s & 63);
+            std::memcpy((s < K) ? h + o_data + s * B : h + o_par + (s - K) * B, share_ptrs[i], B);
+        }
+        rc = kfec::launch_decode(ctx->di, ctx->d_enc, (int)K, (int)N, 1, B, B, h + o_data, h + o_par, mask, h + o_out,
+                                 h + o_idx, h + o_st, ctx->d_stage + o_rec, ctx->stream);
+        if (rc) return KFEC_EHIP;
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess) return KFEC_EHIP;
+        const uint8_t st = h[o_st];
+        if (st == KFEC_GROUP_EMPTY) return KFEC_EMPTY;
+        if (st == KFEC_GROUP_SINGULAR) return KFEC_ESINGULAR;
+        size_t m = 0;
+        while (m < R && h[o_idx + m] != 0xFF) ++m;
+        if (m) {
+            if (!out || !out_ids) return KFEC_EINVAL;
+            std::memcpy(out, h + o_out, m * B);
+            for (size_t t = 0; t < m; ++t) out_ids[t] = h[o_idx + t];
+        }
+        *n_out = m;
+        return KFEC_OK;
+    }
     uint8_t *base = ctx->d_stage;
     uint64_t mask[4] = {0, 0, 0, 0};
     for (size_t i = 0; i < n_shares; ++i) {

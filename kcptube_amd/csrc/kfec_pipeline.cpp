@@ -18,6 +18,7 @@ namespace {
 constexpr uint32_t kFecWaits = KFEC_FEC_WAITS;
 
 size_t round4(size_t x) { return (x + 3) & ~size_t(3); }
+size_t round8(size_t x) { return (x + 7) & ~size_t(7); }
 
 // pinned host and device buffers, grown on demand
 struct Pinned {
@@ -81,6 +82,10 @@ struct Upload {
     // copy the tail and make `s` wait for every upload
     int finish(const Pinned &h, const Device &d, size_t used, hipStream_t s)
     {
+        if (issued == 0) {  // nothing went up early (a small flush): one copy on s, no cross-stream event
+            return (used == 0 || hipMemcpyAsync(d.p, h.p, used, hipMemcpyHostToDevice, s) == hipSuccess) ? KFEC_OK
+                                                                                                        : KFEC_EHIP;
+        }
         if (used > issued && hipMemcpyAsync(static_cast<uint8_t *>(d.p) + issued, static_cast<const uint8_t *>(h.p) + issued,
                                             used - issued, hipMemcpyHostToDevice, cs) != hipSuccess)
             return KFEC_EHIP;
@@ -140,9 +145,18 @@ struct kfec_txq {
     size_t used = 0;  // staged datagram bytes (packed back to back at 4-byte offsets: one H2D of these)
     size_t cap = 0;   // staging arena bytes
     std::vector<kfec_tx *> txs;  // the senders whose partial groups live in the arena
-    Pinned h_dg, h_off, h_len, h_sn, h_conv, h_pkt, h_pkt_len;
+    // h_meta: the per-group tables, filled at [0, GK*8) off, [m_len, +GK*2) len, [m_sn, +G*4) sn, [m_conv, +G*4)
+    // conv; a flush packs the used parts back to back and sends them in ONE copy (small flushes are
+    // latency-bound: each DMA costs microseconds to set up).  h_res: the redundant packets [n][R], then their
+    // lengths, again one copy back.
+    Pinned h_dg, h_meta, h_res;
+    size_t m_len = 0, m_sn = 0, m_conv = 0;
     std::vector<uint64_t> tags;
-    Device d_dg, d_off, d_len, d_sn, d_conv, d_par, d_align, d_pkt, d_pkt_len;
+    Device d_dg, d_meta, d_par, d_align, d_res;
+    uint64_t *h_off() const { return h_meta.as<uint64_t>(); }
+    uint16_t *h_len() const { return reinterpret_cast<uint16_t *>(h_meta.as<uint8_t>() + m_len); }
+    uint32_t *h_sn() const { return reinterpret_cast<uint32_t *>(h_meta.as<uint8_t>() + m_sn); }
+    uint32_t *h_conv() const { return reinterpret_cast<uint32_t *>(h_meta.as<uint8_t>() + m_conv); }
     Upload up;  // declared after the buffers: destroyed (and drained) before them
 };
 
@@ -178,12 +192,13 @@ int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram,
     const size_t pitch = round4(max_datagram + KFEC_FEC_CONTAINER_HEADER);
     const size_t pkt_pitch = round4(KFEC_PKT_REDUNDANT_HEADER + max_datagram + KFEC_FEC_CONTAINER_HEADER);
     // every buffer up front: a flush then costs copies and kernels only (pinning memory takes milliseconds)
-    if (q->h_dg.ensure(GK * q->slot) || q->h_off.ensure(GK * 8) || q->h_len.ensure(GK * 2) ||
-        q->h_sn.ensure(G * 4) || q->h_conv.ensure(G * 4) || q->h_pkt.ensure(G * R1 * pkt_pitch) ||
-        q->h_pkt_len.ensure(G * R1 * 2) || q->d_dg.ensure(GK * q->slot) || q->d_off.ensure(GK * 8) ||
-        q->d_len.ensure(GK * 2) || q->d_sn.ensure(G * 4) || q->d_conv.ensure(G * 4) ||
-        q->d_par.ensure(G * R1 * pitch) || q->d_align.ensure(G * 2) || q->d_pkt.ensure(G * R1 * pkt_pitch) ||
-        q->d_pkt_len.ensure(G * R1 * 2)) {
+    q->m_len = GK * 8;
+    q->m_sn = round8(GK * 10);
+    q->m_conv = q->m_sn + G * 4;
+    const size_t meta = q->m_conv + G * 4, res = G * R1 * (pkt_pitch + 2);
+    if (q->h_dg.ensure(GK * q->slot) || q->h_meta.ensure(meta) || q->h_res.ensure(res) ||
+        q->d_dg.ensure(GK * q->slot) || q->d_meta.ensure(meta) || q->d_res.ensure(res) ||
+        q->d_par.ensure(G * R1 * pitch) || q->d_align.ensure(G * 2)) {
         delete q;
         return KFEC_ENOMEM;
     }
@@ -261,12 +276,12 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
     // the group is complete: it takes queue slot n (compact_into_container + encode run at the flush)
     const size_t g = q->n;
     for (size_t i = 0; i < q->K; ++i) {
-        q->h_off.as<uint64_t>()[g * q->K + i] = tx->cache_off[i];
-        q->h_len.as<uint16_t>()[g * q->K + i] = tx->cache_len[i];
+        q->h_off()[g * q->K + i] = tx->cache_off[i];
+        q->h_len()[g * q->K + i] = tx->cache_len[i];
     }
     q->up.grow(q->h_dg, q->d_dg, q->used);
-    q->h_sn.as<uint32_t>()[g] = tx->sn;
-    q->h_conv.as<uint32_t>()[g] = tx->conv;
+    q->h_sn()[g] = tx->sn;
+    q->h_conv()[g] = tx->conv;
     q->tags[g] = tx->tag;
     q->n = g + 1;
     tx->cached = 0;  // fec_snd_cache.clear(), client.cpp:830-832
@@ -285,33 +300,41 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
     const size_t B = q->mtu + KFEC_FEC_CONTAINER_HEADER, pitch = round4(B);
     const size_t pkt_pitch = round4(KFEC_PKT_REDUNDANT_HEADER + B);
     const size_t nk = n * K;
+    // pack the used tables back to back (each destination lies below its source, and below the sources still
+    // to be moved): [off nk*8][len nk*2][pad][sn n*4][conv n*4]
+    uint8_t *hm = q->h_meta.as<uint8_t>();
+    const size_t L = nk * 8, S = round8(L + nk * 2), C = S + n * 4, T = C + n * 4;
+    std::memmove(hm + L, hm + q->m_len, nk * 2);
+    std::memmove(hm + S, hm + q->m_sn, n * 4);
+    std::memmove(hm + C, hm + q->m_conv, n * 4);
+    uint8_t *dm = q->d_meta.as<uint8_t>();
+    const uint64_t *d_off = reinterpret_cast<const uint64_t *>(dm);
+    const uint16_t *d_len = reinterpret_cast<const uint16_t *>(dm + L);
     if (q->up.finish(q->h_dg, q->d_dg, q->used, s) ||
-        hipMemcpyAsync(q->d_off.p, q->h_off.p, nk * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(q->d_len.p, q->h_len.p, nk * 2, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(q->d_sn.p, q->h_sn.p, n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(q->d_conv.p, q->h_conv.p, n * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+        hipMemcpyAsync(dm, hm, T, hipMemcpyHostToDevice, s) != hipSuccess)
         return KFEC_EHIP;
     const size_t arena = std::max<size_t>(q->used, 4);
-    int rc = kfec_encode_framed_batch(q->ctx, n, q->d_dg.p, arena, q->d_off.as<uint64_t>(), q->d_len.as<uint16_t>(), B,
-                                      pitch, q->d_par.p, q->d_align.as<uint16_t>(), stream);
+    int rc = kfec_encode_framed_batch(q->ctx, n, q->d_dg.p, arena, d_off, d_len, B, pitch, q->d_par.p,
+                                      q->d_align.as<uint16_t>(), stream);
     if (rc) return rc;
+    const size_t P = n * R * pkt_pitch;  // [n][R] compact redundant packets, then their lengths
     if (R) {
-        rc = kfec_pack_batch(q->ctx, n, KFEC_PACK_REDUNDANT | KFEC_PACK_COMPACT, q->d_dg.p, arena, q->d_off.as<uint64_t>(),
-                             q->d_len.as<uint16_t>(), pitch, q->d_par.p, q->d_align.as<uint16_t>(),
-                             q->d_sn.as<uint32_t>(), q->d_conv.as<uint32_t>(), timestamp, q->d_pkt.p, pkt_pitch,
-                             q->d_pkt_len.as<uint16_t>(), stream);
+        uint8_t *dr = q->d_res.as<uint8_t>();
+        rc = kfec_pack_batch(q->ctx, n, KFEC_PACK_REDUNDANT | KFEC_PACK_COMPACT, q->d_dg.p, arena, d_off, d_len, pitch,
+                             q->d_par.p, q->d_align.as<uint16_t>(), reinterpret_cast<const uint32_t *>(dm + S),
+                             reinterpret_cast<const uint32_t *>(dm + C), timestamp, dr, pkt_pitch,
+                             reinterpret_cast<uint16_t *>(dr + P), stream);
         if (rc) return rc;
-        // [n][R] compact redundant packets: two plain copies (a strided 2-D copy ran at ~3 GB/s)
-        if (hipMemcpyAsync(q->h_pkt.p, q->d_pkt.p, n * R * pkt_pitch, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(q->h_pkt_len.p, q->d_pkt_len.p, n * R * 2, hipMemcpyDeviceToHost, s) != hipSuccess)
-            return KFEC_EHIP;
+        if (hipMemcpyAsync(q->h_res.p, dr, P + n * R * 2, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
     }
     if (hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
-    const uint32_t *sn = q->h_sn.as<uint32_t>();
+    const uint32_t *sn = reinterpret_cast<const uint32_t *>(hm + S);
+    const uint8_t *pk = q->h_res.as<uint8_t>();
+    const uint16_t *pk_len = reinterpret_cast<const uint16_t *>(pk + P);
     for (size_t g = 0; g < n && cb; ++g)
         for (size_t r = 0; r < R; ++r) {
-            const uint16_t len = q->h_pkt_len.as<uint16_t>()[g * R + r];
-            if (len) cb(user, q->tags[g], sn[g], (uint8_t)(K + r), q->h_pkt.as<uint8_t>() + (g * R + r) * pkt_pitch, len);
+            const uint16_t len = pk_len[g * R + r];
+            if (len) cb(user, q->tags[g], sn[g], (uint8_t)(K + r), pk + (g * R + r) * pkt_pitch, len);
         }
     q->n = 0;
     // keep the partial groups: move their datagrams to the front of the arena, in arena order (every
@@ -346,10 +369,16 @@ struct kfec_rxq {
     size_t used = 0;  // arena bytes staged (shards packed back to back at 4-byte offsets: one H2D of these)
     size_t cap = 0;   // staging arena bytes
     std::vector<kfec_rx *> rxs;  // the receivers whose cached shards live in the arena
-    Pinned h_arena, h_off, h_len, h_present, h_idx, h_rec_len, h_dst;
+    // h_meta: [0, GN*8) off, [m_len, +GN*2) len, [m_pres, +G*32) present, packed back to back at a flush and
+    // sent in one copy; h_res: recovered datagrams [n][R], then their lengths, then the data indices (one copy)
+    Pinned h_arena, h_meta, h_res;
+    size_t m_len = 0, m_pres = 0;
+    uint64_t *h_off() const { return h_meta.as<uint64_t>(); }
+    uint16_t *h_len() const { return reinterpret_cast<uint16_t *>(h_meta.as<uint8_t>() + m_len); }
+    uint64_t *h_present() const { return reinterpret_cast<uint64_t *>(h_meta.as<uint8_t>() + m_pres); }
     std::vector<uint64_t> tags;
     std::vector<uint32_t> sns;
-    Device d_arena, d_off, d_len, d_present, d_align, d_out, d_idx, d_st, d_ws, d_rec_len, d_dst;
+    Device d_arena, d_meta, d_align, d_out, d_st, d_ws, d_res;
     Upload up;
 };
 
@@ -391,14 +420,14 @@ namespace {
 void rx_enqueue(kfec_rxq *q, uint64_t tag, uint32_t sn, const RxGroup &grp)
 {
     const size_t g = q->n;
-    uint64_t *present = q->h_present.as<uint64_t>() + g * 4;
+    uint64_t *present = q->h_present() + g * 4;
     present[0] = present[1] = present[2] = present[3] = 0;
     // a sub_sn beyond N is cached by the reference (it counts towards size()) but never selected usefully
     for (unsigned s = 0; s < q->N; ++s) {
         if (!grp.test(s)) continue;
         const size_t e = g * q->N + s;
-        q->h_off.as<uint64_t>()[e] = grp.off[s];
-        q->h_len.as<uint16_t>()[e] = grp.len[s];
+        q->h_off()[e] = grp.off[s];
+        q->h_len()[e] = grp.len[s];
         present[s >> 6] |= 1ull << (s & 63);
     }
     q->tags[g] = tag;
@@ -426,12 +455,13 @@ int kfec_rxq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_shard, kf
     q->slot = round4(max_shard);
     const size_t G = q->G, GN = G * q->N, R1 = std::max<size_t>(q->R, 1);
     const size_t pitch = round4(max_shard);
-    if (q->h_arena.ensure(GN * q->slot) || q->h_off.ensure(GN * 8) || q->h_len.ensure(GN * 2) ||
-        q->h_present.ensure(G * 32) || q->d_arena.ensure(GN * q->slot) || q->d_off.ensure(GN * 8) ||
-        q->d_len.ensure(GN * 2) || q->d_present.ensure(G * 32) || q->d_align.ensure(G * 2) || q->d_out.ensure(G * R1 * pitch) ||
-        q->d_idx.ensure(G * R1) || q->d_st.ensure(G) || q->d_ws.ensure(kfec_decode_workspace_size(ctx, G)) ||
-        q->d_rec_len.ensure(G * R1 * 2) || q->d_dst.ensure(G * R1 * pitch) || q->h_idx.ensure(G * R1) ||
-        q->h_rec_len.ensure(G * R1 * 2) || q->h_dst.ensure(G * R1 * pitch)) {
+    q->m_len = GN * 8;
+    q->m_pres = round8(GN * 10);
+    const size_t meta = q->m_pres + G * 32, res = G * R1 * (pitch + 3);
+    if (q->h_arena.ensure(GN * q->slot) || q->h_meta.ensure(meta) || q->h_res.ensure(res) ||
+        q->d_arena.ensure(GN * q->slot) || q->d_meta.ensure(meta) || q->d_res.ensure(res) ||
+        q->d_align.ensure(G * 2) || q->d_out.ensure(G * R1 * pitch) || q->d_st.ensure(G) ||
+        q->d_ws.ensure(kfec_decode_workspace_size(ctx, G))) {
         delete q;
         return KFEC_ENOMEM;
     }
@@ -558,33 +588,41 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
     const size_t N = q->N, R = q->R;
     const size_t B = q->max_shard, pitch = round4(B), dst_pitch = round4(B);
     const size_t nn = n * N;
+    // pack the used tables back to back: [off nn*8][len nn*2][pad][present n*32]
+    uint8_t *hm = q->h_meta.as<uint8_t>();
+    const size_t L = nn * 8, P = round8(L + nn * 2), T = P + n * 32;
+    std::memmove(hm + L, hm + q->m_len, nn * 2);
+    std::memmove(hm + P, hm + q->m_pres, n * 32);
+    uint8_t *dm = q->d_meta.as<uint8_t>();
     if (q->up.finish(q->h_arena, q->d_arena, q->used, s) ||
-        hipMemcpyAsync(q->d_off.p, q->h_off.p, nn * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(q->d_len.p, q->h_len.p, nn * 2, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(q->d_present.p, q->h_present.p, n * 32, hipMemcpyHostToDevice, s) != hipSuccess)
+        hipMemcpyAsync(dm, hm, T, hipMemcpyHostToDevice, s) != hipSuccess)
         return KFEC_EHIP;
+    // results: [n][R] recovered datagrams, then their lengths, then their data indices (one copy back)
+    const size_t D = n * R * dst_pitch;
+    uint8_t *dr = q->d_res.as<uint8_t>();
+    uint16_t *d_rec_len = reinterpret_cast<uint16_t *>(dr + D);
+    uint8_t *d_idx = dr + D + n * R * 2;
     // recv compact_into_container + decode fused: the chosen shares are framed on the fly from the arena
-    int rc = kfec_decode_framed_batch(q->ctx, n, q->d_arena.p, std::max<size_t>(q->used, 4), q->d_off.as<uint64_t>(),
-                                      q->d_len.as<uint16_t>(), q->d_present.as<uint64_t>(), B, pitch, q->d_out.p,
-                                      q->d_idx.as<uint8_t>(), q->d_st.as<uint8_t>(), q->d_align.as<uint16_t>(),
-                                      q->d_ws.p, stream);
+    int rc = kfec_decode_framed_batch(q->ctx, n, q->d_arena.p, std::max<size_t>(q->used, 4),
+                                      reinterpret_cast<const uint64_t *>(dm), reinterpret_cast<const uint16_t *>(dm + L),
+                                      reinterpret_cast<const uint64_t *>(dm + P), B, pitch, q->d_out.p, d_idx,
+                                      q->d_st.as<uint8_t>(), q->d_align.as<uint16_t>(), q->d_ws.p, stream);
     if (rc) return rc;
     if (R) {
-        rc = kfec_unframe_batch(q->ctx, n, B, pitch, q->d_out.p, q->d_idx.as<uint8_t>(), q->d_rec_len.as<uint16_t>(),
-                                q->d_dst.p, dst_pitch, stream);
+        rc = kfec_unframe_batch(q->ctx, n, B, pitch, q->d_out.p, d_idx, d_rec_len, dr, dst_pitch, stream);
         if (rc) return rc;
-        if (hipMemcpyAsync(q->h_idx.p, q->d_idx.p, n * R, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(q->h_rec_len.p, q->d_rec_len.p, n * R * 2, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(q->h_dst.p, q->d_dst.p, n * R * dst_pitch, hipMemcpyDeviceToHost, s) != hipSuccess)
-            return KFEC_EHIP;
+        if (hipMemcpyAsync(q->h_res.p, dr, D + n * R * 3, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
     }
     if (hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
+    const uint8_t *hr = q->h_res.as<uint8_t>();
+    const uint16_t *rec_len = reinterpret_cast<const uint16_t *>(hr + D);
+    const uint8_t *rec_idx = hr + D + n * R * 2;
     for (size_t g = 0; g < n && cb && R; ++g)
         for (size_t t = 0; t < R; ++t) {
-            const uint8_t idx = q->h_idx.as<uint8_t>()[g * R + t];
-            const uint16_t len = q->h_rec_len.as<uint16_t>()[g * R + t];
+            const uint8_t idx = rec_idx[g * R + t];
+            const uint16_t len = rec_len[g * R + t];
             if (idx == 0xFF || len == 0xFFFF) continue;
-            cb(user, q->tags[g], q->sns[g], idx, q->h_dst.as<uint8_t>() + (g * R + t) * dst_pitch, len);
+            cb(user, q->tags[g], q->sns[g], idx, hr + (g * R + t) * dst_pitch, len);
         }
     q->n = 0;
     // keep the shards of the groups still waiting for K shares: move them to the front of the arena, in arena
