@@ -808,12 +808,14 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
     }
 }
 
-template <int VEC, int MT, bool DEC>
+template <int VEC, int MT, bool DEC, int PDX = 0>
 __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
 {
     using L = MacLayout<MT>;
     constexpr int W = Gran<VEC>::W;
-    constexpr int PD = VEC >= 32 ? KFEC_PD / 2 : KFEC_PD;  // shards in flight per lane (~64 B per lane)
+    // shards in flight per lane (~64 B per lane); PDX: the latency shape (a handful of groups, often read
+    // straight from pinned host memory) keeps many more loads in flight so the PCIe round trips overlap
+    constexpr int PD = PDX ? PDX : (VEC >= 32 ? KFEC_PD / 2 : KFEC_PD);
     constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
 
@@ -1737,7 +1739,7 @@ static size_t pad_cols(size_t cols)
     return on ? (cols + 63) / 64 * 64 : cols;
 }
 
-template <int VEC, int MT, bool DEC>
+template <int VEC, int MT, bool DEC, int PDX = 0>
 static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
 {
     using L = MacLayout<MT>;
@@ -1751,7 +1753,7 @@ static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
     static const int persist = env_int("KFEC_GRID_PERSIST", 0);
     uint32_t gx = want;
     if (persist) {
-        uint32_t cap = (uint32_t)(std::max(1, di.cus) * resident_blocks((const void *)mac_kernel<VEC, MT, DEC>, lds))
+        uint32_t cap = (uint32_t)(std::max(1, di.cus) * resident_blocks((const void *)mac_kernel<VEC, MT, DEC, PDX>, lds))
                        / (uint32_t)std::max(1, tiles);
         if (tiles > 1 && cap >= 8) cap &= ~7u;
         gx = std::min(want, std::max(cap, 1u));
@@ -1759,9 +1761,15 @@ static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
         gx = (want + 7) & ~7u;
     }
     gx = std::max(1u, gx);
-    hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC>), dim3(gx, tiles), dim3(kMacBlock), lds, s, a);
+    hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC, PDX>), dim3(gx, tiles), dim3(kMacBlock), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+// Batches of at most kLatencyGroups groups (the single-group drop-in calls, whose shares sit in pinned host
+// memory) run the MAC with 4-byte granules and 16 shards in flight per lane: ~8x more lanes and loads in
+// flight than the streaming shape, so the PCIe round trips of a 29 KB group overlap instead of queueing.
+constexpr int kLatencyVec = -4;
+constexpr size_t kLatencyGroups = 4;
 
 template <bool DEC>
 static int dispatch_mac(const DeviceInfo &di, int vec, int mt, MacArgs a, int tiles, hipStream_t s)
@@ -1773,6 +1781,15 @@ static int dispatch_mac(const DeviceInfo &di, int vec, int mt, MacArgs a, int ti
     case 3: return run_mac<V, 3, DEC>(di, a, tiles, s);                      \
     case 4: return run_mac<V, 4, DEC>(di, a, tiles, s);                      \
     default: return run_mac<V, 8, DEC>(di, a, tiles, s);                     \
+    }
+    if (vec == kLatencyVec) {  // the latency shape: dword granules, 16 shards in flight per lane
+        switch (mt) {
+        case 1: return run_mac<4, 1, DEC, 16>(di, a, tiles, s);
+        case 2: return run_mac<4, 2, DEC, 16>(di, a, tiles, s);
+        case 3: return run_mac<4, 3, DEC, 16>(di, a, tiles, s);
+        case 4: return run_mac<4, 4, DEC, 16>(di, a, tiles, s);
+        default: return run_mac<4, 8, DEC, 16>(di, a, tiles, s);
+        }
     }
     switch (vec) {
 #if KFEC_VEC32
@@ -2065,6 +2082,7 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     }
     int vec = 0, mt = 0;
     mac_shape(R, pick_vec_mac(pitch, {d_data, d_parity}), vec, mt);
+    if (G <= kLatencyGroups && vec >= 4) vec = kLatencyVec;
     const int vb = vec >= 4 ? vec : 4;
     const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
     const int tiles = (R + mt - 1) / mt;
@@ -2213,6 +2231,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
 
     int vec = 0, mt = 0;
     mac_shape(R, pick_vec_mac(pitch, {d_data, d_parity, d_out}), vec, mt);
+    if (G <= kLatencyGroups && vec >= 4) vec = kLatencyVec;
     const int vb = vec >= 4 ? vec : 4;
     const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
     const int tiles = (R + mt - 1) / mt;
