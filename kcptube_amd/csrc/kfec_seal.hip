@@ -48,9 +48,11 @@ __constant__ Crc32Tables c_crc = make_crc32_tables();
 // ---- parallel CRC-32 -------------------------------------------------------------------------------
 // Half a wave (32 lanes) per packet.  The message is right-aligned into 512-byte rounds (leading zero bytes
 // leave a CRC computed from a zero register unchanged); lane l takes the 16-byte chunk l of a round and
-// computes its raw CRC (zero init, slicing-by-4), and the 32 chunk CRCs are combined in 5 butterfly levels:
+// computes its raw CRC (zero init, slicing-by-4) and folds it into its own running sum across rounds
+// (Horner with shift_512); the 32 lanes' sums are combined once per packet in 5 butterfly levels:
 //   CRC(A || B) = shift_|B|(CRC(A)) ^ CRC(B),   shift_d(r) = r advanced through d zero bytes,
-// a GF(2)-linear map applied as 4 byte-indexed table lookups.  Rounds combine with shift_512.  The
+// a GF(2)-linear map applied as 4 byte-indexed table lookups (linearity makes the per-lane sums combine
+// exactly like one round's chunk CRCs).  The
 // standard 0xFFFFFFFF init is folded in by complementing the first 4 message bytes (messages >= 4 bytes;
 // shorter ones run serially on one lane), and the result is complemented at the end.
 //   tables: [0] slicing-by-4 (4 x 256), [1 + k] shift by 16 << k bytes (k = 0..5), each 4 x 256 u32
@@ -167,13 +169,17 @@ __device__ uint32_t row_crc32(const uint32_t (*tab)[4][256], const uint32_t *bas
             uint32_t c = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) c = crc_dword(tab[0], c, o[u][i]);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                const uint32_t other = __shfl_xor(c, 1 << k, kRowLanes);
-                c = (lane & (1u << k)) ? crc_shift(tab[1 + k], other) ^ c : crc_shift(tab[1 + k], c) ^ other;
-            }
+            // Horner over this lane's chunks: R = XOR_r shift_{(rounds-1-r)*512}(chunk CRC of round r)
             if (r0 + u < rounds) R = crc_shift(tab[6], R) ^ c;
         }
+    }
+    // one butterfly per packet (not per round): by linearity the 32 lanes' Horner sums combine exactly as
+    // one round's chunk CRCs do.  Level k: the lane holding the earlier block A shifts it past the later
+    // block B (16 << k bytes): A' = shift(A) ^ B -- one table shift per lane, the operands picked by lane bit
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t other = __shfl_xor(R, 1 << k, kRowLanes);
+        const bool later = lane & (1u << k);
+        R = crc_shift(tab[1 + k], later ? other : R) ^ (later ? R : other);
     }
     return ~R;
 }
@@ -364,9 +370,15 @@ __global__ void __launch_bounds__(kSealBlock) open_kernel(SealArgs a)
         }
 #pragma unroll
         for (int k = 0; k < 5; ++k) trailer |= __shfl_xor(trailer, 1 << k, kRowLanes);
-        // CRC of the plaintext just written (same wave: drain the stores first; the lines were never read)
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        const uint32_t crc = row_crc32(s_tab, dst, nd, 0, n, lane);
+        // CRC of the plaintext: for "none" it is the packet's own first n bytes; for plain_xor the plaintext
+        // just written (same wave: drain the stores first)
+        uint32_t crc;
+        if (px) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            crc = row_crc32(s_tab, dst, nd, 0, n, lane);
+        } else {
+            crc = row_crc32(s_tab, a.src, a.src_dw, off, n, lane);
+        }
         if (lane == 0) {
             a.out_len[p] = n;
             a.ok[p] = checksum16(crc) == trailer;
