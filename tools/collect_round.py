@@ -11,8 +11,8 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 go = os.path.join(root, "gpurun_out")
 prof = os.path.join(root, "profiles")
 rnd = os.path.join(go, "round")
-for name in ("bench_203.json", "bench_103dec.json", "bench_20055.json", "wire.json", "seal.json", "gtest.log",
-             "smoke.log"):
+for name in ("bench_203.json", "bench_103dec.json", "bench_20055.json", "wire.json", "wire_ragged.json", "seal.json",
+             "pipeline_threads.json", "latency.json", "gtest.log", "smoke.log"):
     src = os.path.join(rnd, name)
     if os.path.exists(src):
         shutil.copy(src, os.path.join(prof, f"{tag}_{name.replace('.log', '.txt')}"))

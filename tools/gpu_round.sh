@@ -13,5 +13,9 @@ timeout -k 10 300 python bench.py --config 200:55 --no-cpu --steps 5 > $out/benc
 cat $out/bench_*.json | cut -c1-400
 timeout -k 10 200 python tools/bench_wire.py > $out/wire.json || exit 1
 timeout -k 10 200 python tools/bench_seal.py > $out/seal.json || exit 1
+timeout -k 10 200 python tools/bench_wire.py --ragged > $out/wire_ragged.json || exit 1
+# host-memory pipeline (1..8 host threads) and the latency path; binaries built beforehand (tools/*.cpp headers)
+for t in 1 2 4 8; do timeout -k 10 300 ./tools/pipeline_bench 20 23 1440 16384 4 3 $t || exit 1; done > $out/pipeline_threads.json
+timeout -k 10 120 ./tools/latency_bench > $out/latency.json || exit 1
 bash tools/gpu_profile_all.sh || exit 1
 echo round-done
