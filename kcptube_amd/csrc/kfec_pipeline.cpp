@@ -525,7 +525,6 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
     const size_t plen = len - H;
     if (plen + (red ? 0 : KFEC_FEC_CONTAINER_HEADER) > q->max_shard) return KFEC_EINVAL;
     const uint32_t fec_sn = get_be32(pkt + 4);
-    // capacity: this push can queue at most every not-yet-restored cached group plus a new one
     auto found = rx->cache.find(fec_sn);
     // capacity: only this packet's group can become decodable on this push (every other cached group either
     // reached K shares on an earlier push, and was queued and restored then, or still lacks shares)
