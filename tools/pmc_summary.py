@@ -43,7 +43,7 @@ for k, v in agg.items():
 json.dump(summary, open(os.path.join(out, f"{args.tag}_pmc.json"), "w"), indent=1)
 trf_path = os.path.join(out, "pmc_traffic.json")
 trf = json.load(open(trf_path)) if os.path.exists(trf_path) else {}
-dominant = re.compile(r"mac_kernel<\d+, \d+, %s>" % ("true" if args.config.endswith("dec") else "false"))
+dominant = re.compile(r"mac_kernel<\d+, \d+, %s(, \d+)?>" % ("true" if args.config.endswith("dec") else "false"))
 for k, d in summary.items():
     if dominant.search(k) and "hbm_bytes_per_launch" in d:
         trf[args.config] = {"groups": args.groups, "kernel": k, "hbm_bytes_per_launch": int(d["hbm_bytes_per_launch"]),
