@@ -114,8 +114,9 @@ def main():
     from kcptube_amd import FecCode
 
     K, N, B, G, pool, erase, rnd, do_enc, workload = CONFIGS[args.config]
-    if args.groups:
+    if args.groups and args.groups != G:
         G = args.groups
+        workload += f" (--groups override: {G} groups per GPU)"
     R = N - K
     c = FecCode(K, N)
     g0 = rank * G  # this rank's contiguous range of the global group space
