@@ -24,33 +24,6 @@ namespace {
 constexpr int kFrameBlock = 256;
 constexpr uint64_t kMaxGrid = 1u << 24;
 
-__device__ __forceinline__ uint32_t byte_mask(int64_t q0, int64_t len)
-{
-    uint32_t m = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int64_t q = q0 + b;
-        if (q >= 0 && q < len) m |= 0xFFu << (8 * b);
-    }
-    return m;
-}
-
-// bytes [q0, q0 + 4) of the payload base[start, start + len), zero outside it; base is dword aligned and
-// only dwords below lim32 are read
-__device__ __forceinline__ uint32_t payload_dword(const uint32_t *base32, uint64_t lim32, uint64_t start, uint32_t len,
-                                                  int64_t q0)
-{
-    const uint32_t m = byte_mask(q0, len);
-    if (!m) return 0u;
-    const uint64_t a4 = start + (uint64_t)(q0 + 4);  // address of the first byte + 4 (q0 >= -3 here)
-    const uint64_t w1 = a4 >> 2;                      // its dword index + 1
-    const uint32_t sh = (uint32_t)(a4 & 3u);
-    const uint32_t lo = (w1 >= 1 && w1 - 1 < lim32) ? base32[w1 - 1] : 0u;
-    const uint32_t hi = (sh && w1 < lim32) ? base32[w1] : 0u;
-    const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
-    return v & m;
-}
-
 // 16 bytes [q0, q0 + 16) of the payload base[start, start + len) as 4 dwords, zero outside it: one 16-byte
 // load at the covering dword (dword aligned is enough on gfx950, as the MAC kernel's granules rely on) and
 // one more dword, re-based with v_alignbyte_b32.  Dwords at or beyond lim32 read as zero.

@@ -1045,6 +1045,7 @@ __device__ __forceinline__ void tile_stage(const LdsArgs &a, uint8_t *buf, uint3
         for (uint32_t ch = wave; ch * 1024 < bytes; ch += nw) {
             const uint32_t o = ch * 1024 + lane * 16;
             const uint32_t jj = (uint32_t)(((uint64_t)o * a.bs_inv) >> 32), off = o - jj * a.Bs;  // o / Bs
+            (void)off;  // read only in the device pass
             if (o < bytes) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the builtin exists only in the device pass of this single-source file
                 __builtin_amdgcn_global_load_lds(shard_src(jj) + off,
@@ -1547,7 +1548,7 @@ __global__ void __launch_bounds__(kEngThreads) mac_stream_kernel(StreamArgs a)
                 return;
             }
             const uint32_t c0 = c * JS, nj = min(JS, K - c0);
-            uint8_t *slot = smem + s * a.slot_bytes;
+            [[maybe_unused]] uint8_t *slot = smem + s * a.slot_bytes;  // read only in the device pass
             bool work = true;
             const uint8_t *rec = nullptr;
             if constexpr (DEC) {
@@ -1581,7 +1582,8 @@ __global__ void __launch_bounds__(kEngThreads) mac_stream_kernel(StreamArgs a)
                 for (uint32_t ch = 0; ch * 1024 < bytes; ++ch) {
                     const uint32_t o = ch * 1024 + lane * 16;
                     const uint32_t jj = (uint32_t)(((uint64_t)min(o, bytes - 1) * a.bs_inv) >> 32), off = o - jj * a.Bs;
-                    const uint8_t *src;
+                    (void)off;  // read only in the device pass
+                    [[maybe_unused]] const uint8_t *src;
                     if constexpr (DEC) {
                         if (nj <= 64) {
                             src = reinterpret_cast<const uint8_t *>(__shfl(my_base, (int)jj));
@@ -1858,7 +1860,7 @@ static int run_tile(const DeviceInfo &di, LdsArgs a, int tiles, hipStream_t s)
 }
 
 // ---- wave-tile launch ----
-static constexpr size_t kWtLdsMax = 13 * 1024;  // 12 waves (workgroups) per CU fit in 160 KiB
+[[maybe_unused]] static constexpr size_t kWtLdsMax = 13 * 1024;  // 12 waves (workgroups) per CU fit in 160 KiB
 
 struct WtPlan {
     bool ok = false;
