@@ -59,6 +59,26 @@ def build_variant(name: str, defines: dict[str, int]) -> str:
     return out
 
 
+def build_tools(force: bool = False) -> list[str]:
+    """The C++ programs over the public headers: tools/pipeline_bench (kfec_pipeline.h from C++, one
+    sender + receiver per host thread, bit-exact recovery check; also run by tests/test_gpu_pipeline.py) and
+    tools/latency_bench (the per-call latency path)."""
+    inc = os.path.join(ROOT, "include")
+    out = []
+    for name, extra in (("pipeline_bench", ["-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include", "-L", "/opt/rocm/lib",
+                                            "-lamdhip64", "-pthread"]),
+                        ("latency_bench", [])):
+        src = os.path.join(ROOT, "tools", name + ".cpp")
+        exe = os.path.join(ROOT, "tools", name)
+        deps = [src, LIB] + [os.path.join(inc, h) for h in ("kfec.h", "kfec_frame.h", "kfec_pipeline.h")]
+        if force or _stale(exe, deps):
+            cmd = ["g++", "-std=c++17", "-O2", "-I", inc, src, "-o", exe, "-L", PKG, "-lkfec",
+                   "-Wl,-rpath,$ORIGIN/../kcptube_amd"] + extra
+            subprocess.check_call(cmd)
+        out.append(exe)
+    return out
+
+
 def build_compat_test(force: bool = False) -> str:
     """C++ program exercising include/fecpp_compat.hpp against libkfec.so (run by the GPU tests)."""
     src = os.path.join(ROOT, "tests", "cpp", "compat_test.cpp")

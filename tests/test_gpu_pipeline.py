@@ -227,3 +227,19 @@ def test_receiver_frequent_flushes_and_duplicates(dev, oracle, K, N, mtu, max_gr
     assert n_rec > 5
     if max_groups <= 2:
         assert n_full > 0  # the KFEC_ENOMEM -> flush -> retry path ran
+
+
+def test_cpp_program_over_the_pipeline_header(dev):
+    """tools/pipeline_bench.cpp: a C++ program over include/kfec_pipeline.h (what a kcptube build links),
+    two host threads each with their own queues and stream on one shared context, every group losing 3 data
+    packets; it exits 0 only when every lost datagram came back bit-exact."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "pipeline_bench")
+    if not os.path.exists(exe):
+        pytest.skip("tools/pipeline_bench not built (kcptube_amd.build.build_tools)")
+    p = subprocess.run([exe, "10", "13", "1400", "512", "3", "3", "2"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["bad"] == 0 and r["recovered"] == r["recovered_expected"] == 2 * 512 * 3 * 3
