@@ -16,8 +16,9 @@
  *     as it holds >= K shares (even when nothing is missing).
  * What is batched: a group that becomes complete (send) or decodable (receive) is copied into the queue's
  * pinned staging; kfec_txq_flush / kfec_rxq_flush code every queued group in one GPU batch
- * (kfec_encode_framed_batch + kfec_pack_batch; kfec_decode_framed_batch + kfec_unframe_batch) and hand back redundant packets / recovered datagrams through a callback, in queue
- * order.  The reference inputs a recovered datagram to KCP inside fec_find_missings; here that happens at the
+ * (kfec_encode_framed_batch + kfec_pack_batch; kfec_decode_framed_batch, whose recovered shards come back
+ * whole and have their BE16 length read at the callback) and hand back redundant packets / recovered
+ * datagrams through a callback, in queue order.  The reference inputs a recovered datagram to KCP inside fec_find_missings; here that happens at the
  * flush, which the caller schedules (e.g. once per event-loop turn) -- the latency / throughput trade the
  * batching buys.  Shard padding is zero (include/kfec_frame.h).
  *

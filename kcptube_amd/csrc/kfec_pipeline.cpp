@@ -370,7 +370,7 @@ struct kfec_rxq {
     size_t cap = 0;   // staging arena bytes
     std::vector<kfec_rx *> rxs;  // the receivers whose cached shards live in the arena
     // h_meta: [0, GN*8) off, [m_len, +GN*2) len, [m_pres, +G*32) present, packed back to back at a flush and
-    // sent in one copy; h_res: recovered datagrams [n][R], then their lengths, then the data indices (one copy)
+    // sent in one copy; h_res: recovered framed shards [n][R], then their data indices (one copy)
     Pinned h_arena, h_meta, h_res;
     size_t m_len = 0, m_pres = 0;
     uint64_t *h_off() const { return h_meta.as<uint64_t>(); }
@@ -378,7 +378,7 @@ struct kfec_rxq {
     uint64_t *h_present() const { return reinterpret_cast<uint64_t *>(h_meta.as<uint8_t>() + m_pres); }
     std::vector<uint64_t> tags;
     std::vector<uint32_t> sns;
-    Device d_arena, d_meta, d_align, d_out, d_st, d_ws, d_res;
+    Device d_arena, d_meta, d_align, d_st, d_ws, d_res;
     Upload up;
 };
 
@@ -460,7 +460,7 @@ int kfec_rxq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_shard, kf
     const size_t meta = q->m_pres + G * 32, res = G * R1 * (pitch + 3);
     if (q->h_arena.ensure(GN * q->slot) || q->h_meta.ensure(meta) || q->h_res.ensure(res) ||
         q->d_arena.ensure(GN * q->slot) || q->d_meta.ensure(meta) || q->d_res.ensure(res) ||
-        q->d_align.ensure(G * 2) || q->d_out.ensure(G * R1 * pitch) || q->d_st.ensure(G) ||
+        q->d_align.ensure(G * 2) || q->d_st.ensure(G) ||
         q->d_ws.ensure(kfec_decode_workspace_size(ctx, G))) {
         delete q;
         return KFEC_ENOMEM;
@@ -585,7 +585,7 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
     if (n == 0) return KFEC_OK;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t N = q->N, R = q->R;
-    const size_t B = q->max_shard, pitch = round4(B), dst_pitch = round4(B);
+    const size_t B = q->max_shard, pitch = round4(B);
     const size_t nn = n * N;
     // pack the used tables back to back: [off nn*8][len nn*2][pad][present n*32]
     uint8_t *hm = q->h_meta.as<uint8_t>();
@@ -596,32 +596,30 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
     if (q->up.finish(q->h_arena, q->d_arena, q->used, s) ||
         hipMemcpyAsync(dm, hm, T, hipMemcpyHostToDevice, s) != hipSuccess)
         return KFEC_EHIP;
-    // results: [n][R] recovered datagrams, then their lengths, then their data indices (one copy back)
-    const size_t D = n * R * dst_pitch;
+    // results: [n][R] recovered framed shards, then their data indices (one copy back).  extract_from_container
+    // (data_operations.cpp:697-704) is only "skip the BE16 length": done here on the host at the callback, so
+    // no unframe pass and no second copy of the recovered bytes
+    const size_t D = n * R * pitch;
     uint8_t *dr = q->d_res.as<uint8_t>();
-    uint16_t *d_rec_len = reinterpret_cast<uint16_t *>(dr + D);
-    uint8_t *d_idx = dr + D + n * R * 2;
+    uint8_t *d_idx = dr + D;
     // recv compact_into_container + decode fused: the chosen shares are framed on the fly from the arena
     int rc = kfec_decode_framed_batch(q->ctx, n, q->d_arena.p, std::max<size_t>(q->used, 4),
                                       reinterpret_cast<const uint64_t *>(dm), reinterpret_cast<const uint16_t *>(dm + L),
-                                      reinterpret_cast<const uint64_t *>(dm + P), B, pitch, q->d_out.p, d_idx,
+                                      reinterpret_cast<const uint64_t *>(dm + P), B, pitch, dr, d_idx,
                                       q->d_st.as<uint8_t>(), q->d_align.as<uint16_t>(), q->d_ws.p, stream);
     if (rc) return rc;
-    if (R) {
-        rc = kfec_unframe_batch(q->ctx, n, B, pitch, q->d_out.p, d_idx, d_rec_len, dr, dst_pitch, stream);
-        if (rc) return rc;
-        if (hipMemcpyAsync(q->h_res.p, dr, D + n * R * 3, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
-    }
+    if (R && hipMemcpyAsync(q->h_res.p, dr, D + n * R, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
     if (hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
     const uint8_t *hr = q->h_res.as<uint8_t>();
-    const uint16_t *rec_len = reinterpret_cast<const uint16_t *>(hr + D);
-    const uint8_t *rec_idx = hr + D + n * R * 2;
+    const uint8_t *rec_idx = hr + D;
     for (size_t g = 0; g < n && cb && R; ++g)
         for (size_t t = 0; t < R; ++t) {
             const uint8_t idx = rec_idx[g * R + t];
-            const uint16_t len = rec_len[g * R + t];
-            if (idx == 0xFF || len == 0xFFFF) continue;
-            cb(user, q->tags[g], q->sns[g], idx, hr + (g * R + t) * dst_pitch, len);
+            if (idx == 0xFF) continue;
+            const uint8_t *shard = hr + (g * R + t) * pitch;
+            const size_t len = ((size_t)shard[0] << 8) | shard[1];  // ntohs(data_length)
+            if (len + KFEC_FEC_CONTAINER_HEADER > B) continue;     // inconsistent group (kfec_unframe_batch's 0xFFFF)
+            cb(user, q->tags[g], q->sns[g], idx, shard + KFEC_FEC_CONTAINER_HEADER, len);
         }
     q->n = 0;
     // keep the shards of the groups still waiting for K shares: move them to the front of the arena, in arena
