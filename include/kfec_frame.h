@@ -60,6 +60,15 @@ int kfec_encode_framed_batch(const kfec_ctx *ctx, size_t G, const void *d_src, s
                              const uint64_t *d_off, const uint16_t *d_len, size_t B, size_t pitch, void *d_parity,
                              uint16_t *d_align, void *stream);
 
+/* The whole send side in two launches: kfec_encode_framed_batch + kfec_pack_batch(KFEC_PACK_DATA |
+ * KFEC_PACK_REDUNDANT), with the data packets written by the encoder itself while it reads each datagram
+ * for the parity (so the datagrams are read once, not twice).  d_pkt[g][N][pkt_pitch] / d_pkt_len[g][N],
+ * d_parity and d_align are byte-identical to the two-call path. */
+int kfec_encode_pack_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size_t src_bytes, const uint64_t *d_off,
+                           const uint16_t *d_len, size_t B, size_t pitch, void *d_parity, uint16_t *d_align,
+                           const uint32_t *d_sn, const uint32_t *d_conv, uint32_t timestamp, void *d_pkt,
+                           size_t pkt_pitch, uint16_t *d_pkt_len, void *stream);
+
 /* compact_into_container, receive variant (data_operations.cpp:633-667), for G cached groups.
  * Shard s < N of group g is present when bit s of d_present[g][4] is set; its bytes are
  * [d_off[g*N+s], +d_len[g*N+s]) of d_src.  Present data shards (s < K) are framed as on the send side into

@@ -477,6 +477,35 @@ int kfec_pack_batch(const kfec_ctx *ctx, size_t G, unsigned which, const void *d
                : KFEC_OK;
 }
 
+int kfec_encode_pack_batch(const kfec_ctx *ctx, size_t G, const void *d_src, size_t src_bytes, const uint64_t *d_off,
+                           const uint16_t *d_len, size_t B, size_t pitch, void *d_parity, uint16_t *d_align,
+                           const uint32_t *d_sn, const uint32_t *d_conv, uint32_t timestamp, void *d_pkt,
+                           size_t pkt_pitch, uint16_t *d_pkt_len, void *stream)
+{
+    if (!ctx || pitch < B || pitch % 4 || B > 0xFFFF || pkt_pitch % 4) return KFEC_EINVAL;
+    if (G && (!d_src || !al4(d_src) || !d_off || !d_len || !d_align || !d_sn || !d_pkt || !al4(d_pkt) || !d_pkt_len))
+        return KFEC_EINVAL;
+    if (G && ctx->N > ctx->K && (!d_parity || !al4(d_parity) || !d_conv)) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    const hipStream_t s = as_stream(stream);
+    const kfec::DataPackets dp{d_pkt, d_pkt_len, d_sn, pkt_pitch, timestamp};
+    const int rc = kfec::launch_framed_encode(ctx->d_enc, (int)ctx->K, (int)ctx->N, G, d_src, src_bytes, d_off, d_len,
+                                              B, pitch, d_parity, d_align, s, &dp);
+    if (rc < 0) return KFEC_EHIP;
+    if (rc == 0)  // data packets came out of the encoder; the redundant ones from the parity it wrote
+        return kfec::launch_pack((int)ctx->K, (int)ctx->N, G, KFEC_PACK_REDUNDANT, d_src, src_bytes, d_off, d_len, pitch,
+                                 d_parity, d_align, d_sn, d_conv, timestamp, d_pkt, pkt_pitch, d_pkt_len, s)
+                   ? KFEC_EHIP
+                   : KFEC_OK;
+    // shapes the fused kernel does not take: the framed encode (with its own fallback), then both packet kinds
+    const int r = kfec_encode_framed_batch(ctx, G, d_src, src_bytes, d_off, d_len, B, pitch, d_parity, d_align, stream);
+    if (r) return r;
+    return kfec::launch_pack((int)ctx->K, (int)ctx->N, G, KFEC_PACK_DATA | KFEC_PACK_REDUNDANT, d_src, src_bytes, d_off,
+                             d_len, pitch, d_parity, d_align, d_sn, d_conv, timestamp, d_pkt, pkt_pitch, d_pkt_len, s)
+               ? KFEC_EHIP
+               : KFEC_OK;
+}
+
 int kfec_unpack_batch(const kfec_ctx *ctx, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
                       const uint32_t *d_len, kfec_pkt_hdr *d_hdr, void *stream)
 {

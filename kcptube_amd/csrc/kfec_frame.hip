@@ -207,12 +207,12 @@ __global__ void __launch_bounds__(kFrameBlock) pack_kernel(PackArgs a)
     const uint32_t lane = threadIdx.x % kRowLanes;
     for (uint64_t pk = (uint64_t)blockIdx.x * kRowsPerBlock + row_in_block(); pk < a.rows;
          pk += (uint64_t)gridDim.x * kRowsPerBlock) {
-        const uint64_t g = pk / a.N;
-        const uint32_t s = (uint32_t)(pk - g * a.N);
+        // rows run over the selected kinds only: row pk is packet s0 + k of group g (k < nsel)
+        const uint64_t g = pk / a.nsel;
+        const uint32_t s = a.s0 + (uint32_t)(pk - g * a.nsel);
         const bool red = s >= a.K;
-        if (!(a.which & (red ? KFEC_PACK_REDUNDANT : KFEC_PACK_DATA))) continue;
         // output slot: (g, s) of [G][N], or of [G][emitted kinds] with KFEC_PACK_COMPACT
-        const uint64_t slot = (a.which & KFEC_PACK_COMPACT) ? g * a.nsel + (s - a.s0) : pk;
+        const uint64_t slot = (a.which & KFEC_PACK_COMPACT) ? pk : g * a.N + s;
         const uint32_t H = red ? KFEC_PKT_REDUNDANT_HEADER : KFEC_PKT_DATA_HEADER;
         const uint32_t n = red ? a.align[g] : a.len[g * a.K + s];
         const bool fits = H + n <= a.pkt_pitch && !(red && n == 0);
@@ -324,9 +324,16 @@ struct FramedArgs {
     const uint32_t *etab;   // [K][etab_rows][5] perm tables (kfec_internal.hpp enc_tab_*)
     uint64_t pitch;
     uint32_t total, cols, K, R, B, etab_rows, gmax;
+    // data packets (framed_encode_kernel<MT, true>): pkt[g][N][pkt_pitch], pkt_len[g][N], as kfec_pack_batch
+    uint8_t *pkt;
+    uint16_t *pkt_len;
+    const uint32_t *sn;
+    uint64_t pkt_pitch;
+    uint32_t N, timestamp;
 };
 
-// 32 bytes [q0, q0 + 32) of the payload base[start, start + len) as 8 dwords, zero outside it (q0 >= -3).
+// 32 bytes [q0, q0 + 32) of the payload base[start, start + len) as 8 dwords, zero outside it (q0 > -32;
+// a window reaching below the arena's start reads those dwords as zero).
 // Nine dword-aligned dwords (two 16-byte loads and one dword; per-dword guarded loads only where the window
 // touches the ends of the arena) re-based by v_alignbyte_b32, then masked without branches: the window's
 // valid bytes form one 32-bit mask M (bit k = byte k), and dword i's byte mask is its nibble of M spread to
@@ -340,21 +347,21 @@ __device__ __forceinline__ void payload_window(const uint32_t *base32, uint64_t 
         for (int i = 0; i < 8; ++i) o[i] = 0u;
         return;
     }
-    const uint64_t a4 = start + (uint64_t)(int64_t)(q0 + 4);  // first byte's address + 4 (q0 >= -3)
-    const uint64_t w1 = a4 >> 2;                               // its dword index + 1
-    const uint32_t sh = (uint32_t)(a4 & 3u);
+    const int64_t ab = (int64_t)start + q0;  // the window's first byte (below the arena for a header window)
+    const int64_t w0 = ab >> 2;               // its dword (floor)
+    const uint32_t sh = (uint32_t)(ab & 3);
     uint32_t d[9];
-    if (w1 >= 1 && w1 + 8 <= lim32) {
-        const uint4 p = *reinterpret_cast<const uint4 *>(base32 + (w1 - 1));
-        const uint4 q = *reinterpret_cast<const uint4 *>(base32 + (w1 + 3));
+    if (w0 >= 0 && w0 + 9 <= (int64_t)lim32) {
+        const uint4 p = *reinterpret_cast<const uint4 *>(base32 + w0);
+        const uint4 q = *reinterpret_cast<const uint4 *>(base32 + w0 + 4);
         d[0] = p.x; d[1] = p.y; d[2] = p.z; d[3] = p.w;
         d[4] = q.x; d[5] = q.y; d[6] = q.z; d[7] = q.w;
-        d[8] = base32[w1 + 7];
+        d[8] = base32[w0 + 8];
     } else {
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            const uint64_t w = w1 - 1 + i;  // may wrap below zero: then >= lim32 and read as 0
-            d[i] = (w1 + i >= 1 && w < lim32) ? base32[w] : 0u;
+            const int64_t w = w0 + i;
+            d[i] = (w >= 0 && w < (int64_t)lim32) ? base32[w] : 0u;
         }
     }
     const uint32_t mhi = hi >= 32 ? 0xFFFFFFFFu : (1u << hi) - 1u;
@@ -375,12 +382,48 @@ __device__ __forceinline__ void framed_gran(const uint32_t *src, uint64_t lim, u
     if (col == 0) x[0] |= (n >> 8) | ((n & 0xFFu) << 8);  // htons(length)
 }
 
-template <int MT>
+// create_fec_data_packet (connections.cpp:395-411) for datagram j of group g, by the lanes of its columns:
+// lane `col` writes the 16-byte-aligned packet bytes [32 cc, 32 cc + 32) for cc = col, col + cols, ... below
+// the packet's length (windows past the framed columns exist only for a datagram too long for B), re-read
+// from the arena -- the lines the MAC just loaded -- and lane 0 adds the 9-byte header.  Same bytes and
+// lengths as pack_kernel's data packets.
+__device__ __forceinline__ void data_packet(const FramedArgs &a, uint64_t g, uint32_t j, uint32_t col, uint64_t off,
+                                            uint32_t n)
+{
+    const uint32_t plen = KFEC_PKT_DATA_HEADER + n, nd = (plen + 3) / 4;
+    uint32_t *dst = reinterpret_cast<uint32_t *>(a.pkt + (g * a.N + j) * a.pkt_pitch);
+    const bool fits = plen <= a.pkt_pitch;
+    if (col == 0) a.pkt_len[g * a.N + j] = fits ? (uint16_t)plen : (uint16_t)0;
+    if (!fits) return;
+    for (uint32_t cc = col; 32 * cc < plen; cc += a.cols) {
+        uint32_t w[8];
+        // packet byte q holds datagram byte q - 9: the window starts 9 bytes before the datagram for cc = 0
+        payload_window(a.src, a.src_dw, off, n, (int32_t)(32 * cc) - (int32_t)KFEC_PKT_DATA_HEADER, w);
+        if (cc == 0) {
+            w[0] = a.timestamp;                 // host_to_little_endian
+            w[1] = __builtin_bswap32(a.sn[g]);  // htonl
+            w[2] |= j;                          // sub_sn
+        }
+        const uint32_t d0 = 8 * cc;
+        if (d0 + 8 <= nd) {
+            typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(u32x4_t{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4_t *>(dst + d0));
+            __builtin_nontemporal_store(u32x4_t{w[4], w[5], w[6], w[7]}, reinterpret_cast<u32x4_t *>(dst + d0 + 4));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (d0 + i < nd) dst[d0 + i] = w[i];
+        }
+    }
+}
+
+template <int MT, bool DPK = false>
 __global__ void __launch_bounds__(256) framed_encode_kernel(FramedArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_raw[];
     uint64_t *s_off = reinterpret_cast<uint64_t *>(s_raw);
-    uint32_t *s_len = reinterpret_cast<uint32_t *>(s_raw + (size_t)a.gmax * a.K * 8);  // 0xFFFFFFFF: zero slot
+    // s_len: the datagram's length, bit 31 set when its group's slots read as zeros (a datagram too long for B)
+    uint32_t *s_len = reinterpret_cast<uint32_t *>(s_raw + (size_t)a.gmax * a.K * 8);
     const uint32_t K = a.K, cols = a.cols;
     const uint32_t base = blockIdx.x * 256u, item = base + threadIdx.x;
     const uint32_t gfirst = base / cols, glast = min(base + 255u, a.total - 1) / cols, ng = glast - gfirst + 1;
@@ -388,8 +431,8 @@ __global__ void __launch_bounds__(256) framed_encode_kernel(FramedArgs a)
         const uint32_t gs = e / K, j = e - gs * K;
         const uint64_t gj = (uint64_t)(gfirst + gs) * K + j;
         const bool ok = a.align[gfirst + gs] != 0;
-        s_off[e] = ok ? a.off[gj] : 0;
-        s_len[e] = ok ? (uint32_t)a.len[gj] : 0xFFFFFFFFu;
+        s_off[e] = a.off[gj];
+        s_len[e] = (uint32_t)a.len[gj] | (ok ? 0u : 0x80000000u);
     }
     __syncthreads();
     const uint32_t row0 = blockIdx.y * MT;
@@ -403,7 +446,7 @@ __global__ void __launch_bounds__(256) framed_encode_kernel(FramedArgs a)
         for (int w = 0; w < 8; ++w) acc[r][w] = 0;
     auto load = [&](uint32_t j, uint32_t (&x)[8]) {
         const uint32_t n = s_len[gs * K + j];
-        if (n == 0xFFFFFFFFu) {
+        if (n & 0x80000000u) {
 #pragma unroll
             for (int w = 0; w < 8; ++w) x[w] = 0;
         } else {
@@ -430,6 +473,9 @@ __global__ void __launch_bounds__(256) framed_encode_kernel(FramedArgs a)
             const uint32_t s0 = xv & 0x07070707u, s1 = (xv >> 3) & 0x07070707u, s2 = (xv >> 6) & 0x03030303u;
 #pragma unroll
             for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+        }
+        if constexpr (DPK) {
+            if (blockIdx.y == 0) data_packet(a, g, jj, col, s_off[gs * K + jj], s_len[gs * K + jj] & 0xFFFFu);
         }
     };
     for (uint32_t j = 0; j < K; j += 2) {
@@ -598,7 +644,7 @@ int launched() { return hipGetLastError() == hipSuccess ? 0 : -3; }
 // 0 on success, 1 when the fused kernel does not apply (the caller frames, then encodes), -3 on a HIP error
 int launch_framed_encode(const uint8_t *d_enc, int K, int N, size_t G, const void *src, size_t src_bytes,
                          const uint64_t *off, const uint16_t *len, size_t B, size_t pitch, void *parity,
-                         uint16_t *align, hipStream_t s)
+                         uint16_t *align, hipStream_t s, const DataPackets *dp)
 {
     const int R = N - K;
     if (G == 0) return 0;
@@ -627,6 +673,22 @@ int launch_framed_encode(const uint8_t *d_enc, int K, int N, size_t G, const voi
     a.etab_rows = (uint32_t)enc_tab_rows(R);
     a.gmax = gmax;
     const dim3 grid((a.total + 255) / 256, (R + mt - 1) / mt);
+    if (dp) {
+        a.pkt = static_cast<uint8_t *>(dp->pkt);
+        a.pkt_len = dp->pkt_len;
+        a.sn = dp->sn;
+        a.pkt_pitch = dp->pkt_pitch;
+        a.N = N;
+        a.timestamp = dp->timestamp;
+        switch (mt) {
+        case 1: hipLaunchKernelGGL((framed_encode_kernel<1, true>), grid, dim3(256), lds, s, a); break;
+        case 2: hipLaunchKernelGGL((framed_encode_kernel<2, true>), grid, dim3(256), lds, s, a); break;
+        case 3: hipLaunchKernelGGL((framed_encode_kernel<3, true>), grid, dim3(256), lds, s, a); break;
+        case 4: hipLaunchKernelGGL((framed_encode_kernel<4, true>), grid, dim3(256), lds, s, a); break;
+        default: hipLaunchKernelGGL((framed_encode_kernel<8, true>), grid, dim3(256), lds, s, a); break;
+        }
+        return launched();
+    }
     switch (mt) {
     case 1: hipLaunchKernelGGL(framed_encode_kernel<1>, grid, dim3(256), lds, s, a); break;
     case 2: hipLaunchKernelGGL(framed_encode_kernel<2>, grid, dim3(256), lds, s, a); break;
@@ -753,7 +815,8 @@ int launch_pack(int K, int N, size_t G, unsigned which, const void *src, size_t 
     a.timestamp = timestamp;
     a.nsel = ((which & KFEC_PACK_DATA) ? K : 0) + ((which & KFEC_PACK_REDUNDANT) ? N - K : 0);
     a.s0 = (which & KFEC_PACK_DATA) ? 0 : K;
-    a.rows = (uint64_t)G * N;
+    a.rows = (uint64_t)G * a.nsel;
+    if (a.rows == 0) return 0;
     hipLaunchKernelGGL(pack_kernel, dim3(grid_rows(a.rows)), dim3(kFrameBlock), 0, s, a);
     return launched();
 }

@@ -69,9 +69,17 @@ int launch_unpack(int K, size_t P, const void *src, const uint64_t *off, const u
                   hipStream_t s);
 int launch_scatter(int N, size_t P, const kfec_pkt_hdr *hdr, const int32_t *slot, uint32_t sn_base, size_t G,
                    uint64_t *present, uint64_t *off, uint16_t *len, hipStream_t s);
+// data packets written by the fused encode (kfec_encode_pack_batch): [G][N][pkt_pitch] as kfec_pack_batch
+struct DataPackets {
+    void *pkt;
+    uint16_t *pkt_len;
+    const uint32_t *sn;
+    size_t pkt_pitch;
+    uint32_t timestamp;
+};
 int launch_framed_encode(const uint8_t *d_enc, int K, int N, size_t G, const void *src, size_t src_bytes,
                          const uint64_t *off, const uint16_t *len, size_t B, size_t pitch, void *parity,
-                         uint16_t *align, hipStream_t s);
+                         uint16_t *align, hipStream_t s, const DataPackets *dp = nullptr);
 // packet integrity (kfec_seal.hip)
 int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
                 const uint32_t *len, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok, hipStream_t s);

@@ -82,6 +82,8 @@ def load_library():
         # include/kfec_frame.h
         "kfec_frame_data_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, sz, sz, _vp, _vp, _vp]),
         "kfec_encode_framed_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, sz, sz, _vp, _vp, _vp]),
+        "kfec_encode_pack_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, sz, sz, _vp, _vp, _vp, _vp, C.c_uint32, _vp,
+                                             sz, _vp, _vp]),
         "kfec_frame_shards_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, _vp, sz, sz, _vp, _vp, _vp, _vp]),
         "kfec_decode_framed_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, _vp, sz, sz, _vp, _vp, _vp, _vp, _vp,
                                                _vp]),

@@ -78,6 +78,17 @@ class FecFrame:
                                                   _dptr(length), B, pitch, _dptr(parity), _dptr(align),
                                                   _stream_handle(stream)), "kfec_encode_framed_batch")
 
+    def encode_pack(self, src, off, length, parity, align, sn, conv, timestamp: int, pkt, pkt_len, B: int,
+                    stream=None) -> None:
+        """encode_framed + pack(DATA | REDUNDANT) with the data packets written by the encoder: pkt [G][N][pitch],
+        pkt_len int16 [G][N], parity [G][R][pitch], align [G] (all written)."""
+        G, r, pitch = parity.shape
+        assert off.numel() == G * self.K and align.numel() == G and pkt.shape[:2] == (G, self.N)
+        _check(self._lib.kfec_encode_pack_batch(self.code._ctx, G, _dptr(src), src.numel(), _dptr(off), _dptr(length),
+                                                B, pitch, _dptr(parity), _dptr(align), _dptr(sn), _dptr(conv),
+                                                timestamp & 0xFFFFFFFF, _dptr(pkt), pkt.shape[-1], _dptr(pkt_len),
+                                                _stream_handle(stream)), "kfec_encode_pack_batch")
+
     def frame_shards(self, src, off, length, present, data, parity, align, B: int, stream=None) -> None:
         """Receive side: off/length [G*N] shard table, present int64 [G][4]; writes the present slots of
         data [G][K][pitch] / parity [G][R][pitch] and align [G]."""

@@ -571,3 +571,50 @@ def test_decode_framed_recovers_datagrams(dev, oracle, K, N, B):
         assert got == lost[g], g
         n += len(got)
     assert n > G // 3
+
+
+@pytest.mark.parametrize("K,N,B,pitch,pkt_pitch", [(20, 23, 1442, 1444, 1456), (10, 13, 1402, 1404, 1416),
+                                                   (4, 6, 40, 64, 44), (3, 5, 7, 8, 24), (200, 255, 1442, 1444, 1456)])
+def test_encode_pack_matches_two_step(dev, K, N, B, pitch, pkt_pitch):
+    """kfec_encode_pack_batch (data packets written by the encoder) == kfec_encode_framed_batch +
+    kfec_pack_batch(DATA | REDUNDANT), byte for byte over the whole packet array: ragged datagrams, a group
+    with a datagram too long for B (its data packets still go out, longer than the framed columns), packets
+    that do not fit pkt_pitch (length 0, nothing written)."""
+    c, fr = _coder(K, N)
+    R = N - K
+    rng = random.Random(K * 13 + B + pkt_pitch)
+    G = 19 if K < 100 else 3
+    dgs = []
+    for g in range(G):
+        for i in range(K):
+            n = rng.choice([0, 1, B - 2, rng.randint(0, B - 2)])
+            if g == 1 and i == 2 and B > 3:
+                n = B - 1 if K < 100 else B + 5  # too long: align 0 (and, at 200:255, past the framed columns)
+            dgs.append(rng.randbytes(n))
+    src, off, lens = _arena(dgs, dev)
+    d_len = _i16(lens, dev)
+    sn = torch.tensor(np.asarray([rng.getrandbits(32) for _ in range(G)], np.uint32).view(np.int32), device=dev)
+    conv = torch.tensor(np.asarray([rng.getrandbits(32) for _ in range(G)], np.uint32).view(np.int32), device=dev)
+    ts = 0x01234567
+
+    def run(fused):
+        par = torch.full((G, R, pitch), SENT, dtype=torch.uint8, device=dev)
+        al = torch.zeros(G, dtype=torch.int16, device=dev)
+        pkt = torch.full((G, N, pkt_pitch), SENT, dtype=torch.uint8, device=dev)
+        pl = torch.full((G, N), -1, dtype=torch.int16, device=dev)
+        if fused:
+            fr.encode_pack(src, off, d_len, par, al, sn, conv, ts, pkt, pl, B)
+        else:
+            fr.encode_framed(src, off, d_len, par, al, B)
+            fr.pack(src, off, d_len, par, al, sn, conv, ts, pkt, pl)
+        torch.cuda.synchronize()
+        return par.cpu().numpy(), _u16(al), pkt.cpu().numpy(), _u16(pl)
+
+    p1, a1, k1, l1 = run(True)
+    p2, a2, k2, l2 = run(False)
+    assert np.array_equal(a1, a2)
+    assert np.array_equal(l1, l2)
+    assert np.array_equal(k1, k2)
+    B4 = (B + 3) // 4 * 4
+    assert np.array_equal(p1[:, :, :B4], p2[:, :, :B4])
+    assert (l1[:, :K] > 0).sum() > G * K // 2 and (l1 == 0).sum() > 0

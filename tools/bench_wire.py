@@ -4,7 +4,8 @@
     python tools/bench_wire.py [--groups G] [--steps K] [--ragged]
 
 fec=20:3, kcp_mtu=1440.  Send step: frame_data -> encode_batch -> pack (data + redundant packets), and the
-fused form encode_framed (frame + encode in one kernel, checked equal) -> pack.
+fused form encode_framed (frame + encode in one kernel, checked equal) -> pack, and encode_pack (the encoder
+also writes the data packets; then the redundant ones: two launches, checked equal).
 Receive step (every group lost 3 data packets, worst case): unpack -> scatter -> frame_shards -> decode_batch
 -> unframe, and the fused form unpack -> scatter -> decode_framed (frame_shards + decode in one kernel, checked
 equal) -> unframe.  Datagrams are 1440 B (bulk traffic) or, with --ragged, uniform 0..1440 B.  Prints one JSON line:
@@ -83,10 +84,12 @@ def main():
     align2 = torch.empty_like(align)
     out2, idx2, st2, ralign2 = torch.empty_like(out), torch.empty_like(idx), torch.empty_like(st), torch.empty_like(ralign)
     ws2 = c.decode_workspace(G)
+    parity3, align3 = torch.empty_like(parity), torch.empty_like(align)
+    pkt3, plen3 = torch.empty_like(pkt), torch.empty_like(plen)
 
     s = torch.cuda.current_stream()
     names = ["frame_data", "encode", "pack", "unpack", "scatter", "frame_shards", "decode", "unframe", "encode_framed",
-             "decode_framed"]
+             "decode_framed", "encode_pack"]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
     times = {n: [] for n in names}
 
@@ -124,6 +127,10 @@ def main():
         fr.decode_framed(flat, toff, tlen, present, out2, idx2, st2, ralign2, ws2, B)  # fused frame_shards + decode
         if timed:
             ev[10].record(s)
+        # the whole send side in two launches: framed encode writing the data packets, then the redundant ones
+        fr.encode_pack(arena, off, d_len, parity3, align3, sn, conv, 77, pkt3, plen3, B)
+        if timed:
+            ev[11].record(s)
 
     # received packet lengths (what recvmmsg reports) -- identical every step, so taken once up front
     fr.frame_data(arena, off, d_len, data, align, B)
@@ -172,15 +179,23 @@ def main():
         "unframe": lost_bytes * 2,
         "encode_framed": payload + G * R * B,
         "decode_framed": (kept_pkt_bytes - P * 9 - G * R * 4) + G * R * B,
+        "encode_pack": payload + G * R * B * 2 + pkt_bytes,
     }
     send_ms = med["frame_data"] + med["encode"] + med["pack"]
     send_fused_ms = med["encode_framed"] + med["pack"]
     recv_ms = sum(med[n] for n in names[3:8])
     recv_fused_ms = med["unpack"] + med["scatter"] + med["decode_framed"] + med["unframe"]
+    send_fused2_ms = med["encode_pack"]
     ok = ok and torch.equal(parity2, parity) and torch.equal(align2, align)
     ok = ok and torch.equal(idx2, idx) and torch.equal(st2, st) and torch.equal(ralign2, ralign)
     B4 = (B + 3) // 4 * 4
     ok = ok and torch.equal(out2[:, :, :B4], out[:, :, :B4])
+    ok = ok and torch.equal(plen3, plen) and torch.equal(align3, align)
+    pk_np, pk3_np, pl_np = pkt.cpu().numpy(), pkt3.cpu().numpy(), plen.cpu().numpy().view(np.uint16)
+    for g in range(min(G, 256)):  # packet bytes below each packet's length (the rest of the row is scratch)
+        for s_ in range(N):
+            n_ = int(pl_np[g, s_])
+            ok = ok and np.array_equal(pk_np[g, s_, :n_], pk3_np[g, s_, :n_])
     res = {
         "metric": "FEC wire path payload GiB/s (device-resident, packet-in/packet-out), fec=20:3 kcp_mtu=1440",
         "groups": G, "ragged": args.ragged, "steps": args.steps,
@@ -188,6 +203,8 @@ def main():
         "recv_GiBps": round(payload / (recv_ms * 1e-3) / 2**30, 2),
         "send_fused_GiBps": round(payload / (send_fused_ms * 1e-3) / 2**30, 2),
         "recv_fused_GiBps": round(payload / (recv_fused_ms * 1e-3) / 2**30, 2),
+        "send_encode_pack_GiBps": round(payload / (send_fused2_ms * 1e-3) / 2**30, 2),
+        "send_encode_pack_ms": round(send_fused2_ms, 4),
         "recv_fused_ms": round(recv_fused_ms, 4),
         "send_ms": round(send_ms, 4), "send_fused_ms": round(send_fused_ms, 4), "recv_ms": round(recv_ms, 4),
         "kernels": {n: {"ms": round(med[n], 4), "alg_GBps": round(alg[n] / (med[n] * 1e-3) / 1e9, 1)} for n in names},
