@@ -164,14 +164,19 @@ int kfec_group_scatter(const kfec_ctx *ctx, size_t P, const kfec_pkt_hdr *d_hdr,
 /* Seal P packets [d_off[p], +d_len[p]) of d_src into d_dst + p * dst_pitch (dst_pitch % 4 == 0):
  * data || checksum16(data), xor_forward'ed for plain_xor.  d_out_len[p] = len + 2, or 0 for an empty packet
  * (encrypt_data returns "empty data") or one that does not fit in dst_pitch.  Bytes after the sealed packet
- * up to the next multiple of 4 are written as zero. */
+ * up to the next multiple of 4 are written as zero.
+ * d_dst == NULL seals in place (checksum mode only): the two checksum bytes are written right after each
+ * packet in d_src (the caller leaves them room, e.g. pkt_pitch >= packet + 2 after kfec_pack_batch) and
+ * nothing else is written -- the CRC reads each packet once. */
 int kfec_seal_batch(int mode, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
                     const uint32_t *d_len, void *d_dst, size_t dst_pitch, uint32_t *d_out_len, void *stream);
 
 /* Open P sealed packets: (plain_xor: xor_backward, then) split off the 2-byte trailer and compare it with
  * checksum16 of the rest.  d_dst + p * dst_pitch receives the len - 2 plaintext bytes (zero-padded to a
  * multiple of 4), d_out_len[p] = len - 2 and d_ok[p] = 1 when the checksum matches, 0 when it does not
- * (decrypt_data's "checksum incorrect"); packets of <= 2 bytes get d_out_len = 0, d_ok = 0. */
+ * (decrypt_data's "checksum incorrect"); packets of <= 2 bytes get d_out_len = 0, d_ok = 0.
+ * d_dst == NULL opens in place (checksum mode only): the plaintext is the packet's first len - 2 bytes where
+ * it lies; only d_out_len and d_ok are written. */
 int kfec_open_batch(int mode, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
                     const uint32_t *d_len, void *d_dst, size_t dst_pitch, uint32_t *d_out_len, uint8_t *d_ok,
                     void *stream);

@@ -531,7 +531,8 @@ int kfec_seal_batch(int mode, size_t P, const void *d_src, size_t src_bytes, con
                     const uint32_t *d_len, void *d_dst, size_t dst_pitch, uint32_t *d_out_len, void *stream)
 {
     if ((mode != KFEC_SEAL_CHECKSUM && mode != KFEC_SEAL_PLAIN_XOR) || dst_pitch % 4) return KFEC_EINVAL;
-    if (P && (!d_src || !al4(d_src) || !d_off || !d_len || !d_dst || !al4(d_dst) || !d_out_len)) return KFEC_EINVAL;
+    if (!d_dst && mode != KFEC_SEAL_CHECKSUM) return KFEC_EINVAL;  // in place: checksum mode only
+    if (P && (!d_src || !al4(d_src) || !d_off || !d_len || (d_dst && !al4(d_dst)) || !d_out_len)) return KFEC_EINVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return KFEC_ENODEV;
     return kfec::launch_seal(false, mode, P, d_src, src_bytes, d_off, d_len, d_dst, dst_pitch, d_out_len, nullptr,
@@ -545,7 +546,8 @@ int kfec_open_batch(int mode, size_t P, const void *d_src, size_t src_bytes, con
                     void *stream)
 {
     if ((mode != KFEC_SEAL_CHECKSUM && mode != KFEC_SEAL_PLAIN_XOR) || dst_pitch % 4) return KFEC_EINVAL;
-    if (P && (!d_src || !al4(d_src) || !d_off || !d_len || !d_dst || !al4(d_dst) || !d_out_len || !d_ok))
+    if (!d_dst && mode != KFEC_SEAL_CHECKSUM) return KFEC_EINVAL;  // in place: checksum mode only
+    if (P && (!d_src || !al4(d_src) || !d_off || !d_len || (d_dst && !al4(d_dst)) || !d_out_len || !d_ok))
         return KFEC_EINVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return KFEC_ENODEV;

@@ -386,6 +386,43 @@ __global__ void __launch_bounds__(kSealBlock) open_kernel(SealArgs a)
     }
 }
 
+// Checksum mode in place (kfec_seal_batch / kfec_open_batch with d_dst == NULL): the packets stay where they
+// are; seal appends the two checksum bytes after each packet, open verifies the trailer.  The CRC reads the
+// packet once and nothing else moves (separate kernels: a per-packet in-place test inside seal_kernel cost
+// its out-of-place path 24%).
+__global__ void __launch_bounds__(kSealBlock) seal_in_place_kernel(SealArgs a, bool open)
+{
+    __shared__ uint32_t s_tab[kCrcMaps][4][256];
+    stage_tables(a.tab, s_tab);
+    const uint32_t lane = threadIdx.x % kRowLanes;
+    uint8_t *base = const_cast<uint8_t *>(reinterpret_cast<const uint8_t *>(a.src));
+    for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRowLanes; p < a.P;
+         p += (uint64_t)gridDim.x * kRowsPerBlock) {
+        const uint32_t L = a.len[p];
+        const uint64_t off = a.off[p];
+        if (open ? L <= KFEC_SEAL_TRAILER : L == 0) {  // decrypt_data: bad length / encrypt_data: empty data
+            if (lane == 0) {
+                a.out_len[p] = 0;
+                if (open) a.ok[p] = 0;
+            }
+            continue;
+        }
+        const uint32_t n = open ? L - KFEC_SEAL_TRAILER : L;  // bytes under the checksum
+        const uint32_t cs = checksum16(row_crc32(s_tab, a.src, a.src_dw, off, n, lane));
+        if (lane == 0) {
+            uint8_t *t = base + off + n;
+            if (open) {
+                a.ok[p] = cs == ((uint32_t)t[0] | ((uint32_t)t[1] << 8));
+                a.out_len[p] = n;
+            } else {
+                t[0] = (uint8_t)cs;
+                t[1] = (uint8_t)(cs >> 8);
+                a.out_len[p] = L + KFEC_SEAL_TRAILER;
+            }
+        }
+    }
+}
+
 uint32_t *crc_tables(hipStream_t s)
 {
     static std::mutex mu;
@@ -432,7 +469,8 @@ int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes
     // 28 KiB of tables per 512-thread workgroup: 4 resident per CU; each loops over rows of 16 packets
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
     const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * 4));
-    if (open) hipLaunchKernelGGL(open_kernel, grid, dim3(kSealBlock), 0, s, a);
+    if (!dst) hipLaunchKernelGGL(seal_in_place_kernel, grid, dim3(kSealBlock), 0, s, a, open);  // checksum mode
+    else if (open) hipLaunchKernelGGL(open_kernel, grid, dim3(kSealBlock), 0, s, a);
     else hipLaunchKernelGGL(seal_kernel, grid, dim3(kSealBlock), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -145,15 +145,18 @@ class FecFrame:
 
 def seal(mode: int, src, off, length, dst, out_len, stream=None) -> None:
     """encrypt_data (none / plain_xor) for P packets [off[p], off[p] + length[p]) of src (length int32 [P]):
-    dst [P][dst_pitch] receives data || checksum16 (xor_forward'ed for plain_xor), out_len int32 [P]."""
+    dst [P][dst_pitch] receives data || checksum16 (xor_forward'ed for plain_xor), out_len int32 [P].
+    dst None: checksum mode in place (the 2 checksum bytes go right after each packet in src)."""
     P = off.numel()
     _check(load_library().kfec_seal_batch(mode, P, _dptr(src), src.numel(), _dptr(off), _dptr(length), _dptr(dst),
-                                          dst.shape[-1], _dptr(out_len), _stream_handle(stream)), "kfec_seal_batch")
+                                          dst.shape[-1] if dst is not None else 0, _dptr(out_len),
+                                          _stream_handle(stream)), "kfec_seal_batch")
 
 
 def open_(mode: int, src, off, length, dst, out_len, ok, stream=None) -> None:
-    """decrypt_data (none / plain_xor): plaintext to dst [P][dst_pitch], out_len int32 [P], ok uint8 [P]."""
+    """decrypt_data (none / plain_xor): plaintext to dst [P][dst_pitch], out_len int32 [P], ok uint8 [P].
+    dst None: checksum mode in place (only out_len / ok are written)."""
     P = off.numel()
     _check(load_library().kfec_open_batch(mode, P, _dptr(src), src.numel(), _dptr(off), _dptr(length), _dptr(dst),
-                                          dst.shape[-1], _dptr(out_len), _dptr(ok), _stream_handle(stream)),
-           "kfec_open_batch")
+                                          dst.shape[-1] if dst is not None else 0, _dptr(out_len), _dptr(ok),
+                                          _stream_handle(stream)), "kfec_open_batch")

@@ -618,3 +618,55 @@ def test_encode_pack_matches_two_step(dev, K, N, B, pitch, pkt_pitch):
     B4 = (B + 3) // 4 * 4
     assert np.array_equal(p1[:, :, :B4], p2[:, :, :B4])
     assert (l1[:, :K] > 0).sum() > G * K // 2 and (l1 == 0).sum() > 0
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_seal_open_in_place(dev, mode):
+    """Checksum mode in place (d_dst NULL, e.g. straight after kfec_pack_batch): the 2 checksum bytes land right
+    after each packet and nothing else changes, with the lengths of the out-of-place call; opening in place
+    gives its lengths and verdicts.  plain_xor in place is refused (KFEC_EINVAL)."""
+    from kcptube_amd.fec import KfecError
+    from kcptube_amd.frame import open_, seal
+    rng = random.Random(300 + mode)
+    pitch = 1472
+    lens = [1, 2, 3, 4, 5, 1449, 1450, 1451, 1452] + [rng.randint(1, 1460) for _ in range(300)]
+    P = len(lens)
+    rows = np.zeros((P, pitch), np.uint8)
+    for p, n in enumerate(lens):
+        rows[p, :n] = np.frombuffer(rng.randbytes(n), np.uint8)
+    buf = torch.tensor(rows, device=dev)
+    # packets at odd offsets inside the rows (in place needs no alignment)
+    off = torch.arange(P, dtype=torch.int64, device=dev) * pitch
+    d_len = torch.tensor(lens, dtype=torch.int32, device=dev)
+    flat = buf.view(-1)
+    if mode == 1:
+        with pytest.raises(KfecError):
+            seal(mode, flat, off, d_len, None, torch.empty(P, dtype=torch.int32, device=dev))
+        return
+    ref = torch.full((P, pitch), SENT, dtype=torch.uint8, device=dev)
+    rl = torch.full((P,), -1, dtype=torch.int32, device=dev)
+    seal(mode, flat, off, d_len, ref, rl)
+    il = torch.full((P,), -1, dtype=torch.int32, device=dev)
+    seal(mode, flat, off, d_len, None, il)  # in place
+    torch.cuda.synchronize()
+    assert torch.equal(rl, il)
+    r_np, b_np, n_np = ref.cpu().numpy(), buf.cpu().numpy(), rl.cpu().numpy()
+    for p in range(P):
+        n = int(n_np[p])
+        assert np.array_equal(r_np[p, :n], b_np[p, :n]), p
+        assert not b_np[p, n:].any()  # nothing beyond the trailer was written
+    # open in place, a quarter of the packets corrupted first
+    for p in range(0, P, 4):
+        b_np[p, rng.randrange(int(n_np[p]))] ^= 0x10
+    buf2 = torch.tensor(b_np, device=dev)
+    flat2 = buf2.view(-1)
+    sl = torch.tensor(n_np, dtype=torch.int32, device=dev)
+    ref2 = torch.full((P, pitch), SENT, dtype=torch.uint8, device=dev)
+    ol, ok = torch.full((P,), -1, dtype=torch.int32, device=dev), torch.full((P,), 7, dtype=torch.uint8, device=dev)
+    open_(mode, flat2, off, sl, ref2, ol, ok)
+    ol2, ok2 = torch.full((P,), -1, dtype=torch.int32, device=dev), torch.full((P,), 7, dtype=torch.uint8, device=dev)
+    open_(mode, flat2, off, sl, None, ol2, ok2)  # in place
+    torch.cuda.synchronize()
+    assert torch.equal(ol, ol2) and torch.equal(ok, ok2)
+    assert int((ok.cpu().numpy() == 0).sum()) >= P // 4 - 2
+    assert np.array_equal(buf2.cpu().numpy(), b_np)  # opening in place writes nothing into the packets

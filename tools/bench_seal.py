@@ -4,8 +4,9 @@
     python tools/bench_seal.py [--packets P] [--len L] [--steps K]
 
 P packets of L bytes (default 4M x 1449 B = the 20:3 wire's data packets at kcp_mtu 1440) sealed and opened
-in both non-AEAD modes.  Prints one JSON line: per mode, kernel ms (HIP events, median) and algorithmic
-HBM GB/s (read L + write L + 2 per packet).  Opened packets are checked (all checksums good, bytes equal).
+in both non-AEAD modes, and in place in checksum mode.  Prints one JSON line: per mode, kernel ms (HIP
+events, median) and algorithmic HBM GB/s (read L + write L + 2 per packet; in place: read L, write the
+trailer dword).  Opened packets are checked (all checksums good, bytes equal).
 """
 from __future__ import annotations
 
@@ -61,6 +62,26 @@ def main():
         res[name] = {"seal_ms": round(float(np.median(ts)), 4), "open_ms": round(float(np.median(to)), 4),
                      "seal_GBps": round(byt / (np.median(ts) * 1e-3) / 1e9, 1),
                      "open_GBps": round(byt / (np.median(to) * 1e-3) / 1e9, 1)}
+    # in place, checksum mode (d_dst NULL, as after kfec_pack_batch): the CRC reads the packet, seal writes the
+    # 2 trailer bytes, open writes nothing (algorithmic bytes: read L + 2 per packet, write 2 on seal)
+    work = src.clone()
+    wflat = work.view(-1)
+    ti, tio = [], []
+    for i in range(args.steps + 2):
+        e[0].record(s)
+        seal(SEAL_CHECKSUM, wflat, off, ln, None, slen)
+        e[1].record(s)
+        open_(SEAL_CHECKSUM, wflat, off, slen, None, plen, ok)
+        e[2].record(s)
+        torch.cuda.synchronize()
+        if i >= 2:
+            ti.append(e[0].elapsed_time(e[1]))
+            tio.append(e[1].elapsed_time(e[2]))
+    good = good and bool(ok.all().item()) and bool((plen == L).all().item())
+    good = good and torch.equal(work.view(P, pitch)[:, :L], src.view(P, pitch)[:, :L])
+    res["none_in_place"] = {"seal_ms": round(float(np.median(ti)), 4), "open_ms": round(float(np.median(tio)), 4),
+                            "seal_GBps": round(P * (L + 2) / (np.median(ti) * 1e-3) / 1e9, 1),
+                            "open_GBps": round(P * (L + 2) / (np.median(tio) * 1e-3) / 1e9, 1)}
     res["verified"] = good
     print(json.dumps(res), flush=True)
     if not good:
