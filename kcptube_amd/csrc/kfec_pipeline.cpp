@@ -8,7 +8,6 @@
 
 #include <algorithm>
 #include <cstring>
-#include <map>
 #include <memory>
 #include <new>
 #include <vector>
@@ -396,7 +395,10 @@ struct RxGroup {
 struct kfec_rx {
     kfec_rxq *q = nullptr;
     uint64_t tag = 0;
-    std::map<uint32_t, RxGroup *> cache;  // fec_rcv_cache + fec_rcv_restored
+    // fec_rcv_cache + fec_rcv_restored as a flat (sn, group) list: it holds the few groups within gbv_fec_waits
+    // of the newest sn, and every push scans all of it anyway (fec_find_missings), so a linear find beats the
+    // map; order is irrelevant because a push can complete only its own group
+    std::vector<std::pair<uint32_t, RxGroup *>> cache;
     std::vector<std::unique_ptr<RxGroup>> pool;
     std::vector<RxGroup *> free_groups;
     RxGroup *get()
@@ -525,7 +527,7 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
     const size_t plen = len - H;
     if (plen + (red ? 0 : KFEC_FEC_CONTAINER_HEADER) > q->max_shard) return KFEC_EINVAL;
     const uint32_t fec_sn = get_be32(pkt + 4);
-    auto found = rx->cache.find(fec_sn);
+    auto found = std::find_if(rx->cache.begin(), rx->cache.end(), [&](const auto &kv) { return kv.first == fec_sn; });
     // capacity: only this packet's group can become decodable on this push (every other cached group either
     // reached K shares on an earlier push, and was queued and restored then, or still lacks shares)
     const bool fresh = found == rx->cache.end();
@@ -539,7 +541,13 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
         if (rc) return rc;
     }
     // fec_rcv_cache[sn][sub_sn] = ... (client.cpp:869,887): a duplicate overwrites
-    RxGroup *grp = found != rx->cache.end() ? found->second : (rx->cache[fec_sn] = rx->get());
+    RxGroup *grp;
+    if (found != rx->cache.end()) {
+        grp = found->second;
+    } else {
+        grp = rx->get();
+        rx->cache.emplace_back(fec_sn, grp);
+    }
     if (!grp->test(sub)) {
         grp->has[sub >> 6] |= 1ull << (sub & 63);
         grp->count++;
