@@ -319,7 +319,8 @@ struct FramedArgs {
     uint64_t src_dw;
     const uint64_t *off;
     const uint16_t *len;
-    const uint16_t *align;  // 0: the group holds a datagram too long for B (its slots, hence parity, are zero)
+    uint16_t *align;        // written: max length + 2, 0 for a group holding a datagram too long for B (its
+                            // slots, hence parity, are zero)
     uint8_t *parity;
     const uint32_t *etab;   // [K][etab_rows][5] perm tables (kfec_internal.hpp enc_tab_*)
     uint64_t pitch;
@@ -424,16 +425,27 @@ __global__ void __launch_bounds__(256) framed_encode_kernel(FramedArgs a)
     uint64_t *s_off = reinterpret_cast<uint64_t *>(s_raw);
     // s_len: the datagram's length, bit 31 set when its group's slots read as zeros (a datagram too long for B)
     uint32_t *s_len = reinterpret_cast<uint32_t *>(s_raw + (size_t)a.gmax * a.K * 8);
+    uint32_t *s_al = s_len + (size_t)a.gmax * a.K;  // per group: max length + 2 (the align), then the flag pass
     const uint32_t K = a.K, cols = a.cols;
     const uint32_t base = blockIdx.x * 256u, item = base + threadIdx.x;
     const uint32_t gfirst = base / cols, glast = min(base + 255u, a.total - 1) / cols, ng = glast - gfirst + 1;
+    // align of the send side (data_operations.cpp:613-616) computed here, per workgroup, for its groups
+    for (uint32_t gs = threadIdx.x; gs < ng; gs += 256) s_al[gs] = 0;
+    __syncthreads();
     for (uint32_t e = threadIdx.x; e < ng * K; e += 256) {
         const uint32_t gs = e / K, j = e - gs * K;
         const uint64_t gj = (uint64_t)(gfirst + gs) * K + j;
-        const bool ok = a.align[gfirst + gs] != 0;
+        const uint32_t n = a.len[gj];
         s_off[e] = a.off[gj];
-        s_len[e] = (uint32_t)a.len[gj] | (ok ? 0u : 0x80000000u);
+        s_len[e] = n;
+        atomicMax(&s_al[gs], n + KFEC_FEC_CONTAINER_HEADER);
     }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < ng * K; e += 256)
+        if (s_al[e / K] > a.B) s_len[e] |= 0x80000000u;  // a datagram too long for B: the slots read as zeros
+    if (blockIdx.y == 0)  // every workgroup touching a group writes the same value
+        for (uint32_t gs = threadIdx.x; gs < ng; gs += 256)
+            a.align[gfirst + gs] = s_al[gs] > a.B ? (uint16_t)0 : (uint16_t)s_al[gs];
     __syncthreads();
     const uint32_t row0 = blockIdx.y * MT;
     const uint32_t rows = a.R > row0 ? min((uint32_t)MT, a.R - row0) : 0u;
@@ -650,12 +662,9 @@ int launch_framed_encode(const uint8_t *d_enc, int K, int N, size_t G, const voi
     if (G == 0) return 0;
     const uint32_t cols = (uint32_t)((B + 31) / 32);
     const uint32_t gmax = (uint32_t)std::min<size_t>(G, 255 / cols + 2);
-    const size_t lds = (size_t)gmax * K * 12;
+    const size_t lds = (size_t)gmax * K * 12 + (size_t)gmax * 4;
     const int mt = R <= 4 ? std::max(R, 1) : 8;
     if (R == 0 || lds > 32 * 1024 || (uint64_t)G * cols > 0x7FFFFFFFull || pitch % 4 || B > 0xFFFF) return 1;
-    hipLaunchKernelGGL(align_kernel, dim3(grid_for(G)), dim3(kFrameBlock), 0, s, (uint64_t)G, (uint32_t)K, (uint32_t)K,
-                       len, nullptr, (uint32_t)B, align);
-    if (launched()) return -3;
     FramedArgs a{};
     a.src = static_cast<const uint32_t *>(src);
     a.src_dw = (src_bytes + 3) / 4;
