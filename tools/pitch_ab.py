@@ -5,6 +5,7 @@ are the same; only the row alignment in HBM changes).  Interleaved rounds; print
 per round, with the device-side check that every recovered shard equals its original.
 
     python tools/pitch_ab.py [rounds] [pitch ...]
+    PITCH_AB_CFG=10:13:1400:random python tools/pitch_ab.py 3 1400 1408   # other configs (K:N:B[:random])
 """
 import json
 import os
@@ -17,7 +18,9 @@ from kcptube_amd import FecCode  # noqa: E402
 
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 pitches = [int(x) for x in sys.argv[2:]] or [1440, 1472, 1536]
-K, N, B, G = 20, 23, 1440, 1 << 20
+cfg = os.environ.get("PITCH_AB_CFG", "20:23:1440").split(":")
+K, N, B, G = int(cfg[0]), int(cfg[1]), int(cfg[2]), 1 << 20
+rnd = len(cfg) > 3 and cfg[3] == "random"
 R = N - K
 dev = torch.device("cuda:0")
 c = FecCode(K, N)
@@ -25,7 +28,10 @@ st = torch.empty((G,), dtype=torch.uint8, device=dev)
 idx = torch.empty((G, R), dtype=torch.uint8, device=dev)
 masks = torch.empty((G, 4), dtype=torch.int64, device=dev)
 ws = c.decode_workspace(G, device=dev)
-c.erasure_masks(masks, 1, K, R)
+if rnd:  # bench config 10:3dec: 1..R erasures anywhere in the N shards
+    c.erasure_masks(masks, 0x5EED0001, N, R, True)
+else:
+    c.erasure_masks(masks, 1, K, R)
 mism = torch.zeros(1, dtype=torch.int64, device=dev)
 s = torch.cuda.current_stream()
 for r in range(rounds):
