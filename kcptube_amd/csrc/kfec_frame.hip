@@ -761,6 +761,7 @@ int launch_frame(int K, int N, bool recv, size_t G, const void *src, size_t src_
     hipLaunchKernelGGL(align_kernel, dim3(grid_for(G)), dim3(kFrameBlock), 0, s, (uint64_t)G, S, (uint32_t)K, len,
                        recv ? present : nullptr, (uint32_t)B, align);
     if (launched()) return -3;
+    if (!data && !parity) return 0;  // align only (the R = 0 encode: there are no slots to write)
     FrameArgs a{};
     a.src = static_cast<const uint32_t *>(src);
     a.src_dw = (src_bytes + 3) / 4;

@@ -574,7 +574,8 @@ def test_decode_framed_recovers_datagrams(dev, oracle, K, N, B):
 
 
 @pytest.mark.parametrize("K,N,B,pitch,pkt_pitch", [(20, 23, 1442, 1444, 1456), (10, 13, 1402, 1404, 1416),
-                                                   (4, 6, 40, 64, 44), (3, 5, 7, 8, 24), (200, 255, 1442, 1444, 1456)])
+                                                   (4, 6, 40, 64, 44), (3, 5, 7, 8, 24), (200, 255, 1442, 1444, 1456),
+                                                   (3, 3, 40, 40, 52)])
 def test_encode_pack_matches_two_step(dev, K, N, B, pitch, pkt_pitch):
     """kfec_encode_pack_batch (data packets written by the encoder) == kfec_encode_framed_batch +
     kfec_pack_batch(DATA | REDUNDANT), byte for byte over the whole packet array: ragged datagrams, a group
@@ -617,7 +618,7 @@ def test_encode_pack_matches_two_step(dev, K, N, B, pitch, pkt_pitch):
     assert np.array_equal(k1, k2)
     B4 = (B + 3) // 4 * 4
     assert np.array_equal(p1[:, :, :B4], p2[:, :, :B4])
-    assert (l1[:, :K] > 0).sum() > G * K // 2 and (l1 == 0).sum() > 0
+    assert (l1[:, :K] > 0).sum() > G * K // 2 and ((l1 == 0).sum() > 0 or N == K)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
