@@ -76,6 +76,14 @@ def build_tools(force: bool = False) -> list[str]:
                    "-Wl,-rpath,$ORIGIN/../kcptube_amd"] + extra
             subprocess.check_call(cmd)
         out.append(exe)
+    # tools/ceiling: the XOR-only HBM calibration kernels, also the FETCH_SIZE / WRITE_SIZE
+    # calibration target of tools/gpu_profile_all.sh, so it must exist in the tree that travels to the box
+    src = os.path.join(ROOT, "tools", "ceiling.hip")
+    exe = os.path.join(ROOT, "tools", "ceiling")
+    if os.path.exists(src) and (force or _stale(exe, [src])):
+        subprocess.check_call([_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-result",
+                               "-Wno-unused-value", src, "-o", exe])
+    out.append(exe)
     return out
 
 
