@@ -1,24 +1,32 @@
 #!/usr/bin/env python3
 """Benchmark of the kfec hot path: device-resident Reed-Solomon encode + decode on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 20:3|10:3dec|200:55]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 20:3|10:3dec|200:55|20:3loss1]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Metric (BASELINE.json): "FEC encode+decode GiB/s (device-resident), fec=20:3 kcp_mtu=1440".
 One step = encode every group of the batch (K data -> R parity shards) and decode every group with R
 data shards erased (selection, per-group m x m inverse, recovery MAC), all on the device with inputs
 already resident in HBM.  value = payload bytes (G * K * B per GPU, summed over GPUs) per step / step
-time, in GiB/s.  Shard groups are independent, so each rank owns its own contiguous group range
-(weak scaling, no collective on the data path; gloo only for the timing barrier and the max-reduce).
+time, in GiB/s.  Shard groups are independent, so each rank owns a contiguous range of the global group
+space (kcptube_amd.partition.group_range; weak scaling, no collective on the data path; gloo carries only
+the timing barrier, the max-reduce and the verification flag).
 
-Also reported: the roofline of the dominant kernel (the encode MAC launch, HIP events on its stream),
-the decode kernels' figures, and the reference CPU coder (oracle/_ref, compiled from the reference's
-own sources) timed on the host cores on a bounded sample (rank 0, N = 1 only).
+Also reported (rank 0):
+  roofline      the dominant kernel (the encode MAC launch; decode for decode-only configs) from HIP events
+                on its stream, plus the whole step (encode + decode algorithmic bytes / ms_per_step) as total
+                and read-only fractions of the 8 TB/s spec AND of this box's measured linear-read ceiling
+                (tools/libkfec_calib.so, timed in the same run); for fec=200:55 (VALU-bound) the byte-MAC
+                rate against the measured GF-MAC VALU ceiling of the same instruction mix.
+  cpu_baseline  the reference coder (oracle/_ref, compiled from the reference's own sources) on all usable
+                host cores over >= 64k distinct groups (rank 0, N = 1 only).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -28,15 +36,20 @@ sys.path.insert(0, ROOT)
 
 METRIC = "FEC encode+decode GiB/s (device-resident), fec=20:3 kcp_mtu=1440, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SEED = 0x5EED0001
 
+# name: K, N, B, groups per GPU, erasure pool, erasures (ppm for iid), erasure mode, encode?, workload text
+#   erasure mode: 0 = exactly `erasures` ids from [0, pool); 1 = 1 + draw % erasures ids; 2 = i.i.d. loss
 CONFIGS = {
-    # name: K, N, B, groups per GPU, erasure pool, erasures, random count, encode?, workload text
-    "20:3": (20, 23, 1440, 1 << 20, 20, 3, False, True,
+    "20:3": (20, 23, 1440, 1 << 20, 20, 3, 0, True,
              "fec=20:3 kcp_mtu=1440, 1M shard groups per GPU, encode + decode with 3 data shards erased"),
-    "10:3dec": (10, 13, 1400, 1 << 20, 13, 3, True, False,
+    "10:3dec": (10, 13, 1400, 1 << 20, 13, 3, 1, False,
                 "fec=10:3 kcp_mtu=1400, 1M groups, decode-only, random 1-3 erasures over all 13 shards"),
-    "200:55": (200, 255, 1440, 1 << 18, 200, 55, False, True,
+    "200:55": (200, 255, 1440, 1 << 18, 200, 55, 0, True,
                "fec=200:55 kcp_mtu=1440, 256k groups, encode + decode with 55 data shards erased"),
+    "20:3loss1": (20, 23, 1440, 1 << 20, 23, 10000, 2, True,
+                  "fec=20:3 kcp_mtu=1440, 1M groups, encode + decode with i.i.d. 1% loss of every shard "
+                  "(a live link: ~82% of the groups lost no data shard)"),
 }
 
 
@@ -49,57 +62,143 @@ def parse():
     p.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=16.0, help="target CPU-seconds of the baseline sample")
+    p.add_argument("--cpu-groups", type=int, default=1 << 16, help="distinct groups of the CPU baseline sample")
     return p.parse_args()
 
 
-def cpu_baseline(K, N, B, pool, erase, rnd, target_cpu_s, decode_only=False):
-    """Reference coder on the host cores, bounded sample.  Test infrastructure (oracle/), used here
-    only for the reported CPU baseline -- never for the GPU number."""
-    import oracle as orc
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-    G = 1 << 15 if K <= 32 else 1 << 9
-    if orc.RefCoder.available():
-        ref = orc.RefCoder()
-        kind = "reference"
-        run = lambda passes: ref.bench_roundtrip(K, N, B, G, pool, erase, rnd, threads, passes, 0x5EED0001,
-                                                 decode_only)[:2]
-    else:
-        o = orc.Oracle()
-        kind = "port"
-        run = lambda passes: o.bench_roundtrip(K, N, B, G, erase, threads, passes, 0x5EED0001)
-    bps, secs = run(1)  # calibration pass (also warms the pages)
-    passes = max(1, int(target_cpu_s / max(secs * threads, 1e-3)))
-    bps, secs = run(passes)
-    # one core, same groups: about a tenth of the CPU time above
-    if kind == "reference":
-        g1 = max(64, G // 8)
-        bps1 = ref.bench_roundtrip(K, N, B, g1, pool, erase, rnd, 1, 1, 0x5EED0001, decode_only)[0]
-    else:
-        g1 = G
-        bps1 = None
-    import platform
-    model = platform.processor() or ""
+def usable_cores() -> tuple[int, dict]:
+    """Cores this process may run on: the affinity set, capped by a cgroup CPU quota if one is set."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    n = aff if quota is None else max(1, min(aff, int(math.floor(quota + 1e-9))))
+    return n, {"affinity_cpus": aff, "cgroup_quota_cpus": quota}
+
+
+def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
+    import platform
+    return platform.processor() or "unknown CPU"
+
+
+def cpu_baseline(K, N, B, pool, erase, mode, target_cpu_s, groups, decode_only=False):
+    """Reference coder on the host cores, bounded sample.  Test infrastructure (oracle/), used here
+    only for the reported CPU baseline -- never for the GPU number."""
+    import oracle as orc
+    threads, cinfo = usable_cores()
+    if orc.RefCoder.available():
+        ref = orc.RefCoder()
+        kind = "reference"
+        run = lambda G, thr, passes: ref.bench_roundtrip(K, N, B, G, pool, erase, mode, thr, passes, SEED,
+                                                         decode_only)[:2]
+    else:
+        o = orc.Oracle()
+        kind = "port"
+        run = lambda G, thr, passes: o.bench_roundtrip(K, N, B, G, erase, thr, passes, SEED)
+    # per-group cost on one core (small sample), then the all-core run sized to ~target CPU-seconds
+    g_cal = max(16, min(groups, 1024 if K <= 32 else 64))
+    bps_cal, secs_cal = run(g_cal, 1, 1)
+    per_group = secs_cal / g_cal
+    G = groups
+    passes = max(1, int(round(target_cpu_s / max(per_group * G, 1e-6))))
+    bps, secs = run(G, threads, passes)
+    # one core: ~2 s of the same work on a contiguous slice of the same groups
+    g1 = int(max(64, min(G, 2.0 / max(per_group, 1e-9))))
+    bps1 = run(g1, 1, 1)[0]
     what = "decode-only" if decode_only else "encode + decode"
-    return {"value": round(bps / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "value_1core": round(bps1 / 2**30, 4) if bps1 else None,
-            "sample": f"{G} distinct groups x {passes} passes of fec={K}:{N-K} B={B} {what} "
-                      f"({'random 1-%d of all %d' % (erase, N) if rnd else '%d data' % erase} shards erased), "
-                      f"{secs:.1f} s wall on {threads} threads, {model}; value_1core: {g1} groups x 1 pass "
-                      f"on 1 thread"}
+    erasure = {0: f"{erase} data shards erased", 1: f"random 1-{erase} of all {N} shards erased",
+               2: f"i.i.d. {erase / 1e4:g}% loss of every shard"}[mode]
+    return {"value": round(bps / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "value_1core": round(bps1 / 2**30, 4),
+            "value_per_core": round(bps / 2**30 / threads, 4),
+            "cpu": cpu_model(), **cinfo,
+            "sample": f"{G} distinct groups x {passes} passes of fec={K}:{N-K} B={B} {what} ({erasure}), "
+                      f"{secs:.1f} s wall on {threads} threads (one contiguous group range and one fec_code "
+                      f"per thread); value_1core: {g1} groups x 1 pass on 1 thread"}
+
+
+class Calib:
+    """tools/libkfec_calib.so: on-box read ceiling and GF-MAC VALU ceiling (measurement only)."""
+
+    def __init__(self):
+        path = os.path.join(ROOT, "tools", "libkfec_calib.so")
+        self.lib = ctypes.CDLL(path) if os.path.exists(path) else None
+        if self.lib:
+            self.lib.calib_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+            self.lib.calib_read_bytes.argtypes = [ctypes.c_size_t]
+            self.lib.calib_read_bytes.restype = ctypes.c_size_t
+            self.lib.calib_gfmac.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                             ctypes.c_void_p]
+
+    def _time(self, torch, launch, reps=5):
+        s = torch.cuda.current_stream()
+        best = None
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            if launch(s.cuda_stream) != 0:
+                return None
+            e1.record(s)
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        return best
+
+    def read_ceiling(self, torch, buf):
+        """GB/s of a linear read of `buf` (a device tensor of a few GB)."""
+        if not self.lib:
+            return None
+        sink = torch.zeros(16, dtype=torch.int32, device=buf.device)
+        n = buf.numel() * buf.element_size()
+        ms = self._time(torch, lambda st: self.lib.calib_read(buf.data_ptr(), n, sink.data_ptr(), st))
+        return None if ms is None else self.lib.calib_read_bytes(n) / (ms * 1e-3) / 1e9
+
+    def gfmac_ceiling(self, torch, dev, rows, cus):
+        """byte-MACs/s of the MAC kernels' VALU instruction mix with no memory traffic."""
+        if not self.lib:
+            return None
+        sink = torch.zeros(16, dtype=torch.int32, device=dev)
+        blocks, iters = cus * 8, 2048
+        ms = self._time(torch, lambda st: self.lib.calib_gfmac(sink.data_ptr(), blocks, iters, rows, st), reps=3)
+        return None if ms is None else blocks * 256 * iters * 32 * rows / (ms * 1e-3)
+
+
+def rank_groups(groups_per_gpu: int, world: int, rank: int) -> tuple[int, int, int]:
+    """(g0, g1, total): this rank's contiguous slice of the global group space (weak scaling:
+    total = groups_per_gpu * world, split by kcptube_amd.partition.group_range)."""
+    from kcptube_amd.partition import group_range
+    total = groups_per_gpu * world
+    g0, g1 = group_range(total, world, rank)
+    return g0, g1, total
 
 
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
+
+    from kcptube_amd import FecCode
+    from kcptube_amd.partition import combine_digests, group_range
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -111,16 +210,14 @@ def main():
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
 
-    from kcptube_amd import FecCode
-
-    K, N, B, G, pool, erase, rnd, do_enc, workload = CONFIGS[args.config]
+    K, N, B, G, pool, erase, mode, do_enc, workload = CONFIGS[args.config]
     if args.groups and args.groups != G:
         G = args.groups
         workload += f" (--groups override: {G} groups per GPU)"
     R = N - K
+    g0, g1, total_groups = rank_groups(G, world, rank)  # this rank's contiguous range of the global groups
+    G = g1 - g0
     c = FecCode(K, N)
-    g0 = rank * G  # this rank's contiguous range of the global group space
-    seed = 0x5EED0001
     data = torch.empty((G, K, B), dtype=torch.uint8, device=dev)
     par = torch.empty((G, R, B), dtype=torch.uint8, device=dev)
     masks = torch.empty((G, 4), dtype=torch.int64, device=dev)
@@ -128,8 +225,8 @@ def main():
     idx = torch.empty((G, R), dtype=torch.uint8, device=dev)
     st = torch.empty((G,), dtype=torch.uint8, device=dev)
     ws = c.decode_workspace(G, device=dev)
-    c.synth(data, seed, g0=g0)
-    c.erasure_masks(masks, seed, pool, erase, rnd, g0=g0)
+    c.synth(data, SEED, g0=g0)
+    c.erasure_masks(masks, SEED, pool, erase, mode, g0=g0)
     c.encode_batch(data, par)  # parity exists before a decode-only step
     torch.cuda.synchronize()
 
@@ -176,29 +273,59 @@ def main():
     torch.cuda.synchronize()
     n_rec = int((idx != 0xFF).sum().item())
     n_dec = int((idx[:, 0] != 0xFF).sum().item()) if R > 0 else 0  # groups with m > 0 (m = 0 reads nothing)
-    ok = int(mism.item()) == 0 and int(st.max().item()) == 0 and n_rec > 0
+    # (i.i.d. loss: a group that lost more than R shards has too few shares, status 1, as the reference's {})
+    st_ok = int(st.max().item()) <= (1 if mode == 2 else 0)
+    ok = int(mism.item()) == 0 and st_ok and n_rec > 0
+    # KFEC_BENCH_DIGEST=P (tests): the global group space cut into P parts (group_range), one SHA-256 per part
+    # over its parity, recovered bytes and recovered ids, gathered in part order and combined (a checksum of
+    # checksums): equal for every world size that divides P iff no group was lost, duplicated or changed
+    parts = int(os.environ.get("KFEC_BENCH_DIGEST", "0") or 0)
+    my_digs = []
+    if parts:
+        import hashlib
+        if parts % world:
+            raise SystemExit("KFEC_BENCH_DIGEST must be a multiple of the world size")
+        o = out.cpu().numpy()
+        ix = idx.cpu().numpy()
+        o[ix == 0xFF] = 0
+        pn = par.cpu().numpy()
+        for p in range(rank * parts // world, (rank + 1) * parts // world):
+            a, b = group_range(total_groups, parts, p)
+            a, b = a - g0, b - g0
+            my_digs.append(hashlib.sha256(pn[a:b].tobytes() + o[a:b].tobytes() + ix[a:b].tobytes()).hexdigest())
+    counts = torch.tensor([0 if ok else 1, n_rec, n_dec], dtype=torch.int64)
+    all_digs = [my_digs]
     if world > 1:
-        t = torch.tensor([0 if ok else 1], dtype=torch.int64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ok = int(t.item()) == 0
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+        if parts:
+            all_digs = [None] * world
+            dist.all_gather_object(all_digs, my_digs)
+    ok = int(counts[0].item()) == 0
+    n_rec_all, n_dec_all = int(counts[1].item()), int(counts[2].item())
 
-    payload = K * B * G * world * args.steps
+    payload = K * B * total_groups * args.steps
     value = payload / elapsed / 2**30
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline: algorithmic HBM bytes per launch / measured launch duration
+    # roofline: algorithmic HBM bytes per launch / measured launch duration (rank 0's share)
     enc_bytes = G * (K + R) * B                    # read K*B, write R*B per group
     dec_bytes = n_dec * K * B + n_rec * B          # read the K selected shares, write the m recovered
     enc_read = G * K * B
     dec_read = n_dec * K * B
     if do_enc:
         dom_bytes, dom_read, dom_ms = enc_bytes, enc_read, enc_ms
-        dom_name = "mac_kernel<VEC,MT,encode> (kfec_encode_batch)"
+        dom_name = "mac_kernel<32,MT,encode> (kfec_encode_batch)"
     else:
         dom_bytes, dom_read, dom_ms = dec_bytes, dec_read, dec_ms
-        dom_name = "decode_prep_* + mac_kernel<VEC,MT,decode> (kfec_decode_batch)"
+        dom_name = "decode_prep + syn_kernel (kfec_decode_batch)"
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     achieved_read = dom_read / (dom_ms * 1e-3) / 1e9
+    step_bytes = (enc_bytes if do_enc else 0) + dec_bytes
+    step_read = (enc_read if do_enc else 0) + dec_read
+    step_ms_local = ms_per_step  # whole step, wall clock, all launches and gaps included
+    step_gbs = step_bytes / (step_ms_local * 1e-3) / 1e9
+    step_read_gbs = step_read / (step_ms_local * 1e-3) / 1e9
+
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
@@ -209,6 +336,36 @@ def main():
                 traffic = tr.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+
+    calib = Calib()
+    read_ceiling = calib.read_ceiling(torch, data) if rank == 0 else None
+    roof = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),
+            "achieved_read": round(achieved_read, 1), "frac_read": round(achieved_read / HBM_PEAK_GBS, 4),
+            # the whole step (encode + decode) against the spec peak and the measured read ceiling
+            "step_bytes": step_bytes, "step_read_bytes": step_read, "step_ms": round(step_ms_local, 4),
+            "step_achieved": round(step_gbs, 1), "step_frac": round(step_gbs / HBM_PEAK_GBS, 4),
+            "step_frac_read": round(step_read_gbs / HBM_PEAK_GBS, 4),
+            "read_ceiling": round(read_ceiling, 1) if read_ceiling else None,
+            "step_frac_of_ceiling": round(step_gbs / read_ceiling, 4) if read_ceiling else None,
+            "step_frac_read_of_ceiling": round(step_read_gbs / read_ceiling, 4) if read_ceiling else None,
+            "frac_of_ceiling": round(achieved / read_ceiling, 4) if read_ceiling else None}
+    if args.config == "200:55" and rank == 0:
+        # VALU-bound: byte-MACs per second of each kernel against the same instruction mix with no memory
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        ceil_mac = calib.gfmac_ceiling(torch, dev, 8, cus)
+        enc_mac = G * R * K * B / (enc_ms * 1e-3)
+        dec_mac = n_rec * K * B / (dec_ms * 1e-3)
+        roof.update({"bound": "valu", "unit": "byte-MAC/s", "achieved": round(enc_mac, 0),
+                     "peak": round(ceil_mac, 0) if ceil_mac else None,
+                     "frac": round(enc_mac / ceil_mac, 4) if ceil_mac else None,
+                     "decode_achieved": round(dec_mac, 0),
+                     "decode_frac": round(dec_mac / ceil_mac, 4) if ceil_mac else None,
+                     "hbm_achieved": round(achieved, 1), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "ceiling_kernel": "tools/calib.hip gfmac<8>: mac_kernel's perm-MAC mix, 8 rows x 32-B "
+                                       "granules, tables from LDS, no memory"})
+
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -223,23 +380,23 @@ def main():
         "dtype": "u8",
         "data": "synthetic: splitmix64 counter bytes generated on device (SURVEY 8d); erasure patterns per-group PRNG",
         "config": {"workload": workload, "fec": f"{K}:{R}", "kcp_mtu": B, "groups_per_gpu": G,
-                   "global_groups": G * world, "parallelism": f"{world} independent group ranges (no collective)"},
-        "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),
-                     "achieved_read": round(achieved_read, 1), "frac_read": round(achieved_read / HBM_PEAK_GBS, 4)},
+                   "global_groups": total_groups,
+                   "parallelism": f"{world} independent group ranges (no collective)"},
+        "roofline": roof,
         "encode_ms": round(enc_ms, 4) if do_enc else None,
         "decode_ms": round(dec_ms, 4),
         "decode_hbm_GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),
         "roundtrip_hbm_GBps": round(((enc_bytes if do_enc else 0) + dec_bytes) / ((enc_ms if do_enc else 0) + dec_ms) / 1e6, 1),
-        "recovered_shards_per_step": n_rec * world,
-        "decoded_groups_per_step": n_dec * world,
+        "recovered_shards_per_step": n_rec_all,
+        "decoded_groups_per_step": n_dec_all,
         "verified_bit_exact": ok,
         "cpu_baseline": None,
     }
+    if parts:
+        result["combined_digest"] = combine_digests([d for ds in all_digs for d in ds])
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            result["cpu_baseline"] = cpu_baseline(K, N, B, pool, erase, rnd, args.cpu_seconds,
+            result["cpu_baseline"] = cpu_baseline(K, N, B, pool, erase, mode, args.cpu_seconds, args.cpu_groups,
                                                   decode_only=not do_enc)
         except Exception as e:  # the GPU number stands on its own
             result["cpu_baseline"] = {"error": repr(e)}

@@ -103,18 +103,16 @@ int kfec_decode_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, con
  * splitmix64(seed ^ ((g*N + s) * ceil(B/8) + w)) (little-endian words). */
 int kfec_synth(const kfec_ctx *ctx, uint64_t seed, size_t g0, size_t G, size_t s0, size_t ns, size_t B,
                size_t pitch, void *d_out, void *stream);
-/* Per-group erasure masks: erase `count` distinct ids drawn from [0, pool) (count = 1 + draw % count_max
- * when random_count != 0), every other id in [0, N) present.  Same draw as the CPU harness. */
+/* Per-group erasure masks: erase `count` distinct ids drawn from [0, pool) (count = count_max, or
+ * 1 + draw % count_max when random_count == 1), every other id in [0, N) present; random_count == 2:
+ * i.i.d. loss, every id in [0, N) lost independently with probability count_max / 1e6 (pool ignored).
+ * Same draws as the CPU harness (oracle/rs_oracle.c). */
 int kfec_erasure_masks(const kfec_ctx *ctx, uint64_t seed, size_t g0, size_t G, size_t pool,
                        size_t count_max, int random_count, uint64_t *d_present, void *stream);
 /* Compare recovered shards with the original data: d_mismatch[0] += number of (g, t) slots whose bytes
  * [0, B) differ from d_data[g][d_out_idx[g][t]].  d_mismatch is a device uint64 (caller zeroes it). */
 int kfec_verify_recovered(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, const void *d_data,
                           const void *d_out, const uint8_t *d_out_idx, uint64_t *d_mismatch, void *stream);
-
-/* Non-zero if a bounded spin of the persistent stream-engine kernel ever timed out on the current device
- * (bit 0: loader, bit 1: consumer).  Never expected; the engine exits instead of hanging the GPU. */
-uint32_t kfec_debug_flags(void);
 
 /* Library version string and the device the context runs on (-1 if none). */
 const char *kfec_version(void);

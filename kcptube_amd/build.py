@@ -76,6 +76,14 @@ def build_tools(force: bool = False) -> list[str]:
                    "-Wl,-rpath,$ORIGIN/../kcptube_amd"] + extra
             subprocess.check_call(cmd)
         out.append(exe)
+    # tools/libkfec_calib.so: the on-box read and GF-MAC VALU ceilings bench.py reports against
+    src = os.path.join(ROOT, "tools", "calib.hip")
+    so = os.path.join(ROOT, "tools", "libkfec_calib.so")
+    if force or _stale(so, [src, os.path.join(CSRC, "kfec_gf.hpp")]):
+        subprocess.check_call([_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                               "-Wno-unused-result", src, "-o", so + ".tmp"])
+        os.replace(so + ".tmp", so)
+    out.append(so)
     # tools/ceiling: the XOR-only HBM calibration kernels, also the FETCH_SIZE / WRITE_SIZE
     # calibration target of tools/gpu_profile_all.sh, so it must exist in the tree that travels to the box
     src = os.path.join(ROOT, "tools", "ceiling.hip")

@@ -110,9 +110,7 @@ inline int set_dev(const kfec_ctx *c) { return hipSetDevice(c->di.device) == hip
 
 extern "C" {
 
-const char *kfec_version(void) { return "kfec 0.2 (gfx950 perm-MAC, LDS-DMA stream engine)"; }
-
-uint32_t kfec_debug_flags(void) { return kfec::engine_error_word(); }
+const char *kfec_version(void) { return "kfec 0.3 (gfx950 perm-MAC, flattened column kernel)"; }
 
 int kfec_device(const kfec_ctx *ctx) { return ctx ? ctx->di.device : -1; }
 

@@ -8,17 +8,20 @@
 
 namespace kfec {
 
-// Per-group decode record written by the prep kernels and read by the MAC kernel (group-major, so the
-// few records a workgroup needs per iteration are a couple of contiguous cache lines):
+// Per-group decode record written by the prep kernels and read by the MAC kernels (group-major, so the
+// few records a workgroup needs are a couple of contiguous cache lines).  Coefficient form:
 //   [0] status (KFEC_GROUP_*), [1] m = missing data shards, [2..3] 0,
 //   [4, 4+K4)              src[j]     share id used as column j of the selected K x K system,
 //   [4+K4, 4+K4+R*K4)      coef[u][j] row u (u < m) of the inverse decode matrix for missing shard u,
-// with K4 = K rounded up to 4 so that the prep kernel writes whole dwords.
+// with K4 = K rounded up to 4 so that the prep kernel writes whole dwords.  Syndrome form (R <= 8, see
+// write_syn in kfec_kernels.hip): [0] status, [1] m, [2] used-parity bits, [8, 72) the 8 x 8 C matrix.
 inline size_t rec_k4(size_t K) { return (K + 3) & ~size_t(3); }
-inline size_t record_stride(size_t K, size_t R) { return (4 + rec_k4(K) + R * rec_k4(K) + 15) & ~size_t(15); }
-// after the G records: a uint32 count (+ 60 bytes of padding) and the uint32 work list of the decode MAC
-inline size_t decode_list_offset(size_t G, size_t K, size_t R) { return (G * record_stride(K, R) + 255) & ~size_t(255); }
-inline size_t decode_workspace_bytes(size_t G, size_t K, size_t R) { return decode_list_offset(G, K, R) + 64 + 4 * G; }
+inline size_t record_stride(size_t K, size_t R)
+{
+    const size_t coef = (4 + rec_k4(K) + R * rec_k4(K) + 15) & ~size_t(15);
+    return coef > 80 ? coef : 80;
+}
+inline size_t decode_workspace_bytes(size_t G, size_t K, size_t R) { return (G * record_stride(K, R) + 255) & ~size_t(255); }
 
 // The encoding matrix allocation also holds the perm-MAC tables of its parity rows (gf_perm_tables, 5 dwords
 // per coefficient) for the encode kernel, laid out [K][R + 8][5]: shard-major so that the rows of one shard
@@ -40,15 +43,13 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
                   const void *d_data, const void *d_parity, const uint64_t *d_present, void *d_out,
                   uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s);
 int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, const uint64_t *d_present,
-                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s);
+                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s, bool syn = false);
 int launch_synth(uint64_t seed, int N, size_t g0, size_t G, size_t s0, size_t ns, size_t B, size_t pitch,
                  void *d_out, hipStream_t s);
 int launch_erasure_masks(uint64_t seed, int N, size_t g0, size_t G, size_t pool, size_t count_max,
                          int random_count, uint64_t *d_present, hipStream_t s);
 int launch_verify(int K, int N, size_t G, size_t B, size_t pitch, const void *d_data, const void *d_out,
                   const uint8_t *d_out_idx, uint64_t *d_mismatch, hipStream_t s);
-
-uint32_t engine_error_word();
 
 // framing and wire layer (kfec_frame.hip)
 int launch_frame(int K, int N, bool recv, size_t G, const void *src, size_t src_bytes, const uint64_t *off,

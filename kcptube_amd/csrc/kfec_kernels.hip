@@ -31,26 +31,6 @@ namespace kfec {
 
 __constant__ GfTables c_gf = make_gf_tables();
 
-// set by the stream engine if a bounded spin ever times out (read by kfec_engine_error)
-__device__ uint32_t g_engine_err;
-
-static uint32_t *g_err_word()
-{
-    static uint32_t *p[64] = {};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    dev &= 63;
-    if (!p[dev]) (void)hipGetSymbolAddress(reinterpret_cast<void **>(&p[dev]), HIP_SYMBOL(g_engine_err));
-    return p[dev];
-}
-
-uint32_t engine_error_word()
-{
-    uint32_t v = 0;
-    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_engine_err), sizeof(v));
-    return v;
-}
-
 static constexpr int kBlock = 256;
 #ifndef KFEC_MAC_BLOCK
 #define KFEC_MAC_BLOCK 256
@@ -59,25 +39,10 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 
 // build-time tuning knobs (tools/ab.py builds variants; the shipped library uses the defaults)
 #ifndef KFEC_PD
-#define KFEC_PD 4
-#endif
-#ifndef KFEC_ABLATE
-#define KFEC_ABLATE 0
-#endif
-#ifndef KFEC_VEC32
-#define KFEC_VEC32 1  // 32-byte lane granules in the flattened kernel (2 KiB per wave-instruction pair)
+#define KFEC_PD 4  // shards in flight per lane (halved for 32-byte granules)
 #endif
 #ifndef KFEC_MINW
-#define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the flattened kernel
-#endif
-#ifndef KFEC_SGPR_TABLES
-#define KFEC_SGPR_TABLES 0  // encode reads its perm tables with scalar loads instead of LDS (KFEC_SGPR_TABLES env)
-#endif
-#ifndef KFEC_XCD_REMAP
-#define KFEC_XCD_REMAP 0  // XCD-contiguous workgroup numbering in the flattened kernel (A/B knob)
-#endif
-#ifndef KFEC_NTSTORE
-#define KFEC_NTSTORE 1  // nontemporal output stores in the flattened kernel (+2.5% encode, measured)
+#define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the MAC kernels
 #endif
 
 // ---------------------------------------------------------------------------------------------------
@@ -190,6 +155,7 @@ struct PrepArgs {
     uint64_t G;
     int K, N, R;
     uint32_t rec_stride;
+    int syn;  // write syndrome-form records (R <= 8) instead of the coefficient form
 };
 
 // (no early return: the unrolled q index stays a constant, so w[] lives in registers, not scratch)
@@ -225,6 +191,40 @@ __device__ __forceinline__ void write_empty(const PrepArgs &a, uint64_t g, uint8
     rec[1] = 0;
     for (int t = 0; t < a.R; ++t) a.out_idx[g * a.R + t] = 0xFF;
     a.status[g] = st;
+}
+
+// Syndrome-form record (syn_kernel, R <= 8): [0] status 0, [1] m, [2] bit r set = parity row K + r is one
+// of the m shares used, [3..7] 0, [8 + 8u + r] = C[u][r] = Sinv[u][t] for the rank t with P_t = K + r
+// (0 for unused rows and for u >= m): all 8 rows are written so any row tile RT <= 8 reads zeros beyond m.
+template <int MAXM, typename F>
+__device__ __forceinline__ void write_syn(const PrepArgs &a, uint64_t g, int m, const int (&M)[MAXM],
+                                          const int (&P)[MAXM], F sinv)
+{
+    uint64_t *rw = reinterpret_cast<uint64_t *>(a.rec + g * a.rec_stride);
+    uint32_t used = 0;
+    uint64_t row[MAXM];
+#pragma unroll
+    for (int u = 0; u < MAXM; ++u) row[u] = 0;
+#pragma unroll
+    for (int t = 0; t < MAXM; ++t) {
+        if (t < m) {
+            const uint32_t r = (uint32_t)(P[t] - a.K);
+            used |= 1u << r;
+#pragma unroll
+            for (int u = 0; u < MAXM; ++u)
+                if (u < m) row[u] |= (uint64_t)sinv(u, t) << (8 * r);
+        }
+    }
+    rw[0] = (uint64_t)(((uint32_t)m << 8) | (used << 16));
+#pragma unroll
+    for (int u = 0; u < MAXM; ++u) rw[1 + u] = row[u];
+#pragma unroll
+    for (int u = MAXM; u < 8; ++u) rw[1 + u] = 0;
+#pragma unroll
+    for (int t = 0; t < MAXM; ++t)
+        if (t < a.R) a.out_idx[g * a.R + t] = (t < m) ? (uint8_t)M[t] : (uint8_t)0xFF;
+    for (int t = MAXM; t < a.R; ++t) a.out_idx[g * a.R + t] = 0xFF;
+    a.status[g] = 0;
 }
 
 template <int MAXM>
@@ -298,6 +298,10 @@ __global__ void __launch_bounds__(kBlock) decode_prep_small(PrepArgs a)
         }
         if (singular) {
             write_empty(a, g, 2);
+            continue;
+        }
+        if (a.syn) {
+            write_syn<MAXM>(a, g, m, M, P, [&](int u, int t) { return Iv[u][t]; });
             continue;
         }
         rec[0] = 0;
@@ -453,6 +457,10 @@ __global__ void __launch_bounds__(kBlock) decode_prep_perm(PrepArgs a)
         }
         if (singular) {
             write_empty(a, g, 2);
+            continue;
+        }
+        if (a.syn) {
+            write_syn<MAXM>(a, g, m, M, P, [&](int u, int t) { return (Iv[u] >> (8 * t)) & 0xFFu; });
             continue;
         }
         rec[0] = 0;
@@ -661,7 +669,12 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
 }
 
 // ---------------------------------------------------------------------------------------------------
-// (A4/A5/A8/A11) perm-MAC kernel: out[g][row] = XOR_j coef[row][j] * share_j[g]  over V-byte columns.
+// (A4/A5/A8/A11) perm-MAC kernels over V-byte columns.
+//   mac_kernel (coefficient form): out[g][row] = XOR_j coef[row][j] * share_j[g]
+//     encode: coef = the parity rows of the encoding matrix (fecpp.cpp:495-513);
+//     decode for R > 8: coef = the K x K inverse rows of the missing shards, shares gathered through the
+//     record's source ids (fecpp.cpp:550-585).
+//   syn_kernel (syndrome form, decode with R <= 8): see below.
 // ---------------------------------------------------------------------------------------------------
 struct MacArgs {
     const uint8_t *data;    // [G][K][pitch]
@@ -670,17 +683,13 @@ struct MacArgs {
     const uint8_t *enc;     // N x K encoding matrix (encode)
     const uint8_t *rec;     // per-group records (decode)
     uint64_t pitch;
-    uint32_t total;         // G * cpad work items
+    uint32_t total;         // G * cols work items
     uint32_t cols;          // granules per shard
-    uint32_t cpad;          // items per group (>= cols; lanes with col >= cols idle)
     uint32_t G, K, R, B;
     uint32_t rec_stride;
     uint32_t JC;            // shards per LDS chunk
     uint32_t gmax;          // group slots per chunk
-    const uint32_t *etab;   // encode: perm tables [K][etab_rows][5] read with scalar loads (null: LDS path)
-    uint32_t etab_rows;
-    const uint32_t *list;   // decode: the groups with work (m > 0), ascending per wave; null = every group
-    const uint32_t *list_count;
+    uint32_t tiles;         // row tiles of MT output rows
 };
 
 template <int VEC>
@@ -697,15 +706,10 @@ __device__ __forceinline__ Gran<VEC> load_gran(const uint8_t *p, uint32_t col, u
         const uint4 x = reinterpret_cast<const uint4 *>(p)[0], y = reinterpret_cast<const uint4 *>(p)[1];
         v.d[0] = x.x; v.d[1] = x.y; v.d[2] = x.z; v.d[3] = x.w;
         v.d[4] = y.x; v.d[5] = y.y; v.d[6] = y.z; v.d[7] = y.w;
-    } else if constexpr (VEC == 16) {
-        const uint4 x = *reinterpret_cast<const uint4 *>(p);
-        v.d[0] = x.x; v.d[1] = x.y; v.d[2] = x.z; v.d[3] = x.w;
-    } else if constexpr (VEC == 8) {
-        const uint2 x = *reinterpret_cast<const uint2 *>(p);
-        v.d[0] = x.x; v.d[1] = x.y;
     } else if constexpr (VEC == 4) {
         v.d[0] = *reinterpret_cast<const uint32_t *>(p);
     } else {  // bytewise: 4 bytes at p, only those below B
+        static_assert(VEC == 1, "granule");
         uint32_t x = 0;
         const uint32_t b0 = col * 4;
 #pragma unroll
@@ -720,17 +724,10 @@ template <int VEC>
 __device__ __forceinline__ void store_gran(uint8_t *p, const uint32_t *d, uint32_t col, uint32_t B)
 {
     if constexpr (VEC == 32) {
-        store_gran<16>(p, d, col, B);
-        store_gran<16>(p + 16, d + 4, col, B);
-    } else if constexpr (VEC == 16) {
-#if KFEC_NTSTORE
+        // nontemporal: the outputs are not re-read by this launch (+2.5% encode, measured)
         typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
         __builtin_nontemporal_store(u32x4_t{d[0], d[1], d[2], d[3]}, reinterpret_cast<u32x4_t *>(p));
-#else
-        *reinterpret_cast<uint4 *>(p) = make_uint4(d[0], d[1], d[2], d[3]);
-#endif
-    } else if constexpr (VEC == 8) {
-        *reinterpret_cast<uint2 *>(p) = make_uint2(d[0], d[1]);
+        __builtin_nontemporal_store(u32x4_t{d[4], d[5], d[6], d[7]}, reinterpret_cast<u32x4_t *>(p + 16));
     } else if constexpr (VEC == 4) {
         *reinterpret_cast<uint32_t *>(p) = d[0];
     } else {
@@ -761,12 +758,42 @@ __device__ __forceinline__ void store_gran_tail(uint8_t *p, const uint32_t *d, u
         if ((uint32_t)w < nd) reinterpret_cast<uint32_t *>(p)[w] = d[w];
 }
 
+template <int VEC>
+__device__ __forceinline__ Gran<VEC> load_any(const uint8_t *p, uint32_t col, uint32_t B, uint32_t nd)
+{
+    return nd < (uint32_t)Gran<VEC>::W ? load_gran_tail<VEC>(p, nd) : load_gran<VEC>(p, col, B);
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_any(uint8_t *p, const uint32_t *d, uint32_t col, uint32_t B, uint32_t nd)
+{
+    if (nd < (uint32_t)Gran<VEC>::W) store_gran_tail<VEC>(p, d, nd);
+    else store_gran<VEC>(p, d, col, B);
+}
+
 template <int MT>
 struct MacLayout {
     static_assert(MT >= 1 && MT <= 8, "row tile");
     static constexpr int TBL_DW = ((5 * MT + 3) / 4) * 4;  // table dwords per (group, shard): 5 per row
     static constexpr int ENTRY = 16 + 4 * TBL_DW;          // + 8-byte share pointer, 8 pad
 };
+
+// Workgroup b -> (column chunk, row tile).  With R > MT the tiles of one column chunk are numbered
+// b, b+8, b+16, ...: the dispatcher deals workgroups round-robin over the 8 XCDs, so those run back to back
+// on ONE XCD and all but the first read the chunk's shard bytes from that XCD's L2 (speed only: any
+// placement gives the same bytes).  The previous (chunk = x, tile = y) grid ran every chunk of tile 0 before
+// tile 1, so each of the 7 tiles of fec=200:55 re-read the 75.5 GB of data from HBM.
+__device__ __forceinline__ void block_chunk_tile(uint32_t b, uint32_t tiles, uint32_t &chunk, uint32_t &tile)
+{
+    if (tiles <= 1) {
+        chunk = b;
+        tile = 0;
+        return;
+    }
+    const uint32_t k = b >> 3;
+    tile = k % tiles;
+    chunk = (k / tiles) * 8 + (b & 7);
+}
 
 // expand coefficients of shards [c0, c0+nj) for group slots [0, ng) into LDS entries
 template <int MT, bool DEC>
@@ -783,7 +810,7 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
         uint32_t c = 0;
         if constexpr (DEC) {
             const uint32_t K4 = (a.K + 3) & ~3u;
-            const uint32_t g = a.list ? a.list[gfirst + gs] : gfirst + gs;
+            const uint32_t g = gfirst + gs;
             const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
             const uint32_t st = rec[0], m = rec[1];
             if (st == 0 && u < m) c = rec[4 + K4 + u * K4 + j];
@@ -797,17 +824,17 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
             if (u < a.R) c = a.enc[(uint64_t)(a.K + u) * a.K + j];
         }
         uint32_t t[5];
-#if KFEC_ABLATE == 4  // timing-only: no table construction in the per-workgroup expansion
-        t[0] = t[1] = t[2] = t[3] = t[4] = c;
-#else
         gf_perm_tables(c, t);
-#endif
         uint32_t *tp = reinterpret_cast<uint32_t *>(ent + 16) + 5 * r;
 #pragma unroll
         for (int i = 0; i < 5; ++i) tp[i] = t[i];
     }
 }
 
+// One lane = one (group, V-byte column) item; consecutive lanes take consecutive columns and wrap into the
+// next group, so a wave-instruction reads 2 KiB of one shard row (V = 32).  One workgroup per 256 items
+// (non-persistent grid: the dispatcher refills each CU as workgroups retire).  Per lane: K loads of V bytes
+// (PD in flight), MT accumulator rows, MT stores.
 template <int VEC, int MT, bool DEC, int PDX = 0>
 __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
 {
@@ -819,849 +846,260 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
 
-    const uint32_t row0 = blockIdx.y * MT;
-    const uint32_t K = a.K, cols = a.cpad;
-    const bool gtab = !DEC && a.etab != nullptr;  // encode: wave-uniform tables straight from memory
-    const bool enc_once = !DEC && (gtab || K <= a.JC);
-    if (enc_once && !gtab) {
+    uint32_t chunk, tile;
+    block_chunk_tile(blockIdx.x, a.tiles, chunk, tile);
+    const uint32_t base = chunk * kMacBlock;
+    if (base >= a.total) return;  // padding chunk of the XCD-ordered tile grid (whole workgroup)
+    const uint32_t row0 = tile * MT;
+    const uint32_t K = a.K, cols = a.cols;
+    const bool enc_once = !DEC && K <= a.JC;
+    if (enc_once) {
         mac_expand<MT, false>(a, s_ent, 0, 1, 0, K, row0);
         __syncthreads();
     }
-    const uint32_t stride = gridDim.x * kMacBlock;
-    // XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs, so workgroup b would run
-    // next to b+8, not b+1.  Re-numbering (bijective, MI355X guide T1) gives each XCD a contiguous run of
-    // items, so the 128-B lines that straddle two workgroups' columns are fetched by one L2, not two.
-    uint32_t wg = blockIdx.x;
-#if KFEC_XCD_REMAP
-    {
-        const uint32_t n = gridDim.x, q = n / 8, r = n % 8, x = wg % 8, i = wg / 8;
-        wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
-    }
-#endif
-    // decode with a work list: only the groups that lost data shards are visited (list index space)
-    const uint32_t total = (DEC && a.list) ? min(*a.list_count, a.G) * cols : a.total;
-    for (uint32_t base = wg * kMacBlock; base < total; base += stride) {
-        const uint32_t item = base + threadIdx.x;
-        const uint32_t gi = item < total ? item / cols : 0;  // list index (= group without a list)
-        const uint32_t col = item < total ? item - gi * cols : 0;
-        const bool in = item < total && col < a.cols;
-        const uint32_t g = (DEC && a.list) ? (item < total ? a.list[gi] : 0u) : gi;
-        // dwords of this lane's granule below B: W except in the last granule of a row when VEC does not
-        // divide B (VEC >= 4 only; the bytewise VEC = 1 path checks every byte itself)
-        const uint32_t nd = (VEC >= 4 && (col + 1) * VB > a.B) ? (a.B - col * VB + 3) / 4 : (uint32_t)W;
-        const uint32_t gfirst = base / cols;
-        const uint32_t glast = min(base + kMacBlock - 1, total - 1) / cols;
-        const uint32_t ng = glast - gfirst + 1;
-        const uint32_t gs = DEC ? gi - gfirst : 0;
+    const uint32_t item = base + threadIdx.x;
+    const bool in = item < a.total;
+    const uint32_t g = in ? item / cols : 0;
+    const uint32_t col = in ? item - g * cols : 0;
+    // dwords of this lane's granule below B: W except in the last granule of a row when VEC does not
+    // divide B (VEC >= 4 only; the bytewise VEC = 1 path checks every byte itself)
+    const uint32_t nd = (VEC >= 4 && (col + 1) * VB > a.B) ? (a.B - col * VB + 3) / 4 : (uint32_t)W;
+    const uint32_t gfirst = base / cols;
+    const uint32_t glast = min(base + kMacBlock - 1, a.total - 1) / cols;
+    const uint32_t ng = glast - gfirst + 1;
+    const uint32_t gs = DEC ? g - gfirst : 0;
 
-        uint32_t rows = 0;
-        if (in) {
-            if constexpr (DEC) {
-                const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
-                const uint32_t st = rec[0], m = rec[1];
-                rows = (st == 0 && m > row0) ? min((uint32_t)MT, m - row0) : 0u;
-            } else {
-                rows = a.R > row0 ? min((uint32_t)MT, a.R - row0) : 0u;
-            }
+    uint32_t rows = 0;
+    if (in) {
+        if constexpr (DEC) {
+            const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
+            const uint32_t st = rec[0], m = rec[1];
+            rows = (st == 0 && m > row0) ? min((uint32_t)MT, m - row0) : 0u;
+        } else {
+            rows = a.R > row0 ? min((uint32_t)MT, a.R - row0) : 0u;
         }
-        uint32_t acc[MT][W];
+    }
+    uint32_t acc[MT][W];
 #pragma unroll
-        for (int r = 0; r < MT; ++r)
+    for (int r = 0; r < MT; ++r)
 #pragma unroll
-            for (int w = 0; w < W; ++w) acc[r][w] = 0;
+        for (int w = 0; w < W; ++w) acc[r][w] = 0;
 
-        const uint8_t *enc_base = a.data + ((uint64_t)g * K) * a.pitch + (uint64_t)col * VB;
-        for (uint32_t c0 = 0; c0 < K; c0 += a.JC) {
-            const uint32_t nj = min(a.JC, K - c0);
-            if (!enc_once) {
-                __syncthreads();
-                mac_expand<MT, DEC>(a, s_ent, gfirst, DEC ? ng : 1u, c0, nj, row0);
-                __syncthreads();
+    const uint8_t *enc_base = a.data + ((uint64_t)g * K) * a.pitch + (uint64_t)col * VB;
+    for (uint32_t c0 = 0; c0 < K; c0 += a.JC) {
+        const uint32_t nj = min(a.JC, K - c0);
+        if (!enc_once) {
+            __syncthreads();
+            mac_expand<MT, DEC>(a, s_ent, gfirst, DEC ? ng : 1u, c0, nj, row0);
+            __syncthreads();
+        }
+        if (rows == 0) continue;
+        const uint8_t *ent0 = s_ent + (gs * a.JC) * L::ENTRY;
+        auto share_ptr = [&](uint32_t jj) -> const uint8_t * {
+            if constexpr (DEC) {
+                return *reinterpret_cast<const uint8_t *const *>(ent0 + jj * L::ENTRY) + (uint64_t)col * VB;
+            } else {
+                return enc_base + (uint64_t)(c0 + jj) * a.pitch;
             }
-            if (rows == 0) continue;
-            const uint8_t *ent0 = s_ent + (gs * a.JC) * L::ENTRY;
-            // (a shard visiting order that puts the two readers of a line straddling shards j and j+1 >= PD
-            // loads apart, or lags odd waves, was measured: no gain at 20:3, -15% at 10:3 -- DESIGN.md 4.5)
-            auto sj = [](uint32_t jj) -> uint32_t { return jj; };
-            auto share_ptr = [&](uint32_t jj) -> const uint8_t * {
-                const uint32_t j = sj(jj);
-                if constexpr (DEC) {
-#if KFEC_ABLATE == 2  // timing-only: decode reads shards like encode (data buffer, no pointer indirection)
-                    return enc_base + (uint64_t)(c0 + j) * a.pitch;
-#endif
-                    return *reinterpret_cast<const uint8_t *const *>(ent0 + j * L::ENTRY) + (uint64_t)col * VB;
-                } else {
-                    return enc_base + (uint64_t)(c0 + j) * a.pitch;
-                }
-            };
-            Gran<VEC> x[PD];
+        };
+        Gran<VEC> x[PD];
 #pragma unroll
-            for (int u = 0; u < PD; ++u)
-                if ((uint32_t)u < nj)
-                    x[u] = nd < (uint32_t)W ? load_gran_tail<VEC>(share_ptr(u), nd) : load_gran<VEC>(share_ptr(u), col, a.B);
-            for (uint32_t jb = 0; jb < nj; jb += PD) {
+        for (int u = 0; u < PD; ++u)
+            if ((uint32_t)u < nj) x[u] = load_any<VEC>(share_ptr(u), col, a.B, nd);
+        for (uint32_t jb = 0; jb < nj; jb += PD) {
 #pragma unroll
-                for (int u = 0; u < PD; ++u) {
-                    const uint32_t jj = jb + u;
-                    if (jj < nj) {
-                        const Gran<VEC> cur = x[u];
-                        if (jj + PD < nj)
-                            x[u] = nd < (uint32_t)W ? load_gran_tail<VEC>(share_ptr(jj + PD), nd)
-                                                    : load_gran<VEC>(share_ptr(jj + PD), col, a.B);
-                        const uint8_t *ent = ent0 + sj(jj) * L::ENTRY;
-                        uint32_t t[L::TBL_DW];
-                        if (gtab) {
-                            // uniform address in the constant address space: scalar loads into SGPRs, no LDS
-                            typedef const __attribute__((address_space(4))) uint32_t cu32;
-                            const cu32 *tg = (const cu32 *)(a.etab + ((size_t)(c0 + jj) * a.etab_rows + row0) * 5);
+            for (int u = 0; u < PD; ++u) {
+                const uint32_t jj = jb + u;
+                if (jj < nj) {
+                    const Gran<VEC> cur = x[u];
+                    if (jj + PD < nj) x[u] = load_any<VEC>(share_ptr(jj + PD), col, a.B, nd);
+                    const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + jj * L::ENTRY + 16);
+                    uint32_t t[L::TBL_DW];
 #pragma unroll
-                            for (int i = 0; i < 5 * MT; ++i) t[i] = tg[i];
-                        } else {
-                            const uint4 *tv = reinterpret_cast<const uint4 *>(ent + 16);
+                    for (int i = 0; i < L::TBL_DW / 4; ++i) {
+                        const uint4 q = tv[i];
+                        t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+                    }
 #pragma unroll
-                            for (int i = 0; i < L::TBL_DW / 4; ++i) {
-                                const uint4 q = tv[i];
-                                t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
-                            }
-                        }
+                    for (int w = 0; w < W; ++w) {
+                        const uint32_t xv = cur.d[w];
+                        const uint32_t s0 = xv & 0x07070707u;
+                        const uint32_t s1 = (xv >> 3) & 0x07070707u;
+                        const uint32_t s2 = (xv >> 6) & 0x03030303u;
 #pragma unroll
-                        for (int w = 0; w < W; ++w) {
-                            const uint32_t xv = cur.d[w];
-                            const uint32_t s0 = xv & 0x07070707u;
-                            const uint32_t s1 = (xv >> 3) & 0x07070707u;
-                            const uint32_t s2 = (xv >> 6) & 0x03030303u;
-#pragma unroll
-                            for (int r = 0; r < MT; ++r) {
-#if KFEC_ABLATE == 1  // timing-only build: memory traffic of the real kernel, XOR instead of the GF MAC
-                                acc[r][w] ^= xv ^ t[5 * r];
-                                (void)s0; (void)s1; (void)s2;
-#else
-                                acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
-#endif
-                            }
-                        }
+                        for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
                     }
                 }
             }
         }
-        if (rows) {
-            const uint64_t obase = ((uint64_t)g * a.R + row0) * a.pitch + (uint64_t)col * VB;
+    }
+    if (rows) {
+        const uint64_t obase = ((uint64_t)g * a.R + row0) * a.pitch + (uint64_t)col * VB;
 #pragma unroll
-            for (int r = 0; r < MT; ++r)
-                if ((uint32_t)r < rows) {
-                    uint8_t *o = a.out + obase + (uint64_t)r * a.pitch;
-                    if (nd < (uint32_t)W) store_gran_tail<VEC>(o, acc[r], nd);
-                    else store_gran<VEC>(o, acc[r], col, a.B);
-                }
-        }
+        for (int r = 0; r < MT; ++r)
+            if ((uint32_t)r < rows) store_any<VEC>(a.out + obase + (uint64_t)r * a.pitch, acc[r], col, a.B, nd);
     }
 }
 
 // ---------------------------------------------------------------------------------------------------
-// (A4/A5/A8/A11) group-tile perm-MAC kernel: the primary path for shards up to 8 KiB.
-// One workgroup owns one shard group at a time.  It stages the group's K selected shards (or a chunk of
-// JS of them) into LDS with linear, coalesced 16-B loads -- a whole group of 20 x 1440 B is 225 complete
-// 128-B lines, so no line is fetched twice, unlike per-lane strided column reads whose 1-KiB wave
-// chunks straddle shard boundaries -- then every lane computes one 8-byte column of the MT output rows
-// from LDS.  The coefficient tables of the chunk are expanded into LDS once per group (decode) or once
-// per kernel (encode) and read back with broadcast ds_read_b128.
+// (A11) syndrome-form decode MAC for R <= 8.
+// The selected shares are every present data shard plus the m parity shares P_t (fecpp.cpp:528-548), and
+// the recovered shards are D_M = Sinv * (P - E_P,present * D_present), where E is the parity part of the
+// encoding matrix and Sinv the m x m inverse computed by the prep kernel.  Per column:
+//   y_r = parity_r ^ XOR_{j present} E[r][j] * D_j     for every parity row r < RT  (the encode loop, with
+//         the SAME wave-uniform tables for every group: scalar loads, no LDS, no pointer gather; a missing
+//         data shard is simply not loaded, a parity row that is not used is not loaded)
+//   out_u = XOR_r C[u][r] * y_r                         C[u][P_t - K] = Sinv[u][t], 0 for unused rows
+// so the only per-group coefficients are the RT x RT bytes of C (LDS, built per workgroup).  Expanding the
+// coefficient form instead (K x m per-group tables and share pointers in LDS before the first load) kept
+// decode ~5-10% behind encode.  A group with nothing to recover (m = 0, the zero-loss case of
+// fec_find_missings, client.cpp:923-925) issues no loads and no stores; a wave of such groups skips the loop.
+// The product is the same linear map of the same shares as the reference's K x K inverse, so the bytes are
+// the reference's.
 // ---------------------------------------------------------------------------------------------------
-struct LdsArgs {
-    const uint8_t *data;    // [G][K][pitch]
-    const uint8_t *parity;  // [G][R][pitch]
-    uint8_t *out;           // encode: parity, decode: recovered [G][R][pitch]
-    const uint8_t *enc;     // N x K (encode)
-    const uint8_t *rec;     // per-group records (decode)
+struct SynArgs {
+    const uint8_t *data;      // [G][K][pitch]
+    const uint8_t *parity;    // [G][R][pitch]
+    uint8_t *out;             // [G][R][pitch] recovered data shards, ascending index
+    const uint8_t *rec;       // syndrome-form records (kfec_internal.hpp)
+    const uint64_t *present;  // [G][4]
+    const uint32_t *etab;     // [K][etab_rows][5] perm tables of the parity rows (zero slack rows)
     uint64_t pitch;
-    uint32_t G, K, R, B;
-    uint32_t rec_stride;
-    uint32_t JS;            // shards staged per chunk
-    uint32_t Bs;            // LDS row stride of a staged shard (multiple of 16, >= B)
-    uint32_t cols;          // 8-byte columns = ceil(B / 8)
-    uint64_t bs_inv;        // ceil(2^32 / Bs): o / Bs for staged offsets o < 2^16 without a divide
-    uint32_t tbl_all;       // encode: tables of all K shards stay in LDS for the whole kernel
+    uint32_t total, cols, G, K, R, B, rec_stride, etab_rows;
 };
 
-template <int MT>
-struct TileLayout {
-    static constexpr int T4 = (MT + 3) / 4 * 4;
-    static constexpr int TBL = MT * 16 + T4 * 4;  // per shard: [MT][t0..t3] then t4[MT] (padded to 16 B)
+template <int RT>
+struct SynLayout {
+    static constexpr int TD = ((5 * RT + 3) / 4) * 4;  // table dwords per (group, output row u): RT tables
 };
 
-// expand coefficient tables of shards [c0, c0+nj) for rows [row0, row0+MT) of group g into LDS
-template <int MT, bool DEC>
-__device__ __forceinline__ void tile_expand(const LdsArgs &a, uint8_t *s_tbl, uint32_t g, uint32_t c0, uint32_t nj,
-                                            uint32_t row0, uint32_t m)
+template <int VEC, int RT, int PDX = 0>
+__global__ void __launch_bounds__(kMacBlock, KFEC_MINW) syn_kernel(SynArgs a)
 {
-    using L = TileLayout<MT>;
-    for (uint32_t e = threadIdx.x; e < nj * MT; e += blockDim.x) {
-        const uint32_t r = e % MT, jj = e / MT, j = c0 + jj, u = row0 + r;
-        uint32_t c = 0;
-        if constexpr (DEC) {
-            if (u < m) c = a.rec[(uint64_t)g * a.rec_stride + 4 + ((a.K + 3) & ~3u) * (1 + u) + j];
-        } else {
-            if (u < a.R) c = a.enc[(uint64_t)(a.K + u) * a.K + j];
-        }
+    constexpr int W = Gran<VEC>::W;
+    constexpr int PD = PDX ? PDX : (VEC >= 32 ? KFEC_PD / 2 : KFEC_PD);
+    constexpr int VB = VEC >= 4 ? VEC : 4;
+    constexpr int TD = SynLayout<RT>::TD;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ct[];  // [gmax][RT][TD]
+
+    const uint32_t base = blockIdx.x * kMacBlock;
+    const uint32_t cols = a.cols, K = a.K;
+    const uint32_t gfirst = base / cols;
+    const uint32_t glast = min(base + kMacBlock - 1, a.total - 1) / cols;
+    const uint32_t ng = glast - gfirst + 1;
+    // C tables of the workgroup's groups (zero for a group that recovers nothing)
+    for (uint32_t e = threadIdx.x; e < ng * RT * RT; e += kMacBlock) {
+        const uint32_t gs = e / (RT * RT), ur = e - gs * (RT * RT), u = ur / RT, r = ur - u * RT;
+        const uint8_t *rec = a.rec + (uint64_t)(gfirst + gs) * a.rec_stride;
         uint32_t t[5];
-        gf_perm_tables(c, t);
-        uint8_t *base = s_tbl + jj * L::TBL;
-        *reinterpret_cast<uint4 *>(base + r * 16) = make_uint4(t[0], t[1], t[2], t[3]);
-        reinterpret_cast<uint32_t *>(base + MT * 16)[r] = t[4];
+        gf_perm_tables(rec[0] == 0 ? rec[8 + 8 * u + r] : 0u, t);
+        uint32_t *tp = s_ct + (gs * RT + u) * TD + 5 * r;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) tp[i] = t[i];
     }
-}
 
-template <int SV>
-__device__ __forceinline__ void stage_copy(uint8_t *dst, const uint8_t *src)
-{
-    if constexpr (SV == 16) *reinterpret_cast<uint4 *>(dst) = *reinterpret_cast<const uint4 *>(src);
-    else if constexpr (SV == 8) *reinterpret_cast<uint2 *>(dst) = *reinterpret_cast<const uint2 *>(src);
-    else if constexpr (SV == 4) *reinterpret_cast<uint32_t *>(dst) = *reinterpret_cast<const uint32_t *>(src);
-    else *dst = *src;
-}
-
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-
-// One work unit = (group g, chunk of shards [c0, c0+nj)).  Stage a unit into an LDS buffer of JS rows of
-// Bs bytes.  SV == 16: LDS-DMA (global_load_lds_dwordx4): each wave-instruction fills 1 KiB of LDS
-// contiguously while every lane names its own 16-B source -- a gather of shard rows; asynchronous, no
-// VGPRs, completion awaited by the next s_waitcnt vmcnt(0) + barrier.  Other SV (pitch not 16-aligned):
-// synchronous register staging.
-template <int SV, bool DEC>
-__device__ __forceinline__ void tile_stage(const LdsArgs &a, uint8_t *buf, uint32_t g, uint32_t c0, uint32_t nj)
-{
-    const uint32_t K = a.K;
-    auto shard_src = [&](uint32_t jj) -> const uint8_t * {
-        if constexpr (DEC) {
-            const uint32_t sid = a.rec[(uint64_t)g * a.rec_stride + 4 + c0 + jj];
-            return (sid < K) ? a.data + ((uint64_t)g * K + sid) * a.pitch
-                             : a.parity + ((uint64_t)g * a.R + (sid - K)) * a.pitch;
-        } else {
-            return a.data + ((uint64_t)g * K + c0 + jj) * a.pitch;
-        }
-    };
-    if constexpr (SV == 16) {
-        const uint32_t bytes = nj * a.Bs;
-        const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-        for (uint32_t ch = wave; ch * 1024 < bytes; ch += nw) {
-            const uint32_t o = ch * 1024 + lane * 16;
-            const uint32_t jj = (uint32_t)(((uint64_t)o * a.bs_inv) >> 32), off = o - jj * a.Bs;  // o / Bs
-            (void)off;  // read only in the device pass
-            if (o < bytes) {
-#if defined(__HIP_DEVICE_COMPILE__)  // the builtin exists only in the device pass of this single-source file
-                __builtin_amdgcn_global_load_lds(shard_src(jj) + off,
-                                                 (__attribute__((address_space(3))) void *)(buf + ch * 1024), 16, 0, 0);
-#endif
-            }
-        }
-    } else {
-        const uint32_t gps = a.Bs / SV;  // granules per staged row (rows padded to 16 B)
-        const uint32_t total = nj * gps;
-        constexpr int NB = 8;
-        for (uint32_t base = threadIdx.x; base < total; base += NB * blockDim.x) {
-            uint8_t v[NB][SV];
-#pragma unroll
-            for (int k = 0; k < NB; ++k) {
-                const uint32_t gi = base + k * blockDim.x;
-                if (gi < total) {
-                    const uint32_t jj = gi / gps, off = (gi - jj * gps) * SV;
-                    if (off < a.B) {
-                        const uint8_t *src = shard_src(jj) + off;
-                        if constexpr (SV == 8) *reinterpret_cast<uint2 *>(v[k]) = *reinterpret_cast<const uint2 *>(src);
-                        else if constexpr (SV == 4) *reinterpret_cast<uint32_t *>(v[k]) = *reinterpret_cast<const uint32_t *>(src);
-                        else v[k][0] = *src;
-                    }
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < NB; ++k) {
-                const uint32_t gi = base + k * blockDim.x;
-                if (gi < total) {
-                    const uint32_t jj = gi / gps, off = (gi - jj * gps) * SV;
-                    uint8_t *dst = buf + jj * a.Bs + off;
-                    if constexpr (SV == 8) *reinterpret_cast<uint2 *>(dst) = *reinterpret_cast<uint2 *>(v[k]);
-                    else if constexpr (SV == 4) *reinterpret_cast<uint32_t *>(dst) = *reinterpret_cast<uint32_t *>(v[k]);
-                    else *dst = v[k][0];
-                }
-            }
+    const uint32_t item = base + threadIdx.x;
+    const bool in = item < a.total;
+    const uint32_t g = in ? item / cols : gfirst;
+    const uint32_t col = in ? item - g * cols : 0;
+    const uint32_t nd = (VEC >= 4 && (col + 1) * VB > a.B) ? (a.B - col * VB + 3) / 4 : (uint32_t)W;
+    uint32_t m = 0, used = 0;
+    if (in) {
+        const uint32_t h = *reinterpret_cast<const uint32_t *>(a.rec + (uint64_t)g * a.rec_stride);
+        if ((h & 0xFFu) == 0) {
+            m = (h >> 8) & 0xFFu;
+            used = (h >> 16) & 0xFFu;
         }
     }
-}
+    const bool active = m > 0;
+    uint32_t acc[RT][W];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int w = 0; w < W; ++w) acc[r][w] = 0;
 
-// acc[r] ^= coef(r, jj) * x over one 8-byte column, tables at tb (TileLayout)
-template <int MT>
-__device__ __forceinline__ void tile_mac(u32x2_t (&acc)[MT], u32x2_t x, const uint8_t *tb)
-{
-    using L = TileLayout<MT>;
-    uint32_t t4[L::T4];
+    if (active) {
+        const uint64_t *pr = a.present + (uint64_t)g * 4;
+        const uint64_t p0 = pr[0];
+        const uint64_t p1 = K > 64 ? pr[1] : 0ull, p2 = K > 128 ? pr[2] : 0ull, p3 = K > 192 ? pr[3] : 0ull;
+        auto has = [&](uint32_t j) -> bool {
+            const uint64_t wq = j < 64 ? p0 : (j < 128 ? p1 : (j < 192 ? p2 : p3));
+            return (wq >> (j & 63u)) & 1ull;
+        };
+        const uint8_t *dbase = a.data + ((uint64_t)g * K) * a.pitch + (uint64_t)col * VB;
+        auto ld = [&](uint32_t j) -> Gran<VEC> {
+            Gran<VEC> v;
 #pragma unroll
-    for (int q = 0; q < L::T4 / 4; ++q) {
-        const uint4 v = reinterpret_cast<const uint4 *>(tb + MT * 16)[q];
-        t4[4 * q] = v.x; t4[4 * q + 1] = v.y; t4[4 * q + 2] = v.z; t4[4 * q + 3] = v.w;
-    }
-    uint32_t s0[2], s1[2], s2[2];
+            for (int w = 0; w < W; ++w) v.d[w] = 0;
+            if (has(j)) v = load_any<VEC>(dbase + (uint64_t)j * a.pitch, col, a.B, nd);
+            return v;
+        };
+        Gran<VEC> x[PD];
 #pragma unroll
-    for (int w = 0; w < 2; ++w) {
-        s0[w] = x[w] & 0x07070707u;
-        s1[w] = (x[w] >> 3) & 0x07070707u;
-        s2[w] = (x[w] >> 6) & 0x03030303u;
-    }
+        for (int u = 0; u < PD; ++u)
+            if ((uint32_t)u < K) x[u] = ld(u);
+        typedef const __attribute__((address_space(4))) uint32_t cu32;  // uniform: scalar loads into SGPRs
+        for (uint32_t jb = 0; jb < K; jb += PD) {
 #pragma unroll
-    for (int r = 0; r < MT; ++r) {
-        const uint4 v = reinterpret_cast<const uint4 *>(tb)[r];
-        const uint32_t t[5] = {v.x, v.y, v.z, v.w, t4[r]};
-#if KFEC_ABLATE == 1
-        acc[r][0] ^= x[0] ^ t[0];
-        acc[r][1] ^= x[1] ^ t[4];
-#else
+            for (int u = 0; u < PD; ++u) {
+                const uint32_t j = jb + u;
+                if (j < K) {
+                    const Gran<VEC> cur = x[u];
+                    if (j + PD < K) x[u] = ld(j + PD);
+                    const cu32 *tg = (const cu32 *)(a.etab + (size_t)j * a.etab_rows * 5);
+                    uint32_t t[5 * RT];
 #pragma unroll
-        for (int w = 0; w < 2; ++w) acc[r][w] = perm_mac(acc[r][w], t, s0[w], s1[w], s2[w]);
-#endif
-    }
-}
-
-// as tile_mac, with the shard's tables already in registers (TileLayout order)
-template <int MT>
-__device__ __forceinline__ void tile_mac_regs(u32x2_t (&acc)[MT], u32x2_t x, const uint4 *tv)
-{
-    using L = TileLayout<MT>;
-    const uint32_t *t4 = reinterpret_cast<const uint32_t *>(tv + MT);
-    uint32_t s0[2], s1[2], s2[2];
+                    for (int i = 0; i < 5 * RT; ++i) t[i] = tg[i];
 #pragma unroll
-    for (int w = 0; w < 2; ++w) {
-        s0[w] = x[w] & 0x07070707u;
-        s1[w] = (x[w] >> 3) & 0x07070707u;
-        s2[w] = (x[w] >> 6) & 0x03030303u;
-    }
+                    for (int w = 0; w < W; ++w) {
+                        const uint32_t xv = cur.d[w];
+                        const uint32_t s0 = xv & 0x07070707u;
+                        const uint32_t s1 = (xv >> 3) & 0x07070707u;
+                        const uint32_t s2 = (xv >> 6) & 0x03030303u;
 #pragma unroll
-    for (int r = 0; r < MT; ++r) {
-        const uint32_t t[5] = {tv[r].x, tv[r].y, tv[r].z, tv[r].w, t4[r]};
-#if KFEC_ABLATE == 1
-        acc[r][0] ^= x[0] ^ t[0];
-        acc[r][1] ^= x[1] ^ t[4];
-#else
-#pragma unroll
-        for (int w = 0; w < 2; ++w) acc[r][w] = perm_mac(acc[r][w], t, s0[w], s1[w], s2[w]);
-#endif
-    }
-    (void)sizeof(L);
-}
-
-// Persistent workgroup walking its (group, chunk) units through a 2-deep LDS ring: the DMA of unit u+1
-// is in flight while unit u is computed.  Tables (and, for encode with few shards, the whole table set)
-// live beside the ring.
-template <int MT, bool DEC, int SV>
-__global__ void __launch_bounds__(256) mac_tile_kernel(LdsArgs a)
-{
-    using L = TileLayout<MT>;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t K = a.K, JS = a.JS, row0 = blockIdx.y * MT;
-    const uint32_t nch = (K + JS - 1) / JS;  // chunks per group
-    // LDS carve-up as integer offsets from smem: selecting between two pointers at run time makes hipcc
-    // lose the LDS address space and emit flat loads for the whole compute loop
-    const uint32_t ring_sz = JS * a.Bs, tbl0 = 2 * ring_sz, tring_sz = JS * L::TBL;
-    uint8_t *tbl_base = smem + tbl0;
-    // encode tables for all K shards fit once (enc_all) or are expanded per unit into a 2-deep ring
-    const bool enc_all = !DEC && a.tbl_all;
-
-    // rows of this workgroup's tile for group g; 0 = nothing to do for g
-    auto rows_of = [&](uint32_t g) -> uint32_t {
-        if constexpr (DEC) {
-            const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
-            const uint32_t st = rec[0], m = rec[1];
-            return (st == 0 && m > row0) ? min((uint32_t)MT, m - row0) : 0u;
-        } else {
-            return a.R > row0 ? min((uint32_t)MT, a.R - row0) : 0u;
-        }
-    };
-    auto m_of = [&](uint32_t g) -> uint32_t {
-        if constexpr (DEC) return a.rec[(uint64_t)g * a.rec_stride + 1];
-        else return 0u;
-    };
-    // first group at or after g with work for this tile
-    auto next_group = [&](uint32_t g) -> uint32_t {
-        while (g < a.G && rows_of(g) == 0) g += gridDim.x;
-        return g;
-    };
-
-    if (enc_all) tile_expand<MT, false>(a, tbl_base, 0, 0, K, row0, 0);
-
-    uint32_t g = next_group(blockIdx.x), c = 0;
-    if (g >= a.G) return;
-    // prologue: unit (g, 0) into slot 0
-    if (!enc_all) tile_expand<MT, DEC>(a, smem + tbl0, g, 0, min(JS, K), row0, m_of(g));
-    tile_stage<SV, DEC>(a, smem, g, 0, min(JS, K));
-    uint32_t slot = 0, rows = rows_of(g);
-    u32x2_t acc[MT];
-#pragma unroll
-    for (int r = 0; r < MT; ++r) acc[r] = u32x2_t{0u, 0u};
-    const uint32_t col = threadIdx.x;
-    while (true) {
-        // the unit after (g, c)
-        uint32_t gn = g, cn = c + 1;
-        if (cn == nch) {
-            cn = 0;
-            gn = next_group(g + gridDim.x);
-        }
-        if constexpr (SV == 16) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // unit (g, c) has landed in ring[slot]; everyone is done with ring[slot ^ 1]
-        if (gn < a.G) {
-            const uint32_t njn = min(JS, K - cn * JS);
-            if (!enc_all) tile_expand<MT, DEC>(a, smem + tbl0 + (slot ^ 1) * tring_sz, gn, cn * JS, njn, row0, m_of(gn));
-            tile_stage<SV, DEC>(a, smem + (slot ^ 1) * ring_sz, gn, cn * JS, njn);
-        }
-        const uint32_t nj = min(JS, K - c * JS);
-        const uint32_t tb_off = enc_all ? tbl0 + c * JS * L::TBL : tbl0 + slot * tring_sz;
-        if (col < a.cols) {
-            const uint8_t *tb = smem + tb_off;
-            const uint8_t *xs = smem + slot * ring_sz + col * 8;
-            for (uint32_t jj = 0; jj < nj; ++jj)
-                tile_mac<MT>(acc, *reinterpret_cast<const u32x2_t *>(xs + jj * a.Bs), tb + jj * L::TBL);
-        }
-        if (c + 1 == nch) {  // group finished: store its rows
-            if (col < a.cols) {
-                const uint64_t obase = ((uint64_t)g * a.R + row0) * a.pitch + (uint64_t)col * 8;
-#pragma unroll
-                for (int r = 0; r < MT; ++r) {
-                    if ((uint32_t)r < rows) {
-                        uint8_t *o = a.out + obase + (uint64_t)r * a.pitch;
-                        if constexpr (SV >= 8) {
-                            *reinterpret_cast<u32x2_t *>(o) = acc[r];
-                        } else if constexpr (SV == 4) {
-                            // pitch is only 4-aligned: the second dword may lie past the slot's pitch
-                            *reinterpret_cast<uint32_t *>(o) = acc[r][0];
-                            if (col * 8 + 4 < a.B) *reinterpret_cast<uint32_t *>(o + 4) = acc[r][1];
-                        } else {
-#pragma unroll
-                            for (int b = 0; b < 8; ++b)
-                                if (col * 8 + b < a.B) o[b] = (uint8_t)(acc[r][b >> 2] >> (8 * (b & 3)));
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < MT; ++r) acc[r] = u32x2_t{0u, 0u};
-            if (gn >= a.G) break;
-            rows = rows_of(gn);
-        }
-        g = gn;
-        c = cn;
-        slot ^= 1;
-    }
-}
-
-// ---------------------------------------------------------------------------------------------------
-// (A4/A5/A8/A11) wave-tile kernel: the primary path for 16-B aligned layouts, B <= 2 KiB, R <= 8.
-// One workgroup = one wave, persistent over its groups.  A group is streamed in chunks of JS shards
-// (20 x 1440 B -> chunks of 8, 8, 4 shards = 90, 90, 45 whole 128-B lines): every wave-instruction
-// loads 1 KiB of consecutive bytes, so each line is requested exactly once (per-lane column loads make
-// the L2 fetch the lines that straddle two shards twice: +12% DRAM reads, measured).  The chunk lands
-// in VGPRs (up to 12 x 16 B per lane), is written to the wave's private LDS tile, and the next chunk's
-// loads are issued before the current one is computed, so ~12 chunks (~135 KiB) are in flight per CU.
-// Each lane computes 16-byte columns l and l + 64 of the MT output rows from LDS.  No barriers: the
-// only LDS hazards are inside one wave (s_waitcnt lgkmcnt + wave barrier).
-// ---------------------------------------------------------------------------------------------------
-static constexpr int kWtLoads = 12;  // max 16-B loads per lane per chunk (12 KiB chunks)
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs
-
-struct WtArgs {
-    const uint8_t *data, *parity;
-    uint8_t *out;
-    const uint8_t *enc, *rec;
-    uint64_t pitch;
-    uint32_t G, K, R, B;
-    uint32_t rec_stride;
-    uint32_t JS, nch;       // shards per chunk, chunks per group
-    uint32_t Bs;            // staged row stride in LDS (B rounded up to 16)
-    uint32_t cols;          // 16-B columns = ceil(B / 16) (<= 128)
-    uint64_t bs_inv;        // ceil(2^32 / Bs)
-};
-
-// issue the loads of chunk c of group g into pf; `base` = this lane's shard base address for g (lane j
-// holds shard j's), shuffled to the lanes that need it
-template <bool DEC>
-__device__ __forceinline__ void wt_issue(const WtArgs &a, u32x4_t (&pf)[kWtLoads], uint32_t g, uint32_t c, uint64_t base)
-{
-    const uint32_t K = a.K, lane = threadIdx.x;
-    const uint32_t c0 = c * a.JS, nj = min(a.JS, K - c0), bytes = nj * a.Bs;
-#pragma unroll
-    for (int i = 0; i < kWtLoads; ++i) {
-        const uint32_t o = i * 1024 + lane * 16;
-        const uint32_t oc = min(o, bytes - 1);
-        const uint32_t jj = (uint32_t)(((uint64_t)oc * a.bs_inv) >> 32), off = oc - jj * a.Bs;
-        uint64_t sb;
-        if (K <= 64) {
-            sb = __shfl(base, (int)(c0 + jj));
-        } else {
-            uint32_t sid = c0 + jj;
-            if constexpr (DEC) sid = a.rec[(uint64_t)g * a.rec_stride + 4 + c0 + jj];
-            sb = reinterpret_cast<uint64_t>((sid < K) ? a.data + ((uint64_t)g * K + sid) * a.pitch
-                                                      : a.parity + ((uint64_t)g * a.R + (sid - K)) * a.pitch);
-        }
-        if (o < bytes) pf[i] = *reinterpret_cast<const u32x4_t *>(reinterpret_cast<const uint8_t *>(sb) + off);
-    }
-}
-
-template <int MT, bool DEC>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) mac_wave_kernel(WtArgs a)
-{
-    using L = TileLayout<MT>;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t K = a.K, JS = a.JS, nch = a.nch, lane = threadIdx.x;
-    uint8_t *tile = smem;                              // JS rows of Bs bytes
-    uint8_t *tbl = smem + ((JS * a.Bs + 15) & ~15u);   // K x TBL coefficient tables
-    const uint32_t K4 = (K + 3) & ~3u;
-
-    auto rows_of = [&](uint32_t g) -> uint32_t {
-        if constexpr (DEC) {
-            const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
-            return rec[0] == 0 ? min((uint32_t)MT, (uint32_t)rec[1]) : 0u;
-        } else {
-            return min((uint32_t)MT, a.R);
-        }
-    };
-    auto next_group = [&](uint32_t g) -> uint32_t {
-        if constexpr (DEC)
-            while (g < a.G && rows_of(g) == 0) g += gridDim.x;
-        return g;
-    };
-    // shard base addresses of group g, lane j holds shard j's (decode: the selected share)
-    auto shard_base = [&](uint32_t g) -> uint64_t {
-        uint64_t p = 0;
-        if (lane < K) {
-            uint32_t sid = lane;
-            if constexpr (DEC) sid = a.rec[(uint64_t)g * a.rec_stride + 4 + lane];
-            p = reinterpret_cast<uint64_t>((sid < K) ? a.data + ((uint64_t)g * K + sid) * a.pitch
-                                                     : a.parity + ((uint64_t)g * a.R + (sid - K)) * a.pitch);
-        }
-        return p;
-    };
-    u32x4_t pf[kWtLoads];
-    auto expand = [&](uint32_t g) {
-        uint32_t m = a.R;
-        const uint8_t *rec = nullptr;
-        if constexpr (DEC) {
-            rec = a.rec + (uint64_t)g * a.rec_stride;
-            m = rec[1];
-        }
-        for (uint32_t e = lane; e < K * MT; e += 64) {
-            const uint32_t r = e % MT, j = e / MT;
-            uint32_t cf = 0;
-            if constexpr (DEC) {
-                if (r < m) cf = rec[4 + K4 * (1 + r) + j];
-            } else {
-                if (r < a.R) cf = a.enc[(uint64_t)(K + r) * K + j];
-            }
-            uint32_t t[5];
-            gf_perm_tables(cf, t);
-            *reinterpret_cast<uint4 *>(tbl + j * L::TBL + r * 16) = make_uint4(t[0], t[1], t[2], t[3]);
-            reinterpret_cast<uint32_t *>(tbl + j * L::TBL + MT * 16)[r] = t[4];
-        }
-    };
-
-    uint32_t g = next_group(blockIdx.x);
-    if (g >= a.G) return;
-    if constexpr (!DEC) expand(0);
-    uint64_t base = shard_base(g);
-    wt_issue<DEC>(a, pf, g, 0, base);
-    uint32_t c = 0, rows = rows_of(g);
-    uint32_t accw[2][MT][4];
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int r = 0; r < MT; ++r)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) accw[p][r][w] = 0;
-    bool need_tables = DEC;
-    while (true) {
-        // the chunk in pf has landed (the compiler waits on first use): stage it into the LDS tile
-        const uint32_t c0 = c * JS, nj = min(JS, K - c0), bytes = nj * a.Bs;
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous chunk's tile reads are done
-#pragma unroll
-        for (int i = 0; i < kWtLoads; ++i) {
-            const uint32_t o = i * 1024 + lane * 16;
-            if (o < bytes) *reinterpret_cast<u32x4_t *>(tile + o) = pf[i];
-        }
-        if (need_tables) {
-            expand(g);
-            need_tables = false;
-        }
-        // next unit, and its loads, before computing this one
-        uint32_t gn = g, cn = c + 1;
-        if (cn == nch) {
-            cn = 0;
-            gn = next_group(g + gridDim.x);
-        }
-        uint64_t nbase = base;
-        if (gn < a.G) {
-            if (gn != g) nbase = shard_base(gn);
-            wt_issue<DEC>(a, pf, gn, cn, nbase);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        // compute chunk (g, c) from the tile
-        for (uint32_t jj = 0; jj < nj; ++jj) {
-            const uint8_t *tb = tbl + (c0 + jj) * L::TBL;
-            uint4 tv[L::TBL / 16];
-#pragma unroll
-            for (int q = 0; q < L::TBL / 16; ++q) tv[q] = reinterpret_cast<const uint4 *>(tb)[q];
-            const uint32_t *t4 = reinterpret_cast<const uint32_t *>(tv + MT);
-#pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                const uint32_t col = lane + 64 * p;
-                if (p == 1 && col >= a.cols) break;
-                const uint4 xv = *reinterpret_cast<const uint4 *>(tile + jj * a.Bs + col * 16);
-                const uint32_t x[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    const uint32_t s0 = x[w] & 0x07070707u, s1 = (x[w] >> 3) & 0x07070707u, s2 = (x[w] >> 6) & 0x03030303u;
-#pragma unroll
-                    for (int r = 0; r < MT; ++r) {
-                        const uint32_t t[5] = {tv[r].x, tv[r].y, tv[r].z, tv[r].w, t4[r]};
-#if KFEC_ABLATE == 1
-                        accw[p][r][w] ^= x[w] ^ t[0];
-                        (void)s0; (void)s1; (void)s2;
-#else
-                        accw[p][r][w] = perm_mac(accw[p][r][w], t, s0, s1, s2);
-#endif
+                        for (int r = 0; r < RT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
                     }
                 }
             }
         }
-        if (c + 1 == nch) {  // group done: store its rows, 16 B per lane and column
-            const uint64_t obase = (uint64_t)g * a.R * a.pitch;
+        // the parity shares of the rows in use
 #pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                const uint32_t col = lane + 64 * p;
-                if (col < a.cols) {
+        for (int r = 0; r < RT; ++r) {
+            if ((used >> r) & 1u) {
+                const Gran<VEC> y =
+                    load_any<VEC>(a.parity + ((uint64_t)g * a.R + r) * a.pitch + (uint64_t)col * VB, col, a.B, nd);
 #pragma unroll
-                    for (int r = 0; r < MT; ++r)
-                        if ((uint32_t)r < rows) {
-                            __builtin_nontemporal_store(u32x4_t{accw[p][r][0], accw[p][r][1], accw[p][r][2], accw[p][r][3]},
-                                                        reinterpret_cast<u32x4_t *>(a.out + obase + (uint64_t)r * a.pitch + col * 16));
-                        }
-                }
-#pragma unroll
-                for (int r = 0; r < MT; ++r)
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) accw[p][r][w] = 0;
+                for (int w = 0; w < W; ++w) acc[r][w] ^= y.d[w];
             }
-            if (gn >= a.G) break;
-            rows = rows_of(gn);
-            need_tables = DEC;
-        }
-        g = gn;
-        c = cn;
-        base = nbase;
-    }
-}
-
-// ---------------------------------------------------------------------------------------------------
-// (A4/A5/A8/A11) stream engine: one persistent workgroup per CU, role-split waves.
-//   loader waves (kEngNL) gather whole groups (or chunks of JS shards) into a kEngS-slot LDS ring with
-//     LDS-DMA (global_load_lds_dwordx4, per-lane 16-B sources, 1 KiB of LDS per wave-instruction).
-//     A group of 20 x 1440 B is 225 complete 128-B lines, so no line is fetched twice.  Each loader owns
-//     units u = w, w + NL, ...: waits for the slot to be free, issues all its DMAs, waits vmcnt(0),
-//     publishes the slot.  Several units are in flight per CU at any time.
-//   consumer teams (2 x kEngTW waves) take alternate groups; each lane owns one 8-byte column and
-//     accumulates its MT output rows over the group's chunks, then stores them (non-temporal).
-//   Hand-off: LDS counters filled[s] (fill generation) and consumed[s] (consumer waves done), workgroup-
-//   scope release/acquire.  Every spin is bounded: on timeout the wave sets a flag and leaves, so a bug
-//   can never hang the GPU (outputs would then fail verification).
-// ---------------------------------------------------------------------------------------------------
-static constexpr int kEngS = 5;     // ring slots
-static constexpr int kEngNL = 3;    // loader waves
-static constexpr int kEngTW = 4;    // waves per consumer team (256 lanes: one 8-byte column each)
-static constexpr int kEngThreads = (kEngNL + 2 * kEngTW) * 64;
-static constexpr uint32_t kSpinMax = 1u << 22;
-
-struct StreamArgs {
-    const uint8_t *data, *parity;
-    uint8_t *out;
-    const uint8_t *enc, *rec;
-    uint32_t *err;          // device word: set non-zero if a spin timed out
-    uint64_t pitch;
-    uint32_t G, K, R, B;
-    uint32_t rec_stride;
-    uint32_t JS, nch;       // shards per unit, units per group
-    uint32_t Bs;            // LDS row stride (B rounded up to 16)
-    uint32_t slot_bytes;    // JS * Bs rounded up to 1 KiB
-    uint32_t cols;          // 8-byte columns = ceil(B / 8)
-    uint64_t bs_inv;        // ceil(2^32 / Bs)
-};
-
-__device__ __forceinline__ uint32_t lds_load_acq(uint32_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// wait until *p >= target; false on timeout
-__device__ __forceinline__ bool spin_ge(uint32_t *p, uint32_t target)
-{
-    for (uint32_t i = 0; i < kSpinMax; ++i) {
-        if (lds_load_acq(p) >= target) return true;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-
-template <int MT, bool DEC>
-__global__ void __launch_bounds__(kEngThreads) mac_stream_kernel(StreamArgs a)
-{
-    using L = TileLayout<MT>;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t K = a.K, JS = a.JS, nch = a.nch;
-    // LDS: [S slots][tables: encode K*TBL once | decode S*JS*TBL][filled[S], consumed[S]]
-    const uint32_t tbl0 = kEngS * a.slot_bytes;
-    const uint32_t tbl_bytes = DEC ? kEngS * JS * L::TBL : K * L::TBL;
-    uint32_t *filled = reinterpret_cast<uint32_t *>(smem + tbl0 + tbl_bytes);
-    uint32_t *consumed = filled + kEngS;
-
-    if (threadIdx.x < kEngS) {
-        filled[threadIdx.x] = 0;
-        consumed[threadIdx.x] = 0;
-    }
-    if constexpr (!DEC) {  // encode tables of all K shards, once
-        for (uint32_t e = threadIdx.x; e < K * MT; e += blockDim.x) {
-            const uint32_t r = e % MT, j = e / MT;
-            const uint32_t cf = (r < a.R) ? a.enc[(uint64_t)(K + r) * K + j] : 0u;
-            uint32_t t[5];
-            gf_perm_tables(cf, t);
-            uint8_t *tb = smem + tbl0 + j * L::TBL;
-            *reinterpret_cast<uint4 *>(tb + r * 16) = make_uint4(t[0], t[1], t[2], t[3]);
-            reinterpret_cast<uint32_t *>(tb + MT * 16)[r] = t[4];
         }
     }
-    __syncthreads();
-
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t my_groups = a.G > blockIdx.x ? (a.G - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
-    const uint32_t n_units = my_groups * nch;
-
-    if (wave < kEngNL) {
-        // ---------------- loader ----------------
-        for (uint32_t u = wave; u < n_units; u += kEngNL) {
-            const uint32_t k = u / nch, c = u - k * nch, g = blockIdx.x + k * gridDim.x;
-            const uint32_t s = u % kEngS, f = u / kEngS;
-            if (!spin_ge(&consumed[s], kEngTW * f)) {
-                if (lane == 0) atomicOr(a.err, 1u);
-                return;
-            }
-            const uint32_t c0 = c * JS, nj = min(JS, K - c0);
-            [[maybe_unused]] uint8_t *slot = smem + s * a.slot_bytes;  // read only in the device pass
-            bool work = true;
-            const uint8_t *rec = nullptr;
-            if constexpr (DEC) {
-                rec = a.rec + (uint64_t)g * a.rec_stride;
-                const uint32_t st = rec[0], m = rec[1];
-                work = (st == 0 && m > 0);
-                if (work) {
-                    uint8_t *tb = smem + tbl0 + s * JS * L::TBL;
-                    for (uint32_t e = lane; e < nj * MT; e += 64) {
-                        const uint32_t r = e % MT, jj = e / MT;
-                        const uint32_t cf = (r < m) ? rec[4 + ((K + 3) & ~3u) * (1 + r) + c0 + jj] : 0u;
-                        uint32_t t[5];
-                        gf_perm_tables(cf, t);
-                        *reinterpret_cast<uint4 *>(tb + jj * L::TBL + r * 16) = make_uint4(t[0], t[1], t[2], t[3]);
-                        reinterpret_cast<uint32_t *>(tb + jj * L::TBL + MT * 16)[r] = t[4];
-                    }
+    __syncthreads();  // C tables
+    if (active) {
+        const uint32_t *ct = s_ct + (g - gfirst) * RT * TD;
+        const uint64_t obase = ((uint64_t)g * a.R) * a.pitch + (uint64_t)col * VB;
+#pragma unroll
+        for (int u = 0; u < RT; ++u) {
+            if ((uint32_t)u < m) {
+                uint32_t t[TD];
+                const uint4 *tv = reinterpret_cast<const uint4 *>(ct + u * TD);
+#pragma unroll
+                for (int i = 0; i < TD / 4; ++i) {
+                    const uint4 q = tv[i];
+                    t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
                 }
-            }
-            if (work) {
-                // shard base addresses of this unit, one per lane (nj <= 64 is not required: lanes
-                // beyond 64 shards fall back to a direct lookup), fetched with one coalesced load
-                uint64_t my_base = 0;
-                if constexpr (DEC) {
-                    if (lane < nj) {
-                        const uint32_t sid = rec[4 + c0 + lane];
-                        my_base = reinterpret_cast<uint64_t>((sid < K) ? a.data + ((uint64_t)g * K + sid) * a.pitch
-                                                                       : a.parity + ((uint64_t)g * a.R + (sid - K)) * a.pitch);
+                uint32_t o[W];
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int r = 0; r < RT; ++r) {
+                        const uint32_t yv = acc[r][w];
+                        v = perm_mac(v, t + 5 * r, yv & 0x07070707u, (yv >> 3) & 0x07070707u, (yv >> 6) & 0x03030303u);
                     }
+                    o[w] = v;
                 }
-                const uint32_t bytes = nj * a.Bs;
-                for (uint32_t ch = 0; ch * 1024 < bytes; ++ch) {
-                    const uint32_t o = ch * 1024 + lane * 16;
-                    const uint32_t jj = (uint32_t)(((uint64_t)min(o, bytes - 1) * a.bs_inv) >> 32), off = o - jj * a.Bs;
-                    (void)off;  // read only in the device pass
-                    [[maybe_unused]] const uint8_t *src;
-                    if constexpr (DEC) {
-                        if (nj <= 64) {
-                            src = reinterpret_cast<const uint8_t *>(__shfl(my_base, (int)jj));
-                        } else {
-                            const uint32_t sid = rec[4 + c0 + jj];
-                            src = (sid < K) ? a.data + ((uint64_t)g * K + sid) * a.pitch
-                                            : a.parity + ((uint64_t)g * a.R + (sid - K)) * a.pitch;
-                        }
-                    } else {
-                        src = a.data + ((uint64_t)g * K + c0 + jj) * a.pitch;
-                    }
-                    if (o < bytes) {
-#if defined(__HIP_DEVICE_COMPILE__)
-                        __builtin_amdgcn_global_load_lds(src + off, (__attribute__((address_space(3))) void *)(slot + ch * 1024),
-                                                         16, 0, 0);
-#endif
-                    }
-                }
+                store_any<VEC>(a.out + obase + (uint64_t)u * a.pitch, o, col, a.B, nd);
             }
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_store(&filled[s], f + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        return;
-    }
-    // ---------------- consumer ----------------
-    const uint32_t team = (wave - kEngNL) / kEngTW, tw = (wave - kEngNL) % kEngTW;
-    const uint32_t col = tw * 64 + lane;
-    for (uint32_t k = team; k < my_groups; k += 2) {
-        const uint32_t g = blockIdx.x + k * gridDim.x;
-        uint32_t rows;
-        if constexpr (DEC) {
-            const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
-            const uint32_t st = rec[0], m = rec[1];
-            rows = (st == 0) ? min((uint32_t)MT, m) : 0u;
-        } else {
-            rows = min((uint32_t)MT, a.R);
-        }
-        u32x2_t acc[MT];
-#pragma unroll
-        for (int r = 0; r < MT; ++r) acc[r] = u32x2_t{0u, 0u};
-        for (uint32_t c = 0; c < nch; ++c) {
-            const uint32_t u = k * nch + c, s = u % kEngS, f = u / kEngS;
-            if (!spin_ge(&filled[s], f + 1)) {
-                if (lane == 0) atomicOr(a.err, 2u);
-                return;
-            }
-            const uint32_t c0 = c * JS, nj = min(JS, K - c0);
-            if (rows && col < a.cols) {
-                const uint8_t *xs = smem + s * a.slot_bytes + col * 8;
-                const uint8_t *tb = DEC ? smem + tbl0 + s * JS * L::TBL : smem + tbl0 + c0 * L::TBL;
-                // software pipeline: shard jj+1's data and tables are read while shard jj is computed
-                // (2 waves per SIMD cannot hide LDS latency by themselves)
-                u32x2_t xn = *reinterpret_cast<const u32x2_t *>(xs);
-                uint4 tn[L::TBL / 16];
-#pragma unroll
-                for (int q = 0; q < L::TBL / 16; ++q) tn[q] = reinterpret_cast<const uint4 *>(tb)[q];
-                for (uint32_t jj = 0; jj < nj; ++jj) {
-                    const u32x2_t x = xn;
-                    uint4 tc[L::TBL / 16];
-#pragma unroll
-                    for (int q = 0; q < L::TBL / 16; ++q) tc[q] = tn[q];
-                    if (jj + 1 < nj) {
-                        xn = *reinterpret_cast<const u32x2_t *>(xs + (jj + 1) * a.Bs);
-#pragma unroll
-                        for (int q = 0; q < L::TBL / 16; ++q)
-                            tn[q] = reinterpret_cast<const uint4 *>(tb + (jj + 1) * L::TBL)[q];
-                    }
-                    tile_mac_regs<MT>(acc, x, tc);
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_fetch_add(&consumed[s], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if (rows && col < a.cols) {
-            uint8_t *o = a.out + ((uint64_t)g * a.R) * a.pitch + (uint64_t)col * 8;
-#pragma unroll
-            for (int r = 0; r < MT; ++r)
-                if ((uint32_t)r < rows) __builtin_nontemporal_store(acc[r], reinterpret_cast<u32x2_t *>(o + (uint64_t)r * a.pitch));
         }
     }
 }
@@ -1669,103 +1107,19 @@ __global__ void __launch_bounds__(kEngThreads) mac_stream_kernel(StreamArgs a)
 // ---------------------------------------------------------------------------------------------------
 // host-side launch helpers
 // ---------------------------------------------------------------------------------------------------
-static int pick_vec(size_t pitch, std::initializer_list<const void *> ptrs)
-{
-#if KFEC_VEC32
-    {
-        bool ok = (pitch % 32) == 0;
-        for (const void *p : ptrs) ok = ok && (reinterpret_cast<uintptr_t>(p) % 16) == 0;
-        if (ok) return 32;
-    }
-#endif
-    for (int v : {16, 8, 4}) {
-        bool ok = (pitch % v) == 0;
-        for (const void *p : ptrs) ok = ok && (reinterpret_cast<uintptr_t>(p) % v) == 0;
-        if (ok) return v;
-    }
-    return 1;
-}
-
-// granule of the flattened kernel: 32 B whenever the pitch and every base pointer are dword aligned (the
-// tail granule of a row is loaded / stored dword by dword), bytewise otherwise
+// granule of the MAC kernels: 32 B whenever the pitch and every base pointer are dword aligned (the tail
+// granule of a row is loaded / stored dword by dword), bytewise otherwise
 static int pick_vec_mac(size_t pitch, std::initializer_list<const void *> ptrs)
 {
     bool ok = (pitch % 4) == 0;
     for (const void *p : ptrs) ok = ok && (reinterpret_cast<uintptr_t>(p) % 4) == 0;
-#if KFEC_VEC32
     return ok ? 32 : 1;
-#else
-    return ok ? 16 : 1;
-#endif
 }
 
-// resident 256-thread blocks per CU for a kernel (occupancy API, capped at 8: MI355X_MICROARCH.md
-// "Residency": the API can over-report by one for SGPR-heavy kernels; ours stay below 80 SGPRs)
-static int env_int(const char *name, int dflt)
-{
-    const char *e = getenv(name);
-    return e && *e ? atoi(e) : dflt;
-}
-
-static int resident_blocks(const void *kernel, size_t lds)
-{
-    static const int cap = std::max(1, std::min(8, env_int("KFEC_BLOCKS", 8)));
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, kBlock, lds) != hipSuccess || n <= 0) n = 1;
-    return std::min(n, cap);
-}
-
+// output rows per tile: MT = R up to 4, else 8-row tiles.  Measured at 200:55: taller tiles on
+// narrower granules read each input byte fewer times but are no faster (VALU-bound there, and 32-B
+// granules amortise each table read over the most bytes).
 static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
-
-// (granule bytes, output rows per tile) of the flattened kernel: the widest granule and MT = min(R, 8)
-// rows.  Measured at 200:55: taller tiles on narrower granules (16 x 16 B, 32 x 8 B) read each
-// input byte fewer times but are no faster -- the re-reads hit L2 and the kernel is VALU-bound there,
-// where 32-B granules amortise each table read over the most bytes.  KFEC_MT / KFEC_VEC override.
-static void mac_shape(int R, int vec_max, int &vec, int &mt)
-{
-    static const int mt_env = env_int("KFEC_MT", 0), vec_env = env_int("KFEC_VEC", 0);
-    vec = vec_max;
-    mt = pick_mt(R);
-    if (mt_env == 1 || mt_env == 2 || mt_env == 3 || mt_env == 4 || mt_env == 8) mt = mt_env;
-    if (vec_env > 0 && vec_env <= vec_max && (vec_env & (vec_env - 1)) == 0) vec = vec_env;
-}
-
-// KFEC_PAD=1: pad a group's items to whole waves, so one wave-instruction reads a whole shard row and
-// both halves of every 128-B line that straddles two shards are read by consecutive instructions
-static size_t pad_cols(size_t cols)
-{
-    static const bool on = [] {
-        const char *e = getenv("KFEC_PAD");
-        return e && std::string(e) == "1";
-    }();
-    return on ? (cols + 63) / 64 * 64 : cols;
-}
-
-template <int VEC, int MT, bool DEC, int PDX = 0>
-static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
-{
-    using L = MacLayout<MT>;
-    const size_t lds = a.etab ? 0 : (size_t)a.gmax * a.JC * L::ENTRY;
-    // one workgroup per 256 items (non-persistent): the dispatcher refills each CU as workgroups retire.
-    // Measured against a persistent grid sized to the resident workgroups (KFEC_GRID_PERSIST=1): encode
-    // 6.90 -> 6.08 ms and decode 7.39 -> 6.75 ms at 20:3 B=1440 1M groups, 205 -> 173 ms encode at 200:55
-    // (DESIGN.md 5).  With several row tiles the grid's x extent stays a multiple of the 8 XCDs, so
-    // workgroups (x, y) and (x, y') share an XCD and the tiles' re-reads of the same shard bytes hit its L2.
-    const uint32_t want = (a.total + kMacBlock - 1) / kMacBlock;
-    static const int persist = env_int("KFEC_GRID_PERSIST", 0);
-    uint32_t gx = want;
-    if (persist) {
-        uint32_t cap = (uint32_t)(std::max(1, di.cus) * resident_blocks((const void *)mac_kernel<VEC, MT, DEC, PDX>, lds))
-                       / (uint32_t)std::max(1, tiles);
-        if (tiles > 1 && cap >= 8) cap &= ~7u;
-        gx = std::min(want, std::max(cap, 1u));
-    } else if (tiles > 1) {
-        gx = (want + 7) & ~7u;
-    }
-    gx = std::max(1u, gx);
-    hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC, PDX>), dim3(gx, tiles), dim3(kMacBlock), lds, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -3;
-}
 
 // Batches of at most kLatencyGroups groups (the single-group drop-in calls, whose shares sit in pinned host
 // memory) run the MAC with 4-byte granules and 16 shards in flight per lane: ~8x more lanes and loads in
@@ -1773,36 +1127,51 @@ static int run_mac(const DeviceInfo &di, MacArgs a, int tiles, hipStream_t s)
 constexpr int kLatencyVec = -4;
 constexpr size_t kLatencyGroups = 4;
 
-template <bool DEC>
-static int dispatch_mac(const DeviceInfo &di, int vec, int mt, MacArgs a, int tiles, hipStream_t s)
+template <int VEC, int MT, bool DEC, int PDX = 0>
+static int run_mac(MacArgs a, hipStream_t s)
 {
-#define KFEC_MT_CASES(V)                                                     \
-    switch (mt) {                                                            \
-    case 1: return run_mac<V, 1, DEC>(di, a, tiles, s);                      \
-    case 2: return run_mac<V, 2, DEC>(di, a, tiles, s);                      \
-    case 3: return run_mac<V, 3, DEC>(di, a, tiles, s);                      \
-    case 4: return run_mac<V, 4, DEC>(di, a, tiles, s);                      \
-    default: return run_mac<V, 8, DEC>(di, a, tiles, s);                     \
+    using L = MacLayout<MT>;
+    const size_t lds = (size_t)a.gmax * a.JC * L::ENTRY;
+    const uint32_t chunks = (a.total + kMacBlock - 1) / kMacBlock;
+    const uint32_t nb = a.tiles > 1 ? ((chunks + 7) & ~7u) * a.tiles : chunks;
+    hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <bool DEC>
+static int dispatch_mac(int vec, int mt, MacArgs a, hipStream_t s)
+{
+    if constexpr (DEC) {  // coefficient-form decode: R > 8, 8-row tiles only
+        (void)mt;
+        if (vec == kLatencyVec) return run_mac<4, 8, true, 16>(a, s);
+        if (vec == 32) return run_mac<32, 8, true>(a, s);
+        return run_mac<1, 8, true>(a, s);
     }
     if (vec == kLatencyVec) {  // the latency shape: dword granules, 16 shards in flight per lane
         switch (mt) {
-        case 1: return run_mac<4, 1, DEC, 16>(di, a, tiles, s);
-        case 2: return run_mac<4, 2, DEC, 16>(di, a, tiles, s);
-        case 3: return run_mac<4, 3, DEC, 16>(di, a, tiles, s);
-        case 4: return run_mac<4, 4, DEC, 16>(di, a, tiles, s);
-        default: return run_mac<4, 8, DEC, 16>(di, a, tiles, s);
+        case 1: return run_mac<4, 1, DEC, 16>(a, s);
+        case 2: return run_mac<4, 2, DEC, 16>(a, s);
+        case 3: return run_mac<4, 3, DEC, 16>(a, s);
+        case 4: return run_mac<4, 4, DEC, 16>(a, s);
+        default: return run_mac<4, 8, DEC, 16>(a, s);
         }
     }
-    switch (vec) {
-#if KFEC_VEC32
-    case 32: KFEC_MT_CASES(32)
-#endif
-    case 16: KFEC_MT_CASES(16)
-    case 8: KFEC_MT_CASES(8)
-    case 4: KFEC_MT_CASES(4)
-    default: KFEC_MT_CASES(1)
+    if (vec == 32) {
+        switch (mt) {
+        case 1: return run_mac<32, 1, DEC>(a, s);
+        case 2: return run_mac<32, 2, DEC>(a, s);
+        case 3: return run_mac<32, 3, DEC>(a, s);
+        case 4: return run_mac<32, 4, DEC>(a, s);
+        default: return run_mac<32, 8, DEC>(a, s);
+        }
     }
-#undef KFEC_MT_CASES
+    switch (mt) {
+    case 1: return run_mac<1, 1, DEC>(a, s);
+    case 2: return run_mac<1, 2, DEC>(a, s);
+    case 3: return run_mac<1, 3, DEC>(a, s);
+    case 4: return run_mac<1, 4, DEC>(a, s);
+    default: return run_mac<1, 8, DEC>(a, s);
+    }
 }
 
 static int entry_bytes(int mt)
@@ -1816,224 +1185,53 @@ static int entry_bytes(int mt)
     }
 }
 
+static int syn_rt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
+
+static size_t syn_td(int rt)
+{
+    switch (rt) {
+    case 1: return SynLayout<1>::TD;
+    case 2: return SynLayout<2>::TD;
+    case 3: return SynLayout<3>::TD;
+    case 4: return SynLayout<4>::TD;
+    default: return SynLayout<8>::TD;
+    }
+}
+
+template <int VEC, int RT, int PDX = 0>
+static int run_syn(SynArgs a, size_t lds, hipStream_t s)
+{
+    const uint32_t nb = (a.total + kMacBlock - 1) / kMacBlock;
+    hipLaunchKernelGGL((syn_kernel<VEC, RT, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+static int dispatch_syn(int vec, int rt, SynArgs a, size_t lds, hipStream_t s)
+{
+#define KFEC_RT_CASES(V, P)                               \
+    switch (rt) {                                         \
+    case 1: return run_syn<V, 1, P>(a, lds, s);           \
+    case 2: return run_syn<V, 2, P>(a, lds, s);           \
+    case 3: return run_syn<V, 3, P>(a, lds, s);           \
+    case 4: return run_syn<V, 4, P>(a, lds, s);           \
+    default: return run_syn<V, 8, P>(a, lds, s);          \
+    }
+    if (vec == kLatencyVec) KFEC_RT_CASES(4, 16)
+    if (vec == 32) KFEC_RT_CASES(32, 0)
+    KFEC_RT_CASES(1, 0)
+#undef KFEC_RT_CASES
+}
+
 static constexpr size_t kLdsBudget = 32 * 1024;
-static constexpr size_t kTileLdsBudget = 31 * 1024;  // 5 workgroups per CU (160 KiB of LDS)
-
-// group-tile kernel for shards up to 2 KiB (one 8-byte column per lane of a 256-lane workgroup) and
-// < 2^32 groups; larger shards take the flattened kernel
-// Measured slower than the flattened kernel on MI355X once the GF math is in (DESIGN.md "kernel
-// architecture"), so it is opt-in: KFEC_KERNEL=tile.
-static bool use_tile_path(size_t G, size_t B)
-{
-    static const bool on = [] {
-        const char *e = getenv("KFEC_KERNEL");
-        return e && std::string(e) == "tile";
-    }();
-    return on && B <= 2048 && G < 0xFFFFFFFFull;
-}
-
-template <int MT, bool DEC, int SV>
-static int run_tile(const DeviceInfo &di, LdsArgs a, int tiles, hipStream_t s)
-{
-    using L = TileLayout<MT>;
-    a.Bs = (a.B + 15) & ~15u;
-    a.cols = (a.B + 7) / 8;
-    a.bs_inv = ((1ull << 32) + a.Bs - 1) / a.Bs;
-    // 2-deep ring of JS-shard chunks (+ their tables) within the per-workgroup LDS budget; encode keeps
-    // all K shards' tables resident when they are small
-    const size_t all_tbl = (size_t)a.K * L::TBL;
-    a.tbl_all = (!DEC && all_tbl <= 4096) ? 1u : 0u;
-    const size_t per_row = 2 * (size_t)a.Bs + (a.tbl_all ? 0 : 2 * (size_t)L::TBL);
-    const size_t budget = kTileLdsBudget - (a.tbl_all ? all_tbl : 0);
-    const size_t nch = std::max<size_t>(1, (a.K * per_row + budget - 1) / budget);
-    a.JS = (uint32_t)((a.K + nch - 1) / nch);
-    const size_t lds = (size_t)a.JS * per_row + (a.tbl_all ? all_tbl : 0);
-    const uint32_t threads = 256;
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)mac_tile_kernel<MT, DEC, SV>, threads, lds) !=
-            hipSuccess || occ <= 0)
-        occ = 1;
-    const uint32_t cap = (uint32_t)std::max(1, di.cus * std::min(occ, 8) / std::max(1, tiles));
-    const uint32_t gx = std::max(1u, std::min<uint32_t>(a.G, cap));
-    hipLaunchKernelGGL((mac_tile_kernel<MT, DEC, SV>), dim3(gx, tiles), dim3(threads), lds, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
-// ---- wave-tile launch ----
-[[maybe_unused]] static constexpr size_t kWtLdsMax = 13 * 1024;  // 12 waves (workgroups) per CU fit in 160 KiB
-
-struct WtPlan {
-    bool ok = false;
-    uint32_t JS = 0, nch = 0, Bs = 0;
-    size_t lds = 0;
-};
-
-static WtPlan plan_wave(uint32_t K, uint32_t R, uint32_t B, int mt)
-{
-    WtPlan p;
-    if (B == 0 || B > 2048 || R == 0 || R > (uint32_t)mt) return p;
-    const uint32_t tbl = (uint32_t)(mt * 16 + (mt + 3) / 4 * 16);
-    p.Bs = (B + 15) & ~15u;
-    const uint32_t cap = (uint32_t)std::min<size_t>(K, (size_t)kWtLoads * 1024 / p.Bs);
-    if (cap == 0) return p;
-    // prefer chunks that are whole 128-B lines (e.g. 8 x 1440 B = 90 lines), else the largest
-    uint32_t js = cap;
-    for (uint32_t j = cap; j >= 1; --j)
-        if ((j * p.Bs) % 128 == 0 && 2 * j >= cap) {
-            js = j;
-            break;
-        }
-    p.JS = js;
-    p.nch = (K + js - 1) / js;
-    p.lds = ((size_t)js * p.Bs + 15) / 16 * 16 + (size_t)K * tbl;
-    p.ok = p.lds <= 64 * 1024;
-    return p;
-}
-
-template <int MT, bool DEC>
-static int run_wave(const DeviceInfo &di, WtArgs a, const WtPlan &p, hipStream_t s)
-{
-    a.JS = p.JS;
-    a.nch = p.nch;
-    a.Bs = p.Bs;
-    a.cols = (a.B + 15) / 16;
-    a.bs_inv = ((1ull << 32) + a.Bs - 1) / a.Bs;
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)mac_wave_kernel<MT, DEC>, 64, p.lds) !=
-            hipSuccess || occ <= 0)
-        occ = 1;
-    const uint32_t gx = std::max(1u, std::min<uint32_t>(a.G, (uint32_t)std::max(1, di.cus * std::min(occ, 32))));
-    hipLaunchKernelGGL((mac_wave_kernel<MT, DEC>), dim3(gx), dim3(64), p.lds, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
-template <bool DEC>
-static int dispatch_wave(const DeviceInfo &di, WtArgs a, const WtPlan &p, int mt, hipStream_t s)
-{
-    switch (mt) {
-    case 1: return run_wave<1, DEC>(di, a, p, s);
-    case 2: return run_wave<2, DEC>(di, a, p, s);
-    case 3: return run_wave<3, DEC>(di, a, p, s);
-    case 4: return run_wave<4, DEC>(di, a, p, s);
-    default: return run_wave<8, DEC>(di, a, p, s);
-    }
-}
-
-static bool wave_enabled()
-{
-    static const bool on = [] {
-        const char *e = getenv("KFEC_KERNEL");
-        return e && std::string(e) == "wave";
-    }();
-    return on;
-}
-
-// ---- stream engine launch ----
-static constexpr size_t kEngLdsMax = 160 * 1024 - 1024;
-
-struct EngPlan {
-    bool ok = false;
-    uint32_t JS = 0, nch = 0, Bs = 0, slot_bytes = 0;
-    size_t lds = 0;
-};
-
-static EngPlan plan_stream(uint32_t K, uint32_t R, uint32_t B, int mt, bool dec)
-{
-    EngPlan p;
-    if (B == 0 || B > 2048 || R == 0 || R > (uint32_t)mt) return p;
-    const uint32_t tbl = (uint32_t)(mt * 16 + (mt + 3) / 4 * 16);
-    p.Bs = (B + 15) & ~15u;
-    const size_t enc_tbl = dec ? 0 : (size_t)K * tbl;
-    if (enc_tbl + 64 >= kEngLdsMax) return p;
-    for (uint32_t js = std::min<uint32_t>(K, (32 * 1024) / p.Bs); js >= 1; --js) {
-        const uint32_t slot = ((js * p.Bs + 1023) / 1024) * 1024;
-        const size_t lds = (size_t)kEngS * (slot + (dec ? (size_t)js * tbl : 0)) + enc_tbl + 64;
-        if (lds <= kEngLdsMax) {
-            p.ok = true;
-            p.JS = js;
-            p.nch = (K + js - 1) / js;
-            p.slot_bytes = slot;
-            p.lds = lds;
-            return p;
-        }
-    }
-    return p;
-}
-
-template <int MT, bool DEC>
-static int run_stream(const DeviceInfo &di, StreamArgs a, const EngPlan &p, hipStream_t s)
-{
-    static bool attr_set = false;  // per instantiation: allow > 64 KiB of dynamic LDS
-    if (!attr_set) {
-        if (hipFuncSetAttribute((const void *)mac_stream_kernel<MT, DEC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)kEngLdsMax) != hipSuccess)
-            return -3;
-        attr_set = true;
-    }
-    a.JS = p.JS;
-    a.nch = p.nch;
-    a.Bs = p.Bs;
-    a.slot_bytes = p.slot_bytes;
-    a.cols = (a.B + 7) / 8;
-    a.bs_inv = ((1ull << 32) + a.Bs - 1) / a.Bs;
-    const uint32_t gx = std::max(1u, std::min<uint32_t>(a.G, (uint32_t)std::max(1, di.cus)));
-    hipLaunchKernelGGL((mac_stream_kernel<MT, DEC>), dim3(gx), dim3(kEngThreads), p.lds, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
-template <bool DEC>
-static int dispatch_stream(const DeviceInfo &di, StreamArgs a, const EngPlan &p, int mt, hipStream_t s)
-{
-    switch (mt) {
-    case 1: return run_stream<1, DEC>(di, a, p, s);
-    case 2: return run_stream<2, DEC>(di, a, p, s);
-    case 3: return run_stream<3, DEC>(di, a, p, s);
-    case 4: return run_stream<4, DEC>(di, a, p, s);
-    default: return run_stream<8, DEC>(di, a, p, s);
-    }
-}
-
-// the stream engine serves layouts with 16-B aligned slots, B <= 2 KiB and R <= 8 (one row tile).
-// Measured slower than the flattened kernel (its LDS ring holds ~3 groups in flight per CU, the
-// flattened kernel's VGPRs ~4x that), so it is opt-in: KFEC_KERNEL=engine.
-static bool stream_enabled()
-{
-    static const bool on = [] {
-        const char *e = getenv("KFEC_KERNEL");
-        return e && std::string(e) == "engine";
-    }();
-    return on;
-}
-
-template <bool DEC>
-static int dispatch_tile(const DeviceInfo &di, int sv, LdsArgs a, hipStream_t g_stream)
-{
-    const int mt = a.R <= 4 ? std::max<int>(a.R, 1) : 8;
-    const int tiles = ((int)a.R + mt - 1) / mt;
-    if (sv > 16) sv = 16;
-#define KFEC_TILE_MT(SV)                                                           \
-    switch (mt) {                                                                  \
-    case 1: return run_tile<1, DEC, SV>(di, a, tiles, g_stream);                   \
-    case 2: return run_tile<2, DEC, SV>(di, a, tiles, g_stream);                   \
-    case 3: return run_tile<3, DEC, SV>(di, a, tiles, g_stream);                   \
-    case 4: return run_tile<4, DEC, SV>(di, a, tiles, g_stream);                   \
-    default: return run_tile<8, DEC, SV>(di, a, tiles, g_stream);                  \
-    }
-    switch (sv) {
-    case 16: KFEC_TILE_MT(16)
-    case 8: KFEC_TILE_MT(8)
-    case 4: KFEC_TILE_MT(4)
-    default: KFEC_TILE_MT(1)
-    }
-#undef KFEC_TILE_MT
-}
+static constexpr size_t kSynLdsMax = 64 * 1024;
 static constexpr size_t kMaxItemsPerLaunch = 0x7FFFFFFFu;
 
-// split G into launches whose item count fits 32-bit indexing
+// split G into launches whose item count (x row tiles) fits 32-bit indexing
 template <typename F>
-static int for_group_ranges(size_t G, size_t cols, F &&f)
+static int for_group_ranges(size_t G, size_t cols, size_t tiles, F &&f)
 {
-    const size_t gmax_launch = std::max<size_t>(1, kMaxItemsPerLaunch / std::max<size_t>(cols, 1));
+    const size_t cap = kMaxItemsPerLaunch / std::max<size_t>(tiles, 1) / std::max<size_t>(cols, 1);
+    const size_t gmax_launch = std::max<size_t>(1, cap);
     for (size_t g0 = 0; g0 < G; g0 += gmax_launch) {
         const int rc = f(g0, std::min(gmax_launch, G - g0));
         if (rc) return rc;
@@ -2044,53 +1242,18 @@ static int for_group_ranges(size_t G, size_t cols, F &&f)
 int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, size_t B, size_t pitch,
                   const void *d_data, void *d_parity, hipStream_t s)
 {
+    (void)di;
     const int R = N - K;
     if (R == 0 || G == 0 || B == 0) return 0;
-    if (use_tile_path(G, B)) {
-        LdsArgs a{};
-        a.data = static_cast<const uint8_t *>(d_data);
-        a.out = static_cast<uint8_t *>(d_parity);
-        a.enc = d_enc;
-        a.pitch = pitch;
-        a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
-        return dispatch_tile<false>(di, pick_vec(pitch, {d_data, d_parity}), a, s);
-    }
-    if (wave_enabled() && G < 0xFFFFFFFFull && pick_vec(pitch, {d_data, d_parity}) >= 16) {
-        const int mt = pick_mt(R);
-        const WtPlan p = plan_wave(K, R, (uint32_t)B, mt);
-        if (p.ok) {
-            WtArgs a{};
-            a.data = static_cast<const uint8_t *>(d_data);
-            a.out = static_cast<uint8_t *>(d_parity);
-            a.enc = d_enc;
-            a.pitch = pitch;
-            a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
-            return dispatch_wave<false>(di, a, p, mt, s);
-        }
-    }
-    if (stream_enabled() && G < 0xFFFFFFFFull && pick_vec(pitch, {d_data, d_parity}) >= 16) {
-        const int mt = pick_mt(R);
-        const EngPlan p = plan_stream(K, R, (uint32_t)B, mt, false);
-        if (p.ok) {
-            StreamArgs a{};
-            a.data = static_cast<const uint8_t *>(d_data);
-            a.out = static_cast<uint8_t *>(d_parity);
-            a.enc = d_enc;
-            a.err = g_err_word();
-            a.pitch = pitch;
-            a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
-            return dispatch_stream<false>(di, a, p, mt, s);
-        }
-    }
-    int vec = 0, mt = 0;
-    mac_shape(R, pick_vec_mac(pitch, {d_data, d_parity}), vec, mt);
+    int vec = pick_vec_mac(pitch, {d_data, d_parity});
+    const int mt = pick_mt(R);
     if (G <= kLatencyGroups && vec >= 4) vec = kLatencyVec;
     const int vb = vec >= 4 ? vec : 4;
-    const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
+    const size_t cols = (B + vb - 1) / vb;
     const int tiles = (R + mt - 1) / mt;
     const size_t ent = entry_bytes(mt);
     const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / ent));
-    return for_group_ranges(G, cpad, [&](size_t g0, size_t gn) {
+    return for_group_ranges(G, cols, tiles, [&](size_t g0, size_t gn) {
         MacArgs a{};
         a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
         a.parity = nullptr;
@@ -2098,45 +1261,23 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.enc = d_enc;
         a.rec = nullptr;
         a.pitch = pitch;
-        a.total = (uint32_t)(gn * cpad);
+        a.total = (uint32_t)(gn * cols);
         a.cols = (uint32_t)cols;
-        a.cpad = (uint32_t)cpad;
         a.G = (uint32_t)gn;
         a.K = K; a.R = R; a.B = (uint32_t)B;
         a.rec_stride = 0;
         a.JC = JC;
         a.gmax = 1;
-        static const int stab = env_int("KFEC_SGPR_TABLES", KFEC_SGPR_TABLES);
-        if (stab) {
-            a.etab = reinterpret_cast<const uint32_t *>(d_enc + enc_tab_offset(K, K + R));
-            a.etab_rows = (uint32_t)enc_tab_rows(R);
-            a.JC = K;
-        }
-        return dispatch_mac<false>(di, vec, mt, a, tiles, s);
+        a.tiles = (uint32_t)tiles;
+        return dispatch_mac<false>(vec, mt, a, s);
     });
 }
 
-// Work list of the decode MAC: the groups whose decode has work (status OK and at least one data shard
-// missing).  A group with nothing lost -- the common case on a live link, where fec_find_missings decodes
-// every group that reached K shares (client.cpp:924-925) -- then costs the MAC kernel nothing.  Ballot per
-// wave, one atomic per wave: groups are ascending within a wave, waves land in any order.
-__global__ void __launch_bounds__(kBlock) compact_kernel(uint64_t G, uint32_t R, const uint8_t *status,
-                                                         const uint8_t *out_idx, uint32_t *count, uint32_t *list)
-{
-    const uint64_t g = blockIdx.x * (uint64_t)kBlock + threadIdx.x;
-    const bool active = g < G && status[g] == 0 && out_idx[g * R] != 0xFF;
-    const uint64_t mask = __ballot(active);
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t base = 0;
-    if (lane == 0 && mask) base = atomicAdd(count, (uint32_t)__popcll(mask));
-    base = __shfl(base, 0);
-    if (active) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)g;
-}
-
-// decode_prep_*: share selection, the m x m solve and the coefficient rows of every group into the decode
-// records of d_workspace (+ d_out_idx, d_status).  The MAC kernels (here and kfec_frame.hip) consume them.
+// decode_prep_*: share selection, the m x m solve and the coefficient rows (or, syn = true, the syndrome-form
+// records) of every group into d_workspace (+ d_out_idx, d_status).  The MAC kernels here and in
+// kfec_frame.hip consume them.
 int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, const uint64_t *d_present,
-                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s)
+                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s, bool syn)
 {
     const int R = N - K;
     if (G == 0) return 0;
@@ -2151,6 +1292,7 @@ int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N,
     p.G = G;
     p.K = K; p.N = N; p.R = R;
     p.rec_stride = (uint32_t)rs;
+    p.syn = syn ? 1 : 0;
     const int mmax = std::min(K, R);
     if (mmax <= 8) {
         const size_t lds = 768 + (size_t)R * K;
@@ -2183,96 +1325,42 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     if (G == 0) return 0;
     uint8_t *rec = static_cast<uint8_t *>(d_workspace);
     const size_t rs = record_stride(K, R);
-    if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s)) return -3;
-    if (R == 0 || B == 0) return 0;
-    if (use_tile_path(G, B)) {
-        LdsArgs a{};
-        a.data = static_cast<const uint8_t *>(d_data);
-        a.parity = static_cast<const uint8_t *>(d_parity);
-        a.out = static_cast<uint8_t *>(d_out);
-        a.enc = d_enc;
-        a.rec = rec;
-        a.pitch = pitch;
-        a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
-        a.rec_stride = (uint32_t)rs;
-        return dispatch_tile<true>(di, pick_vec(pitch, {d_data, d_parity, d_out}), a, s);
-    }
-    if (wave_enabled() && G < 0xFFFFFFFFull && pick_vec(pitch, {d_data, d_parity, d_out}) >= 16) {
-        const int mt = pick_mt(R);
-        const WtPlan p = plan_wave(K, R, (uint32_t)B, mt);
-        if (p.ok) {
-            WtArgs a{};
-            a.data = static_cast<const uint8_t *>(d_data);
-            a.parity = static_cast<const uint8_t *>(d_parity);
-            a.out = static_cast<uint8_t *>(d_out);
-            a.enc = d_enc;
-            a.rec = rec;
-            a.pitch = pitch;
-            a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
-            a.rec_stride = (uint32_t)rs;
-            return dispatch_wave<true>(di, a, p, mt, s);
-        }
-    }
-    if (stream_enabled() && G < 0xFFFFFFFFull && pick_vec(pitch, {d_data, d_parity, d_out}) >= 16) {
-        const int mt = pick_mt(R);
-        const EngPlan p = plan_stream(K, R, (uint32_t)B, mt, true);
-        if (p.ok) {
-            StreamArgs a{};
-            a.data = static_cast<const uint8_t *>(d_data);
-            a.parity = static_cast<const uint8_t *>(d_parity);
-            a.out = static_cast<uint8_t *>(d_out);
-            a.enc = d_enc;
-            a.rec = rec;
-            a.err = g_err_word();
-            a.pitch = pitch;
-            a.G = (uint32_t)G; a.K = K; a.R = R; a.B = (uint32_t)B;
-            a.rec_stride = (uint32_t)rs;
-            return dispatch_stream<true>(di, a, p, mt, s);
-        }
-    }
-
-    int vec = 0, mt = 0;
-    mac_shape(R, pick_vec_mac(pitch, {d_data, d_parity, d_out}), vec, mt);
+    int vec = pick_vec_mac(pitch, {d_data, d_parity, d_out});
     if (G <= kLatencyGroups && vec >= 4) vec = kLatencyVec;
     const int vb = vec >= 4 ? vec : 4;
-    const size_t cols = (B + vb - 1) / vb, cpad = pad_cols(cols);
+    const size_t cols = (B + vb - 1) / vb;
+    // syndrome form for R <= 8 unless its per-workgroup C tables outgrow LDS (tiny B: hundreds of groups
+    // per workgroup)
+    const int rt = syn_rt(R);
+    const size_t gmax_syn = std::min<size_t>(G, (kMacBlock - 1) / std::max<size_t>(cols, 1) + 2);
+    const size_t lds_syn = gmax_syn * (size_t)rt * syn_td(rt) * 4;
+    const bool syn = R > 0 && R <= 8 && lds_syn <= kSynLdsMax;
+    if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s, syn)) return -3;
+    if (R == 0 || B == 0) return 0;
+    if (syn) {
+        return for_group_ranges(G, cols, 1, [&](size_t g0, size_t gn) {
+            SynArgs a{};
+            a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
+            a.parity = static_cast<const uint8_t *>(d_parity) + g0 * R * pitch;
+            a.out = static_cast<uint8_t *>(d_out) + g0 * R * pitch;
+            a.rec = rec + g0 * rs;
+            a.present = d_present + g0 * 4;
+            a.etab = reinterpret_cast<const uint32_t *>(d_enc + enc_tab_offset(K, N));
+            a.etab_rows = (uint32_t)enc_tab_rows(R);
+            a.pitch = pitch;
+            a.total = (uint32_t)(gn * cols);
+            a.cols = (uint32_t)cols;
+            a.G = (uint32_t)gn;
+            a.K = K; a.R = R; a.B = (uint32_t)B;
+            a.rec_stride = (uint32_t)rs;
+            return dispatch_syn(vec, rt, a, lds_syn, s);
+        });
+    }
+    const int mt = 8;  // coefficient form: R > 8 (or tiny shards), 8-row tiles
     const int tiles = (R + mt - 1) / mt;
     const size_t ent = entry_bytes(mt);
-    // Work-list mode (KFEC_DECODE_LIST=1) measured slower on the benchmark configs, where >= 91% of the groups
-    // lost data: 20:3 decode 6.84 -> 7.35 ms, 10:3 random 3.59 -> 3.75 ms (the list lookup is one more
-    // dependent load at the head of every workgroup, and wave-order compaction scatters neighbouring groups).
-    // It is kept for batches where most groups lost nothing.
-    static const int use_list = env_int("KFEC_DECODE_LIST", 0);
-    if (use_list && G * cpad <= kMaxItemsPerLaunch) {
-        uint32_t *count = reinterpret_cast<uint32_t *>(rec + decode_list_offset(G, K, R));
-        uint32_t *list = count + 16;
-        if (hipMemsetAsync(count, 0, sizeof(uint32_t), s) != hipSuccess) return -3;
-        hipLaunchKernelGGL(compact_kernel, dim3((uint32_t)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, (uint64_t)G,
-                           (uint32_t)R, d_status, d_out_idx, count, list);
-        if (hipGetLastError() != hipSuccess) return -3;
-        const uint32_t gmax = (uint32_t)std::min<size_t>(G, (kMacBlock - 1) / cpad + 2);
-        const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
-        MacArgs a{};
-        a.data = static_cast<const uint8_t *>(d_data);
-        a.parity = static_cast<const uint8_t *>(d_parity);
-        a.out = static_cast<uint8_t *>(d_out);
-        a.enc = d_enc;
-        a.rec = rec;
-        a.pitch = pitch;
-        a.total = (uint32_t)(G * cpad);  // grid size: every group could have work
-        a.cols = (uint32_t)cols;
-        a.cpad = (uint32_t)cpad;
-        a.G = (uint32_t)G;
-        a.K = K; a.R = R; a.B = (uint32_t)B;
-        a.rec_stride = (uint32_t)rs;
-        a.JC = JC;
-        a.gmax = gmax;
-        a.list = list;
-        a.list_count = count;
-        return dispatch_mac<true>(di, vec, mt, a, tiles, s);
-    }
-    return for_group_ranges(G, cpad, [&](size_t g0, size_t gn) {
-        const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kMacBlock - 1) / cpad + 2);
+    return for_group_ranges(G, cols, tiles, [&](size_t g0, size_t gn) {
+        const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kMacBlock - 1) / cols + 2);
         const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
         MacArgs a{};
         a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
@@ -2281,15 +1369,15 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.enc = d_enc;
         a.rec = rec + g0 * rs;
         a.pitch = pitch;
-        a.total = (uint32_t)(gn * cpad);
+        a.total = (uint32_t)(gn * cols);
         a.cols = (uint32_t)cols;
-        a.cpad = (uint32_t)cpad;
         a.G = (uint32_t)gn;
         a.K = K; a.R = R; a.B = (uint32_t)B;
         a.rec_stride = (uint32_t)rs;
         a.JC = JC;
         a.gmax = gmax;
-        return dispatch_mac<true>(di, vec, mt, a, tiles, s);
+        a.tiles = (uint32_t)tiles;
+        return dispatch_mac<true>(vec, mt, a, s);
     });
 }
 
@@ -2329,6 +1417,15 @@ __global__ void __launch_bounds__(kBlock) erasure_kernel(uint64_t seed, uint32_t
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (g >= G) return;
     const uint64_t gg = g0 + g;
+    if (random_count == 2) {  // i.i.d. loss with probability count_max / 1e6 per shard (orc_erasure_mask_iid)
+        uint64_t m[4] = {0, 0, 0, 0};
+        for (uint32_t s = 0; s < N; ++s)
+            if (splitmix64(seed ^ 0xC2B2AE3D27D4EB4Full ^ (gg * 0x100u + s)) % 1000000u >= count_max)
+                m[s >> 6] |= 1ull << (s & 63);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) present[g * 4 + q] = m[q];
+        return;
+    }
     uint32_t cnt = count_max;
     if (random_count) cnt = 1 + (uint32_t)(splitmix64(seed ^ ~gg) % count_max);
     uint64_t m[4];
@@ -2353,7 +1450,8 @@ int launch_erasure_masks(uint64_t seed, int N, size_t g0, size_t G, size_t pool,
 {
     if (G == 0) return 0;
     hipLaunchKernelGGL(erasure_kernel, dim3((uint32_t)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, seed,
-                       (uint32_t)N, (uint64_t)g0, (uint64_t)G, (uint32_t)pool, (uint32_t)std::max<size_t>(count_max, 1),
+                       (uint32_t)N, (uint64_t)g0, (uint64_t)G, (uint32_t)pool,
+                       (uint32_t)(random_count == 2 ? count_max : std::max<size_t>(count_max, 1)),
                        random_count, d_present);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -77,7 +77,6 @@ def load_library():
         "kfec_erasure_masks": (C.c_int, [_vp, C.c_uint64, sz, sz, sz, sz, C.c_int, _vp, _vp]),
         "kfec_verify_recovered": (C.c_int, [_vp, sz, sz, sz, _vp, _vp, _vp, _vp, _vp]),
         "kfec_version": (C.c_char_p, []),
-        "kfec_debug_flags": (C.c_uint32, []),
         "kfec_device": (C.c_int, [_vp]),
         # include/kfec_frame.h
         "kfec_frame_data_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, sz, sz, _vp, _vp, _vp]),
@@ -277,8 +276,10 @@ class FecCode:
         _check(self._lib.kfec_synth(self._ctx, seed, g0, G, s0, ns, B, pitch, _dptr(out), _stream_handle(stream)),
                "kfec_synth")
 
-    def erasure_masks(self, present, seed: int, pool: int, count_max: int, random_count: bool = False,
+    def erasure_masks(self, present, seed: int, pool: int, count_max: int, random_count: bool | int = False,
                       g0: int = 0, stream=None) -> None:
+        """random_count: 0 = exactly count_max ids from [0, pool); 1 = 1 + draw % count_max ids;
+        2 = i.i.d. loss of every id with probability count_max / 1e6."""
         self._need_ctx()
         G = present.shape[0]
         _check(self._lib.kfec_erasure_masks(self._ctx, seed, g0, G, pool, count_max, int(random_count),
@@ -290,11 +291,6 @@ class FecCode:
         B = pitch if B is None else B
         _check(self._lib.kfec_verify_recovered(self._ctx, G, B, pitch, _dptr(data), _dptr(out), _dptr(out_idx),
                                                _dptr(mismatch), _stream_handle(stream)), "kfec_verify_recovered")
-
-
-def debug_flags() -> int:
-    """kfec_debug_flags(): non-zero if the stream engine's bounded spins ever timed out."""
-    return int(load_library().kfec_debug_flags())
 
 
 def version() -> str:

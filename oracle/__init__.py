@@ -70,6 +70,7 @@ class Oracle:
                                       C.c_size_t, C.c_size_t, _u8p, C.c_size_t]
             lib.orc_erasure_mask.argtypes = [C.c_uint64, C.c_size_t, C.c_size_t, C.c_size_t,
                                              C.c_size_t, _u64p]
+            lib.orc_erasure_mask_iid.argtypes = [C.c_uint64, C.c_size_t, C.c_size_t, C.c_size_t, _u64p]
             lib.orc_erasure_count.argtypes = [C.c_uint64, C.c_size_t, C.c_size_t]
             lib.orc_erasure_count.restype = C.c_size_t
             lib.orc_encode_batch.argtypes = [C.c_size_t] * 5 + [_u8p, _u8p]
@@ -139,6 +140,13 @@ class Oracle:
         for g in range(G):
             c = cnt if random_max is None else self.lib.orc_erasure_count(seed, g0 + g, random_max)
             self.lib.orc_erasure_mask(seed, g0 + g, N, pool, c, _ptr(masks[g], _u64p))
+        return masks
+
+    def erasure_masks_iid(self, seed: int, G: int, N: int, ppm: int, g0: int = 0) -> np.ndarray:
+        """i.i.d. loss of every shard with probability ppm / 1e6 (kfec_erasure_masks random_count = 2)."""
+        masks = np.zeros((G, 4), np.uint64)
+        for g in range(G):
+            self.lib.orc_erasure_mask_iid(seed, g0 + g, N, ppm, _ptr(masks[g], _u64p))
         return masks
 
     # ---- batched helpers -------------------------------------------------------------------

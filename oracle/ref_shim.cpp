@@ -114,23 +114,31 @@ double ref_bench_roundtrip(size_t K, size_t N, size_t B, size_t G, size_t pool, 
     (void)warm;
     const size_t W = (B + 7) / 8;
     std::vector<uint8_t> data(G * K * B);
-    for (size_t g = 0; g < G; ++g)
-        for (size_t s = 0; s < K; ++s) {
-            uint8_t *dst = data.data() + (g * K + s) * B;
-            const uint64_t base = (g * N + s) * W;
-            for (size_t w = 0; w < W; ++w) {
-                uint64_t v = smix(seed ^ (base + w));
-                for (size_t k = 0; k < 8 && w * 8 + k < B; ++k) dst[w * 8 + k] = (uint8_t)(v >> (8 * k));
+    // decode-only runs read parity encoded before the timed region
+    std::vector<uint8_t> parity(decode_only ? G * (N - K) * B : 0);
+    // inputs are generated (and, decode-only, encoded) by the same threads over the same ranges, untimed
+    auto prepare = [&](size_t t) {
+        fecpp::fec_code c(K, N);
+        const size_t a = G * t / threads, b = G * (t + 1) / threads;
+        for (size_t g = a; g < b; ++g) {
+            for (size_t s = 0; s < K; ++s) {
+                uint8_t *dst = data.data() + (g * K + s) * B;
+                const uint64_t base = (g * N + s) * W;
+                for (size_t w = 0; w < W; ++w) {
+                    uint64_t v = smix(seed ^ (base + w));
+                    for (size_t k = 0; k < 8 && w * 8 + k < B; ++k) dst[w * 8 + k] = (uint8_t)(v >> (8 * k));
+                }
+            }
+            if (decode_only) {
+                auto red = c.encode(data.data() + g * K * B, K * B, B);
+                for (size_t r = 0; r < N - K; ++r) std::memcpy(parity.data() + (g * (N - K) + r) * B, red[r].get(), B);
             }
         }
-    // decode-only runs read parity encoded before the timed region
-    std::vector<uint8_t> parity;
-    if (decode_only) {
-        parity.resize(G * (N - K) * B);
-        for (size_t g = 0; g < G; ++g) {
-            auto red = warm.encode(data.data() + g * K * B, K * B, B);
-            for (size_t r = 0; r < N - K; ++r) std::memcpy(parity.data() + (g * (N - K) + r) * B, red[r].get(), B);
-        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (size_t t = 0; t < threads; ++t) th.emplace_back(prepare, t);
+        for (auto &x : th) x.join();
     }
     std::vector<size_t> recovered(threads, 0);
     auto worker = [&](size_t t) {
@@ -147,11 +155,16 @@ double ref_bench_roundtrip(size_t K, size_t N, size_t B, size_t G, size_t pool, 
                 };
                 // erasure draw: same definition as orc_erasure_mask / the HIP generator
                 size_t cnt = erase_max;
-                if (random_count) cnt = 1 + (size_t)(smix(seed ^ ~(uint64_t)g) % erase_max);
+                if (random_count == 1) cnt = 1 + (size_t)(smix(seed ^ ~(uint64_t)g) % erase_max);
                 uint8_t perm[256];
                 for (size_t i = 0; i < 256; ++i) perm[i] = (uint8_t)i;
                 bool present[256];
                 for (size_t s = 0; s < N; ++s) present[s] = true;
+                if (random_count == 2) {  // i.i.d. loss, erase_max = ppm (orc_erasure_mask_iid)
+                    cnt = 0;
+                    for (size_t s = 0; s < N; ++s)
+                        present[s] = smix(seed ^ 0xC2B2AE3D27D4EB4Full ^ ((uint64_t)g * 0x100u + s)) % 1000000u >= erase_max;
+                }
                 for (size_t e = 0; e < cnt && e < pool; ++e) {
                     uint64_t r = smix(seed ^ ((uint64_t)g * 0x100u + e));
                     size_t k = e + (size_t)(r % (uint64_t)(pool - e));

@@ -263,6 +263,17 @@ void orc_erasure_mask(uint64_t seed, size_t g, size_t N, size_t pool, size_t cnt
     }
 }
 
+/* i.i.d. loss (random_count == 2 in kfec_erasure_masks): shard s of group g is lost when
+ * splitmix64(seed ^ 0xC2B2AE3D27D4EB4F ^ (g * 0x100 + s)) % 1000000 < ppm, independently for every s < N. */
+void orc_erasure_mask_iid(uint64_t seed, size_t g, size_t N, size_t ppm, uint64_t mask[4])
+{
+    mask[0] = mask[1] = mask[2] = mask[3] = 0;
+    for (size_t s = 0; s < N; ++s) {
+        uint64_t r = splitmix64(seed ^ 0xC2B2AE3D27D4EB4Full ^ ((uint64_t)g * 0x100u + s));
+        if (r % 1000000u >= ppm) mask[s >> 6] |= 1ull << (s & 63);
+    }
+}
+
 /* erasure count for "random 1..maxc over all N" configs: 1 + splitmix64(seed ^ ~g) % maxc */
 size_t orc_erasure_count(uint64_t seed, size_t g, size_t maxc)
 {

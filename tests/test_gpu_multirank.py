@@ -1,0 +1,59 @@
+"""SURVEY 8(e) through the product: bench.py's multi-rank path as the driver launches it
+(torch.distributed.run, one process per rank, gloo barrier + max-reduce, group_range partition), with two
+ranks sharing the box's one GPU.  The per-part digests of the recovered bytes, combined in part order,
+must equal a single-rank run over the same global groups: no group lost, duplicated or changed."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _last_json(stdout: str) -> dict:
+    for line in reversed(stdout.strip().splitlines()):
+        line = line.strip()
+        if line.startswith("{"):
+            return json.loads(line)
+    raise AssertionError("no JSON line in:\n" + stdout[-2000:])
+
+
+def _run(cmd, parts):
+    env = dict(os.environ, KFEC_BENCH_DIGEST=str(parts), HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, f"rc={r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    return _last_json(r.stdout)
+
+
+@pytest.mark.parametrize("config", ["20:3", "10:3dec"])
+def test_bench_two_ranks_match_single_rank(config):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    per_gpu = 4096
+    common = ["--config", config, "--no-cpu", "--steps", "2", "--warmup", "1"]
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                "--groups", str(per_gpu)] + common, parts=2)
+    one = _run([sys.executable, "bench.py", "--gpus", "1", "--groups", str(2 * per_gpu)] + common, parts=2)
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["verified_bit_exact"] and one["verified_bit_exact"]
+    assert two["config"]["global_groups"] == one["config"]["global_groups"] == 2 * per_gpu
+    assert two["recovered_shards_per_step"] == one["recovered_shards_per_step"] > 0
+    assert two["combined_digest"] == one["combined_digest"]
+    assert two["value"] > 0

@@ -1,7 +1,8 @@
-"""CPU tests of the multi-GPU path: world_size-2 gloo processes partition the group space exactly as
+"""CPU tests of the multi-GPU partition: world_size-2 gloo processes partition the group space exactly as
 bench.py's ranks do, compute their share (here with the oracle, since no GPU is present), and the
 combined result equals the single-rank result -- the property the N-GPU bench relies on (no group
-lost or duplicated, no data-path collective)."""
+lost or duplicated, no data-path collective).  The same property through the product (bench.py under
+torch.distributed.run on the GPU) is tests/test_gpu_multirank.py."""
 from __future__ import annotations
 
 import hashlib
@@ -88,9 +89,15 @@ def test_two_rank_gloo_partition_matches_single_rank(tmp_path, oracle):
     np.testing.assert_array_equal(par_all[g0:g1], par_1)
 
 
-def test_bench_rank_offsets_are_disjoint():
-    """bench.py gives rank r the groups [r*G, (r+1)*G) (weak scaling): disjoint and contiguous."""
-    G = 1 << 20
-    spans = [(r * G, (r + 1) * G) for r in range(8)]
-    for (a, b), (c, d) in zip(spans, spans[1:]):
-        assert b == c
+def test_bench_rank_groups_partition_the_global_space():
+    """bench.py's own rank slicing (weak scaling: groups_per_gpu x world, split by group_range) tiles the
+    global group space exactly, for every world size the driver runs."""
+    import bench
+    for per_gpu in (1, 4096, 1 << 20):
+        for world in (1, 2, 4, 8):
+            spans = [bench.rank_groups(per_gpu, world, r) for r in range(world)]
+            assert all(t == per_gpu * world for _, _, t in spans)
+            assert spans[0][0] == 0 and spans[-1][1] == per_gpu * world
+            for (a, b, _), (c, d, _) in zip(spans, spans[1:]):
+                assert b == c
+            assert all(b - a == per_gpu for a, b, _ in spans)
