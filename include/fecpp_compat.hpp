@@ -31,6 +31,10 @@ namespace fecpp
 	using std::size_t;
 	using byte = std::uint8_t;
 
+#if defined(__i386__)|| defined(__amd64__) || defined(__x86_64__) || defined(_M_IX86) || defined(_M_X64) || defined(_M_AMD64)
+#define FECPP_IS_X86
+#endif
+
 	class fec_code
 	{
 	public:
@@ -133,6 +137,13 @@ namespace fecpp
 			if (rc < 0) throw std::runtime_error(std::string(what) + ": HIP failure " + std::to_string(rc));
 		}
 	};
+
+#if defined(FECPP_IS_X86)
+	/* fecpp.hpp:83-85.  Declared so that code naming it still compiles; deliberately NOT defined: it is the
+	 * reference's SSSE3 inner loop, nothing outside fecpp calls it, and this drop-in has no
+	 * CPU compute path -- a use fails at link time instead of silently running on the host. */
+	size_t addmul_ssse3(uint8_t z[], const uint8_t x[], uint8_t y, size_t size);
+#endif
 }
 
 #endif

@@ -44,7 +44,9 @@ typedef struct kfec_ctx kfec_ctx;
 /* Create a coder for K data shares out of N (1 <= K <= N <= 256).  Builds the N x K systematic encoding
  * matrix on the device.  KFEC_EINVAL on a K/N violation, KFEC_ENODEV without a GPU. */
 int kfec_create(size_t K, size_t N, kfec_ctx **out);
-/* reset_martix(K, N) (fecpp.cpp:437-451): re-targets an existing coder; on KFEC_EINVAL the coder is unchanged. */
+/* reset_martix(K, N) (fecpp.cpp:437-451): re-targets an existing coder.  On any error (KFEC_EINVAL, or a
+ * failed allocation / launch) the coder is unchanged: the new matrix is committed only once built.
+ * Batch queues (kfec_pipeline.h) created on the coder must be recreated after a reset. */
 int kfec_reset(kfec_ctx *ctx, size_t K, size_t N);
 void kfec_destroy(kfec_ctx *ctx);
 size_t kfec_get_K(const kfec_ctx *ctx);
@@ -66,7 +68,9 @@ int kfec_encode(const kfec_ctx *ctx, const uint8_t *input, size_t data_length, s
  * the reference (data share i fills row i; each missing row takes the highest unused id), then writes the
  * recovered missing DATA shares in ascending index order: out_ids[*n_out] and out[*n_out * share_size]
  * (capacity: K entries).  KFEC_EMPTY (with *n_out = 0) when the reference returns {}: fewer than K shares,
- * or a chosen share id >= N.  No data share missing -> KFEC_OK with *n_out = 0 (the reference's empty map). */
+ * or a chosen share id >= N.  No data share missing -> KFEC_OK with *n_out = 0 (the reference's empty map).
+ * share_size == 0 -> KFEC_OK with the missing data ids in out_ids and no bytes (the reference's map of
+ * empty vectors, fecpp.cpp:572-583). */
 int kfec_decode(const kfec_ctx *ctx, const size_t *share_ids, const uint8_t *const *share_ptrs,
                 size_t n_shares, size_t share_size, size_t *out_ids, uint8_t *out, size_t *n_out);
 
@@ -75,9 +79,9 @@ int kfec_decode(const kfec_ctx *ctx, const size_t *share_ids, const uint8_t *con
  *   d_data    [G][K][pitch]   data shards of group g
  *   d_parity  [G][R][pitch]   parity shards
  * The code is byte-column independent, so any pitch works.  When pitch and every base pointer are
- * multiples of 4 the kernels move 32-byte granules (the last one of a row dword by dword) and may read and
- * write bytes [B, ceil(B/4)*4) of a slot, which lie inside the slot's pitch; otherwise they move bytes
- * and touch only [0, B).  Bytes [0, B) are bit-exact with the reference. */
+ * multiples of 4 the kernels move 32-byte granules (the last one of a row ending at ceil(B/4)*4) and may
+ * read and write bytes [B, ceil(B/4)*4) of a slot, which lie inside the slot's pitch; otherwise they move
+ * bytes and touch only [0, B).  Bytes [0, B) are bit-exact with the reference. */
 
 /* Parity of G groups: d_parity[g][r] = XOR_j enc[K+r][j] * d_data[g][j]. */
 int kfec_encode_batch(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch, const void *d_data,
@@ -88,7 +92,9 @@ size_t kfec_decode_workspace_size(const kfec_ctx *ctx, size_t G);
 
 /* Recover missing data shards of G groups in place-free fashion.
  *   d_present [G][4] uint64: bit s of group g set <=> shard s (data s < K, parity s - K) is present.
- *     Absent slots of d_data / d_parity are never read.  Bits >= N are ignored.
+ *     Absent slots of d_data / d_parity are never read.  Bits >= N are ignored: the batch layout has no
+ *     slot for a share id >= N, so the reference's "a chosen id >= N returns {}" (fecpp.cpp:550-551) cannot
+ *     arise here; callers holding such ids (kcptube never sends them: sub_sn < N) use kfec_decode.
  *   d_out     [G][R][pitch]: recovered shard t of group g (ascending data index) in slot t.
  *   d_out_idx [G][R] uint8:  data index of recovered slot t, 0xFF for unused slots.
  *   d_status  [G] uint8:     KFEC_GROUP_OK / KFEC_GROUP_EMPTY / KFEC_GROUP_SINGULAR.

@@ -166,8 +166,10 @@ int kfec_group_scatter(const kfec_ctx *ctx, size_t P, const kfec_pkt_hdr *d_hdr,
  * (encrypt_data returns "empty data") or one that does not fit in dst_pitch.  Bytes after the sealed packet
  * up to the next multiple of 4 are written as zero.
  * d_dst == NULL seals in place (checksum mode only): the two checksum bytes are written right after each
- * packet in d_src (the caller leaves them room, e.g. pkt_pitch >= packet + 2 after kfec_pack_batch) and
- * nothing else is written -- the CRC reads each packet once. */
+ * packet in d_src and nothing else is written -- the CRC reads each packet once.  dst_pitch is then the size
+ * of each packet's slot from d_off[p] (e.g. pkt_pitch after kfec_pack_batch, whose packets may fill their
+ * slot): a packet with len + 2 > dst_pitch, or whose trailer would pass src_bytes, gets d_out_len = 0 and
+ * is left untouched, as one that does not fit dst_pitch out of place.  dst_pitch == 0 is KFEC_EINVAL. */
 int kfec_seal_batch(int mode, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
                     const uint32_t *d_len, void *d_dst, size_t dst_pitch, uint32_t *d_out_len, void *stream);
 

@@ -24,7 +24,8 @@
  *
  * Threading: a kfec_tx / kfec_rx and its queue are used from one thread at a time (the reference serialises
  * with mutex_fec_snd / mutex_fec_rcv, connections.hpp:609-611).  Destroy the kfec_tx / kfec_rx of a queue
- * before the queue.
+ * before the queue.  A queue is sized for its coder's K / N: after kfec_reset (reset_martix) of that coder
+ * every push / send / flush of the queue returns KFEC_EINVAL -- recreate the queues.
  * Staging: datagrams and shards are copied once, into the queue's pinned arena, when they arrive; finished
  * 8 MiB stretches of it go H2D on the queue's own copy stream while the host keeps filling it, so a flush
  * waits only for the tail, the kernels and the D2H of its results.
@@ -53,6 +54,8 @@ typedef struct kfec_rx kfec_rx;
 int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram, kfec_txq **out);
 void kfec_txq_destroy(kfec_txq *q);
 size_t kfec_txq_pending(const kfec_txq *q);
+/* Bytes of the queue's datagram staging arena (it grows only when the live partial groups fill it). */
+size_t kfec_txq_capacity(const kfec_txq *q);
 
 /* One connection direction's fec_maker state: conv is the KCP conversation id written into redundant
  * packets (0: the reference builds no FEC groups for this connection). */
@@ -83,6 +86,9 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
 int kfec_rxq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_shard, kfec_rxq **out);
 void kfec_rxq_destroy(kfec_rxq *q);
 size_t kfec_rxq_pending(const kfec_rxq *q);
+/* Bytes of the queue's shard staging arena: when it is full the bytes of restored, evicted and overwritten
+ * shards are reclaimed first, and it doubles only when the groups still waiting for K shares fill it. */
+size_t kfec_rxq_capacity(const kfec_rxq *q);
 
 int kfec_rx_create(kfec_rxq *q, uint64_t tag, kfec_rx **out);
 void kfec_rx_destroy(kfec_rx *rx);

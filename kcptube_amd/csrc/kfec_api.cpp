@@ -47,17 +47,26 @@ int probe_device(kfec::DeviceInfo &di)
     return KFEC_OK;
 }
 
-int build_matrix(kfec_ctx *c)
+// Build the (K, N) matrix into fresh buffers and commit K, N and the matrix only once all of it succeeded:
+// a failed reset leaves the context exactly as it was (the compat class keeps its old K and N too).
+int build_matrix(kfec_ctx *c, size_t K, size_t N)
 {
-    const size_t bytes = c->N * c->K;
-    if (c->d_enc) (void)hipFree(c->d_enc);
-    c->d_enc = nullptr;
-    if (hipMalloc(&c->d_enc, kfec::enc_alloc_bytes(c->K, c->N)) != hipSuccess) return KFEC_ENOMEM;
-    if (kfec::launch_build_matrix(c->d_enc, (int)c->K, (int)c->N, c->stream)) return KFEC_EHIP;
-    c->h_enc.assign(bytes, 0);
-    if (hipMemcpyAsync(c->h_enc.data(), c->d_enc, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+    const size_t bytes = N * K;
+    uint8_t *d = nullptr;
+    if (hipMalloc(&d, kfec::enc_alloc_bytes(K, N)) != hipSuccess) return KFEC_ENOMEM;
+    std::vector<uint8_t> h(bytes, 0);
+    if (kfec::launch_build_matrix(d, (int)K, (int)N, c->stream) ||
+        hipMemcpyAsync(h.data(), d, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(d);
         return KFEC_EHIP;
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return KFEC_EHIP;
+    }
+    if (c->d_enc) (void)hipFree(c->d_enc);  // the stream is idle: no launch still reads the old matrix
+    c->d_enc = d;
+    c->h_enc.swap(h);
+    c->K = K;
+    c->N = N;
     return KFEC_OK;
 }
 
@@ -124,14 +133,12 @@ int kfec_create(size_t K, size_t N, kfec_ctx **out)
     if (rc) return rc;
     kfec_ctx *c = new (std::nothrow) kfec_ctx;
     if (!c) return KFEC_ENOMEM;
-    c->K = K;
-    c->N = N;
     c->di = di;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return KFEC_EHIP;
     }
-    rc = build_matrix(c);
+    rc = build_matrix(c, K, N);
     if (rc) {
         kfec_destroy(c);
         return rc;
@@ -145,9 +152,7 @@ int kfec_reset(kfec_ctx *ctx, size_t K, size_t N)
     if (!ctx || !kn_valid(K, N)) return KFEC_EINVAL;  // reference throws before touching its state
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (set_dev(ctx)) return KFEC_EHIP;
-    ctx->K = K;
-    ctx->N = N;
-    return build_matrix(ctx);
+    return build_matrix(ctx, K, N);
 }
 
 void kfec_destroy(kfec_ctx *ctx)
@@ -221,7 +226,19 @@ int kfec_decode(const kfec_ctx *cctx, const size_t *share_ids, const uint8_t *co
     // fecpp.cpp:550-551: a chosen id >= N returns {}.  Ids >= N are the highest ids, so they are chosen
     // first whenever a data share is missing; with none missing the reference returns {} anyway.
     if (n_shares && share_ids[n_shares - 1] >= N) return KFEC_EMPTY;
-    if (B == 0) return KFEC_OK;
+    if (B == 0) {
+        // nothing to compute, but the reference still returns one (empty) block per missing data row
+        // (fecpp.cpp:572-583): the data ids below K that are not among the shares, ascending
+        size_t m = 0, i = 0;
+        for (size_t d = 0; d < K; ++d) {
+            while (i < n_shares && share_ids[i] < d) ++i;
+            if (i < n_shares && share_ids[i] == d) continue;
+            if (!out_ids) return KFEC_EINVAL;
+            out_ids[m++] = d;
+        }
+        *n_out = m;
+        return KFEC_OK;
+    }
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (set_dev(ctx)) return KFEC_EHIP;
     const size_t o_data = 0, o_par = al256(K * B), o_out = o_par + al256(R * B), o_mask = o_out + al256(R * B);
@@ -528,7 +545,8 @@ int kfec_group_scatter(const kfec_ctx *ctx, size_t P, const kfec_pkt_hdr *d_hdr,
 int kfec_seal_batch(int mode, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
                     const uint32_t *d_len, void *d_dst, size_t dst_pitch, uint32_t *d_out_len, void *stream)
 {
-    if ((mode != KFEC_SEAL_CHECKSUM && mode != KFEC_SEAL_PLAIN_XOR) || dst_pitch % 4) return KFEC_EINVAL;
+    if (mode != KFEC_SEAL_CHECKSUM && mode != KFEC_SEAL_PLAIN_XOR) return KFEC_EINVAL;
+    if (d_dst ? dst_pitch % 4 != 0 : dst_pitch == 0) return KFEC_EINVAL;  // in place: dst_pitch = slot size
     if (!d_dst && mode != KFEC_SEAL_CHECKSUM) return KFEC_EINVAL;  // in place: checksum mode only
     if (P && (!d_src || !al4(d_src) || !d_off || !d_len || (d_dst && !al4(d_dst)) || !d_out_len)) return KFEC_EINVAL;
     int n = 0;

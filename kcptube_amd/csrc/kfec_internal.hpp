@@ -14,14 +14,22 @@ namespace kfec {
 //   [4, 4+K4)              src[j]     share id used as column j of the selected K x K system,
 //   [4+K4, 4+K4+R*K4)      coef[u][j] row u (u < m) of the inverse decode matrix for missing shard u,
 // with K4 = K rounded up to 4 so that the prep kernel writes whole dwords.  Syndrome form (R <= 8, see
-// write_syn in kfec_kernels.hip): [0] status, [1] m, [2] used-parity bits, [8, 72) the 8 x 8 C matrix.
+// write_syn in kfec_kernels.hip): [0] status, [1] m, [2] used-parity bits, [8, 40) present data bits,
+// [40, 104) the 8 x 8 C matrix.
 inline size_t rec_k4(size_t K) { return (K + 3) & ~size_t(3); }
 inline size_t record_stride(size_t K, size_t R)
 {
     const size_t coef = (4 + rec_k4(K) + R * rec_k4(K) + 15) & ~size_t(15);
-    return coef > 80 ? coef : 80;
+    return coef > 112 ? coef : 112;
 }
-inline size_t decode_workspace_bytes(size_t G, size_t K, size_t R) { return (G * record_stride(K, R) + 255) & ~size_t(255); }
+// after the G records (256-aligned): the syndrome decode's active-group list -- a count (+ 252 bytes of
+// padding), per-1024-group chunk counts / offsets, then the list of up to G group ids (uint32 each)
+inline size_t decode_list_offset(size_t G, size_t K, size_t R) { return (G * record_stride(K, R) + 255) & ~size_t(255); }
+inline size_t decode_list_chunks(size_t G) { return (G + 1023) / 1024; }
+inline size_t decode_workspace_bytes(size_t G, size_t K, size_t R)
+{
+    return decode_list_offset(G, K, R) + 256 + 4 * decode_list_chunks(G) + 4 * G;
+}
 
 // The encoding matrix allocation also holds the perm-MAC tables of its parity rows (gf_perm_tables, 5 dwords
 // per coefficient) for the encode kernel, laid out [K][R + 8][5]: shard-major so that the rows of one shard

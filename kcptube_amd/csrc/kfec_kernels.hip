@@ -39,7 +39,13 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 
 // build-time tuning knobs (tools/ab.py builds variants; the shipped library uses the defaults)
 #ifndef KFEC_PD
-#define KFEC_PD 4  // shards in flight per lane (halved for 32-byte granules)
+#define KFEC_PD 4  // granules per lane in the load pipeline of the 32-byte shape (PD - 1 in flight during a MAC)
+#endif
+#ifndef KFEC_SYN_MAX_R
+#define KFEC_SYN_MAX_R 8  // decode in syndrome form up to this R (0: coefficient form always; A/B builds)
+#endif
+#ifndef KFEC_SYN_MINW
+#define KFEC_SYN_MINW 1  // __launch_bounds__ minimum waves per SIMD of the syndrome-form decode kernel
 #endif
 #ifndef KFEC_MINW
 #define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the MAC kernels
@@ -194,11 +200,13 @@ __device__ __forceinline__ void write_empty(const PrepArgs &a, uint64_t g, uint8
 }
 
 // Syndrome-form record (syn_kernel, R <= 8): [0] status 0, [1] m, [2] bit r set = parity row K + r is one
-// of the m shares used, [3..7] 0, [8 + 8u + r] = C[u][r] = Sinv[u][t] for the rank t with P_t = K + r
-// (0 for unused rows and for u >= m): all 8 rows are written so any row tile RT <= 8 reads zeros beyond m.
+// of the m shares used, [3..7] 0, [8, 40) the present DATA shard bits (4 x u64, so the MAC kernel gets
+// its header and the first 64 bits in one 16-byte load), [40 + 8u + r] = C[u][r] = Sinv[u][t] for the rank
+// t with P_t = K + r (0 for unused rows and for u >= m): all 8 rows are written so any row tile RT <= 8
+// reads zeros beyond m.
 template <int MAXM, typename F>
 __device__ __forceinline__ void write_syn(const PrepArgs &a, uint64_t g, int m, const int (&M)[MAXM],
-                                          const int (&P)[MAXM], F sinv)
+                                          const int (&P)[MAXM], const uint64_t (&w)[4], F sinv)
 {
     uint64_t *rw = reinterpret_cast<uint64_t *>(a.rec + g * a.rec_stride);
     uint32_t used = 0;
@@ -217,9 +225,11 @@ __device__ __forceinline__ void write_syn(const PrepArgs &a, uint64_t g, int m, 
     }
     rw[0] = (uint64_t)(((uint32_t)m << 8) | (used << 16));
 #pragma unroll
-    for (int u = 0; u < MAXM; ++u) rw[1 + u] = row[u];
+    for (int q = 0; q < 4; ++q) rw[1 + q] = w[q] & bits_below(a.K, q);
 #pragma unroll
-    for (int u = MAXM; u < 8; ++u) rw[1 + u] = 0;
+    for (int u = 0; u < MAXM; ++u) rw[5 + u] = row[u];
+#pragma unroll
+    for (int u = MAXM; u < 8; ++u) rw[5 + u] = 0;
 #pragma unroll
     for (int t = 0; t < MAXM; ++t)
         if (t < a.R) a.out_idx[g * a.R + t] = (t < m) ? (uint8_t)M[t] : (uint8_t)0xFF;
@@ -301,7 +311,7 @@ __global__ void __launch_bounds__(kBlock) decode_prep_small(PrepArgs a)
             continue;
         }
         if (a.syn) {
-            write_syn<MAXM>(a, g, m, M, P, [&](int u, int t) { return Iv[u][t]; });
+            write_syn<MAXM>(a, g, m, M, P, w, [&](int u, int t) { return Iv[u][t]; });
             continue;
         }
         rec[0] = 0;
@@ -460,7 +470,7 @@ __global__ void __launch_bounds__(kBlock) decode_prep_perm(PrepArgs a)
             continue;
         }
         if (a.syn) {
-            write_syn<MAXM>(a, g, m, M, P, [&](int u, int t) { return (Iv[u] >> (8 * t)) & 0xFFu; });
+            write_syn<MAXM>(a, g, m, M, P, w, [&](int u, int t) { return (Iv[u] >> (8 * t)) & 0xFFu; });
             continue;
         }
         rec[0] = 0;
@@ -738,37 +748,20 @@ __device__ __forceinline__ void store_gran(uint8_t *p, const uint32_t *d, uint32
     }
 }
 
-// Last granule of a shard row when B is not a multiple of VEC (e.g. B = 1400 at VEC = 32): only the nd
-// dwords that hold bytes below B are loaded / stored (bytes [B, 4*ceil(B/4)) lie inside the pitch), so no
-// lane reads or writes past its own slot -- pitch only needs to be a multiple of 4.
+// Byte offset of a lane's granule in a shard row: VB * col, except that the last granule of a row whose B
+// is not a multiple of VB is moved back to end at round4(B).  It then overlaps the previous granule, whose
+// output bytes it recomputes identically (the MAC is column-wise: output byte i depends only on byte i of
+// every share), so every lane loads and stores one whole granule and the shard loop has no per-lane branch.
+// (A per-lane "tail" branch around the loads made hipcc wait for every load right where it was issued --
+// the two paths define the granule registers differently -- so nothing was in flight across shards.)
+// Bytes in [B, round4(B)) are read and written, inside the slot (pitch % 4 == 0); the host only takes
+// VB > 4 when B >= VB.
 template <int VEC>
-__device__ __forceinline__ Gran<VEC> load_gran_tail(const uint8_t *p, uint32_t nd)
+__device__ __forceinline__ uint32_t gran_off(uint32_t col, uint32_t B)
 {
-    Gran<VEC> v;
-#pragma unroll
-    for (int w = 0; w < Gran<VEC>::W; ++w) v.d[w] = (uint32_t)w < nd ? reinterpret_cast<const uint32_t *>(p)[w] : 0u;
-    return v;
-}
-
-template <int VEC>
-__device__ __forceinline__ void store_gran_tail(uint8_t *p, const uint32_t *d, uint32_t nd)
-{
-#pragma unroll
-    for (int w = 0; w < Gran<VEC>::W; ++w)
-        if ((uint32_t)w < nd) reinterpret_cast<uint32_t *>(p)[w] = d[w];
-}
-
-template <int VEC>
-__device__ __forceinline__ Gran<VEC> load_any(const uint8_t *p, uint32_t col, uint32_t B, uint32_t nd)
-{
-    return nd < (uint32_t)Gran<VEC>::W ? load_gran_tail<VEC>(p, nd) : load_gran<VEC>(p, col, B);
-}
-
-template <int VEC>
-__device__ __forceinline__ void store_any(uint8_t *p, const uint32_t *d, uint32_t col, uint32_t B, uint32_t nd)
-{
-    if (nd < (uint32_t)Gran<VEC>::W) store_gran_tail<VEC>(p, d, nd);
-    else store_gran<VEC>(p, d, col, B);
+    constexpr uint32_t VB = VEC >= 4 ? VEC : 4;
+    if constexpr (VEC >= 4) return min(col * VB, ((B + 3) & ~3u) - VB);
+    return col * 4;
 }
 
 template <int MT>
@@ -842,7 +835,8 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     constexpr int W = Gran<VEC>::W;
     // shards in flight per lane (~64 B per lane); PDX: the latency shape (a handful of groups, often read
     // straight from pinned host memory) keeps many more loads in flight so the PCIe round trips overlap
-    constexpr int PD = PDX ? PDX : (VEC >= 32 ? KFEC_PD / 2 : KFEC_PD);
+    // (MT = 8, the VALU-bound tall tiles: 2, to keep 3 waves per SIMD)
+    constexpr int PD = PDX ? PDX : (VEC >= 32 ? (MT >= 8 ? 2 : KFEC_PD) : 2 * KFEC_PD);
     constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
 
@@ -861,9 +855,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     const bool in = item < a.total;
     const uint32_t g = in ? item / cols : 0;
     const uint32_t col = in ? item - g * cols : 0;
-    // dwords of this lane's granule below B: W except in the last granule of a row when VEC does not
-    // divide B (VEC >= 4 only; the bytewise VEC = 1 path checks every byte itself)
-    const uint32_t nd = (VEC >= 4 && (col + 1) * VB > a.B) ? (a.B - col * VB + 3) / 4 : (uint32_t)W;
+    const uint32_t off = gran_off<VEC>(col, a.B);
     const uint32_t gfirst = base / cols;
     const uint32_t glast = min(base + kMacBlock - 1, a.total - 1) / cols;
     const uint32_t ng = glast - gfirst + 1;
@@ -885,7 +877,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
 #pragma unroll
         for (int w = 0; w < W; ++w) acc[r][w] = 0;
 
-    const uint8_t *enc_base = a.data + ((uint64_t)g * K) * a.pitch + (uint64_t)col * VB;
+    const uint8_t *enc_base = a.data + ((uint64_t)g * K) * a.pitch + off;
     for (uint32_t c0 = 0; c0 < K; c0 += a.JC) {
         const uint32_t nj = min(a.JC, K - c0);
         if (!enc_once) {
@@ -897,47 +889,53 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
         const uint8_t *ent0 = s_ent + (gs * a.JC) * L::ENTRY;
         auto share_ptr = [&](uint32_t jj) -> const uint8_t * {
             if constexpr (DEC) {
-                return *reinterpret_cast<const uint8_t *const *>(ent0 + jj * L::ENTRY) + (uint64_t)col * VB;
+                return *reinterpret_cast<const uint8_t *const *>(ent0 + jj * L::ENTRY) + off;
             } else {
                 return enc_base + (uint64_t)(c0 + jj) * a.pitch;
             }
         };
+        auto mac = [&](const Gran<VEC> &cur, uint32_t jj) {
+            const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + jj * L::ENTRY + 16);
+            uint32_t t[L::TBL_DW];
+#pragma unroll
+            for (int i = 0; i < L::TBL_DW / 4; ++i) {
+                const uint4 q = tv[i];
+                t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+            }
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint32_t xv = cur.d[w];
+                const uint32_t s0 = xv & 0x07070707u;
+                const uint32_t s1 = (xv >> 3) & 0x07070707u;
+                const uint32_t s2 = (xv >> 6) & 0x03030303u;
+#pragma unroll
+                for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+            }
+        };
+        // PD shards in flight.  Every load is unconditional (past the end it re-reads the last shard, a
+        // cache hit): a load under a branch makes hipcc wait for it at the branch's join, i.e. at issue.
         Gran<VEC> x[PD];
 #pragma unroll
-        for (int u = 0; u < PD; ++u)
-            if ((uint32_t)u < nj) x[u] = load_any<VEC>(share_ptr(u), col, a.B, nd);
-        for (uint32_t jb = 0; jb < nj; jb += PD) {
+        for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min((uint32_t)u, nj - 1)), col, a.B);
+        uint32_t jb = 0;
+        for (; jb + PD <= nj; jb += PD) {
 #pragma unroll
             for (int u = 0; u < PD; ++u) {
-                const uint32_t jj = jb + u;
-                if (jj < nj) {
-                    const Gran<VEC> cur = x[u];
-                    if (jj + PD < nj) x[u] = load_any<VEC>(share_ptr(jj + PD), col, a.B, nd);
-                    const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + jj * L::ENTRY + 16);
-                    uint32_t t[L::TBL_DW];
-#pragma unroll
-                    for (int i = 0; i < L::TBL_DW / 4; ++i) {
-                        const uint4 q = tv[i];
-                        t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
-                    }
-#pragma unroll
-                    for (int w = 0; w < W; ++w) {
-                        const uint32_t xv = cur.d[w];
-                        const uint32_t s0 = xv & 0x07070707u;
-                        const uint32_t s1 = (xv >> 3) & 0x07070707u;
-                        const uint32_t s2 = (xv >> 6) & 0x03030303u;
-#pragma unroll
-                        for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
-                    }
-                }
+                // consume, then refill the same registers: PD - 1 granules stay in flight during the MAC
+                // (loading first would need a fresh register set and a copy -- and a wait -- per iteration)
+                mac(x[u], jb + u);
+                x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
             }
         }
+#pragma unroll
+        for (int u = 0; u < PD; ++u)
+            if (jb + u < nj) mac(x[u], jb + u);
     }
     if (rows) {
-        const uint64_t obase = ((uint64_t)g * a.R + row0) * a.pitch + (uint64_t)col * VB;
+        const uint64_t obase = ((uint64_t)g * a.R + row0) * a.pitch + off;
 #pragma unroll
         for (int r = 0; r < MT; ++r)
-            if ((uint32_t)r < rows) store_any<VEC>(a.out + obase + (uint64_t)r * a.pitch, acc[r], col, a.B, nd);
+            if ((uint32_t)r < rows) store_gran<VEC>(a.out + obase + (uint64_t)r * a.pitch, acc[r], col, a.B);
     }
 }
 
@@ -962,10 +960,11 @@ struct SynArgs {
     const uint8_t *parity;    // [G][R][pitch]
     uint8_t *out;             // [G][R][pitch] recovered data shards, ascending index
     const uint8_t *rec;       // syndrome-form records (kfec_internal.hpp)
-    const uint64_t *present;  // [G][4]
     const uint32_t *etab;     // [K][etab_rows][5] perm tables of the parity rows (zero slack rows)
+    const uint32_t *list;     // ascending ids of the groups with data to recover (active_* kernels)
+    const uint32_t *list_count;
     uint64_t pitch;
-    uint32_t total, cols, G, K, R, B, rec_stride, etab_rows;
+    uint32_t total, cols, cols_pad, G, K, R, B, rec_stride, etab_rows;
 };
 
 template <int RT>
@@ -973,147 +972,330 @@ struct SynLayout {
     static constexpr int TD = ((5 * RT + 3) / 4) * 4;  // table dwords per (group, output row u): RT tables
 };
 
-template <int VEC, int RT, int PDX = 0>
-__global__ void __launch_bounds__(kMacBlock, KFEC_MINW) syn_kernel(SynArgs a)
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+// One granule at byte offset o of a buffer resource.  An offset beyond the resource returns zeros and
+// touches no memory: that is how an absent share is "not loaded" without a per-lane branch.
+template <int VEC>
+__device__ __forceinline__ Gran<VEC> bload(__amdgpu_buffer_rsrc_t r, uint32_t o)
+{
+    static_assert(VEC == 32 || VEC == 4, "dword granules");
+    Gran<VEC> v;
+    if constexpr (VEC == 32) {
+        const u32x4v x = __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0);
+        const u32x4v y = __builtin_amdgcn_raw_buffer_load_b128(r, o + 16u, 0, 0);
+        v.d[0] = x.x; v.d[1] = x.y; v.d[2] = x.z; v.d[3] = x.w;
+        v.d[4] = y.x; v.d[5] = y.y; v.d[6] = y.z; v.d[7] = y.w;
+    } else {
+        v.d[0] = __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, 0);
+    }
+    return v;
+}
+
+constexpr uint32_t kAbsent = 0x80000000u;  // beyond every resource (the host keeps them below 2^31 bytes)
+
+// C tables of one group into LDS: tp[u * TD + 5 r + i] (zero for a group that recovers nothing)
+template <int RT>
+__device__ __forceinline__ void syn_expand_one(const uint8_t *rec, uint32_t ur, uint32_t *tp)
+{
+    constexpr int TD = SynLayout<RT>::TD;
+    const uint32_t u = ur / RT, r = ur - u * RT;
+    uint32_t t[5];
+    gf_perm_tables(rec[0] == 0 ? rec[40 + 8 * u + r] : 0u, t);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) tp[u * TD + 5 * r + i] = t[i];
+}
+
+// y_r = parity_r ^ XOR_{j present} E[r][j] * D_j for one lane's column (rd / rp: resources over its group's
+// data / parity rows, drow / prow: byte offsets of the lane's granule in the group's first data / parity row)
+template <int VEC, int RT, int PD>
+__device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][Gran<VEC>::W], __amdgpu_buffer_rsrc_t rd,
+                                         __amdgpu_buffer_rsrc_t rp, uint32_t drow, uint32_t prow, uint32_t used,
+                                         uint64_t p0, const uint8_t *rec)
 {
     constexpr int W = Gran<VEC>::W;
-    constexpr int PD = PDX ? PDX : (VEC >= 32 ? KFEC_PD / 2 : KFEC_PD);
-    constexpr int VB = VEC >= 4 ? VEC : 4;
-    constexpr int TD = SynLayout<RT>::TD;
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_ct[];  // [gmax][RT][TD]
+    const uint32_t K = a.K, pitch = (uint32_t)a.pitch;
+    // the parity shares of the rows in use start the accumulators (issued with the first data loads)
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+        const Gran<VEC> y = bload<VEC>(rp, ((used >> r) & 1u) ? prow + r * pitch : kAbsent);
+#pragma unroll
+        for (int w = 0; w < W; ++w) acc[r][w] = y.d[w];
+    }
+    const uint64_t *pr = reinterpret_cast<const uint64_t *>(rec + 8);
+    const uint64_t p1 = K > 64 ? pr[1] : 0ull, p2 = K > 128 ? pr[2] : 0ull, p3 = K > 192 ? pr[3] : 0ull;
+    auto dofs = [&](uint32_t j) -> uint32_t {
+        const uint64_t wq = j < 64 ? p0 : (j < 128 ? p1 : (j < 192 ? p2 : p3));
+        return ((wq >> (j & 63u)) & 1ull) ? drow + j * pitch : kAbsent;
+    };
+    typedef const __attribute__((address_space(4))) uint32_t cu32;  // uniform: scalar loads into SGPRs
+    auto mac = [&](const Gran<VEC> &cur, uint32_t j) {
+        const cu32 *tg = (const cu32 *)(a.etab + (size_t)j * a.etab_rows * 5);
+        uint32_t t[5 * RT];
+#pragma unroll
+        for (int i = 0; i < 5 * RT; ++i) t[i] = tg[i];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint32_t xv = cur.d[w];
+            const uint32_t s0 = xv & 0x07070707u;
+            const uint32_t s1 = (xv >> 3) & 0x07070707u;
+            const uint32_t s2 = (xv >> 6) & 0x03030303u;
+#pragma unroll
+            for (int r = 0; r < RT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+        }
+    };
+    // PD shards in flight, every load unconditional (see mac_kernel)
+    Gran<VEC> x[PD];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) x[u] = bload<VEC>(rd, dofs(min((uint32_t)u, K - 1)));
+    uint32_t jb = 0;
+    for (; jb + PD <= K; jb += PD) {
+#pragma unroll
+        for (int u = 0; u < PD; ++u) {
+            mac(x[u], jb + u);
+            x[u] = bload<VEC>(rd, dofs(min(jb + u + PD, K - 1)));
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PD; ++u)
+        if (jb + u < K) mac(x[u], jb + u);
+}
 
+// out_u = XOR_r C[u][r] * y_r for u < m, stored to recovered slot u of group g
+template <int VEC, int RT>
+__device__ __forceinline__ void syn_final(const SynArgs &a, const uint32_t (&acc)[RT][Gran<VEC>::W], const uint32_t *ct,
+                                          uint32_t m, uint32_t g, uint32_t off, uint32_t col)
+{
+    constexpr int W = Gran<VEC>::W;
+    constexpr int TD = SynLayout<RT>::TD;
+    const uint64_t obase = ((uint64_t)g * a.R) * a.pitch + off;
+#pragma unroll
+    for (int u = 0; u < RT; ++u) {
+        if ((uint32_t)u < m) {
+            uint32_t t[TD];
+            const uint4 *tv = reinterpret_cast<const uint4 *>(ct + u * TD);
+#pragma unroll
+            for (int i = 0; i < TD / 4; ++i) {
+                const uint4 q = tv[i];
+                t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+            }
+            uint32_t o[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int r = 0; r < RT; ++r) {
+                    const uint32_t yv = acc[r][w];
+                    v = perm_mac(v, t + 5 * r, yv & 0x07070707u, (yv >> 3) & 0x07070707u, (yv >> 6) & 0x03030303u);
+                }
+                o[w] = v;
+            }
+            store_gran<VEC>(a.out + obase + (uint64_t)u * a.pitch, o, col, a.B);
+        }
+    }
+}
+
+// Two launch shapes, chosen per launch ON THE DEVICE from the number of groups with data to recover (the
+// prep's list count; no host round trip).  Both kernels are launched; the one not chosen exits at once.
+//  * dense (syn_kernel: most groups lost a data shard, e.g. the m = R benchmark configs): lane = (group,
+//    column) over all groups, exactly the encode's item order; groups with nothing to recover issue no loads;
+//  * listed (syn_list_kernel: few groups lost data, e.g. a live link at ~1% loss, where fec_find_missings
+//    decodes every group that reached K shares, client.cpp:923-925): one wave per (listed group, 64 columns),
+//    persistent over the ascending list of active groups only, so the work is proportional to the groups that
+//    lost data instead of to the waves that hold one of them.
+// Listed is taken when it needs fewer lanes: cnt * cols_pad < G * cols.
+__device__ __forceinline__ bool syn_listed(const SynArgs &a, uint32_t cnt)
+{
+    return (uint64_t)cnt * a.cols_pad < (uint64_t)a.G * a.cols;
+}
+
+template <int VEC, int RT, int PDX = 0>
+__global__ void __launch_bounds__(kMacBlock) syn_list_kernel(SynArgs a)
+{
+    constexpr int W = Gran<VEC>::W;
+    constexpr int PD = PDX ? PDX : (VEC >= 32 ? KFEC_PD : 2 * KFEC_PD);
+    constexpr int TD = SynLayout<RT>::TD;
+    __shared__ __attribute__((aligned(16))) uint32_t s_ct[kMacBlock / 64][RT * TD];
+    const uint32_t cnt = *a.list_count;
+    if (!syn_listed(a, cnt)) return;
+    const uint32_t wpg = a.cols_pad / 64;  // waves per group
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t *ct = s_ct[threadIdx.x / 64];  // this wave's C tables (written and read by this wave only)
+    const uint32_t tasks = cnt * wpg;
+    for (uint32_t t = blockIdx.x * (kMacBlock / 64) + threadIdx.x / 64; t < tasks; t += gridDim.x * (kMacBlock / 64)) {
+        const uint32_t li = __builtin_amdgcn_readfirstlane(t / wpg);
+        const uint32_t col = (t - li * wpg) * 64 + lane;
+        const uint32_t g = __builtin_amdgcn_readfirstlane(a.list[li]);
+        const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
+        if (lane < RT * RT) syn_expand_one<RT>(rec, lane, ct);
+        const bool in = col < a.cols;
+        const uint32_t off = gran_off<VEC>(in ? col : 0u, a.B);
+        const uint4 h = *reinterpret_cast<const uint4 *>(rec);  // header + present data bits 0..63
+        const uint32_t m = (h.x >> 8) & 0xFFu;  // listed groups have status 0 and m > 0
+        const uint32_t used = (h.x >> 16) & 0xFFu;
+        const uint64_t p0 = (uint64_t)h.z | ((uint64_t)h.w << 32);
+        uint32_t acc[RT][W];
+        if (in) {
+            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(a.data + (uint64_t)g * a.K * a.pitch), (short)0, (int)(a.K * a.pitch), 0x00020000);
+            const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(a.parity + (uint64_t)g * a.R * a.pitch), (short)0, (int)(a.R * a.pitch), 0x00020000);
+            syn_loop<VEC, RT, PD>(a, acc, rd, rp, off, off, used, p0, rec);
+        }
+        // the tables were written by lanes of this wave: LDS operations of one wave complete in order, the
+        // fence keeps the compiler from moving the reads above the writes
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (in) syn_final<VEC, RT>(a, acc, ct, m, g, off, col);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the next task rewrites the tables
+    }
+}
+
+template <int VEC, int RT, int PDX = 0>
+__global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a)
+{
+    constexpr int W = Gran<VEC>::W;
+    constexpr int PD = PDX ? PDX : (VEC >= 32 ? KFEC_PD : 2 * KFEC_PD);
+    constexpr int TD = SynLayout<RT>::TD;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ct[];  // [group slot][RT][TD]
+    if (syn_listed(a, *a.list_count)) return;  // the listed kernel has it (whole workgroup)
     const uint32_t base = blockIdx.x * kMacBlock;
     const uint32_t cols = a.cols, K = a.K;
     const uint32_t gfirst = base / cols;
     const uint32_t glast = min(base + kMacBlock - 1, a.total - 1) / cols;
     const uint32_t ng = glast - gfirst + 1;
-    // C tables of the workgroup's groups (zero for a group that recovers nothing)
+    // C tables of the workgroup's groups
     for (uint32_t e = threadIdx.x; e < ng * RT * RT; e += kMacBlock) {
-        const uint32_t gs = e / (RT * RT), ur = e - gs * (RT * RT), u = ur / RT, r = ur - u * RT;
-        const uint8_t *rec = a.rec + (uint64_t)(gfirst + gs) * a.rec_stride;
-        uint32_t t[5];
-        gf_perm_tables(rec[0] == 0 ? rec[8 + 8 * u + r] : 0u, t);
-        uint32_t *tp = s_ct + (gs * RT + u) * TD + 5 * r;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) tp[i] = t[i];
+        const uint32_t gs = e / (RT * RT);
+        syn_expand_one<RT>(a.rec + (uint64_t)(gfirst + gs) * a.rec_stride, e - gs * (RT * RT), s_ct + gs * RT * TD);
     }
-
     const uint32_t item = base + threadIdx.x;
     const bool in = item < a.total;
     const uint32_t g = in ? item / cols : gfirst;
     const uint32_t col = in ? item - g * cols : 0;
-    const uint32_t nd = (VEC >= 4 && (col + 1) * VB > a.B) ? (a.B - col * VB + 3) / 4 : (uint32_t)W;
+    const uint32_t off = gran_off<VEC>(col, a.B);
+    const uint32_t gs = g - gfirst;
     uint32_t m = 0, used = 0;
+    uint64_t p0 = 0;
+    const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
     if (in) {
-        const uint32_t h = *reinterpret_cast<const uint32_t *>(a.rec + (uint64_t)g * a.rec_stride);
-        if ((h & 0xFFu) == 0) {
-            m = (h >> 8) & 0xFFu;
-            used = (h >> 16) & 0xFFu;
+        const uint4 h = *reinterpret_cast<const uint4 *>(rec);  // header + present data bits 0..63
+        if ((h.x & 0xFFu) == 0) {
+            m = (h.x >> 8) & 0xFFu;
+            used = (h.x >> 16) & 0xFFu;
         }
+        p0 = (uint64_t)h.z | ((uint64_t)h.w << 32);
     }
     const bool active = m > 0;
     uint32_t acc[RT][W];
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-        for (int w = 0; w < W; ++w) acc[r][w] = 0;
-
     if (active) {
-        const uint64_t *pr = a.present + (uint64_t)g * 4;
-        const uint64_t p0 = pr[0];
-        const uint64_t p1 = K > 64 ? pr[1] : 0ull, p2 = K > 128 ? pr[2] : 0ull, p3 = K > 192 ? pr[3] : 0ull;
-        auto has = [&](uint32_t j) -> bool {
-            const uint64_t wq = j < 64 ? p0 : (j < 128 ? p1 : (j < 192 ? p2 : p3));
-            return (wq >> (j & 63u)) & 1ull;
-        };
-        const uint8_t *dbase = a.data + ((uint64_t)g * K) * a.pitch + (uint64_t)col * VB;
-        auto ld = [&](uint32_t j) -> Gran<VEC> {
-            Gran<VEC> v;
-#pragma unroll
-            for (int w = 0; w < W; ++w) v.d[w] = 0;
-            if (has(j)) v = load_any<VEC>(dbase + (uint64_t)j * a.pitch, col, a.B, nd);
-            return v;
-        };
-        Gran<VEC> x[PD];
-#pragma unroll
-        for (int u = 0; u < PD; ++u)
-            if ((uint32_t)u < K) x[u] = ld(u);
-        typedef const __attribute__((address_space(4))) uint32_t cu32;  // uniform: scalar loads into SGPRs
-        for (uint32_t jb = 0; jb < K; jb += PD) {
-#pragma unroll
-            for (int u = 0; u < PD; ++u) {
-                const uint32_t j = jb + u;
-                if (j < K) {
-                    const Gran<VEC> cur = x[u];
-                    if (j + PD < K) x[u] = ld(j + PD);
-                    const cu32 *tg = (const cu32 *)(a.etab + (size_t)j * a.etab_rows * 5);
-                    uint32_t t[5 * RT];
-#pragma unroll
-                    for (int i = 0; i < 5 * RT; ++i) t[i] = tg[i];
-#pragma unroll
-                    for (int w = 0; w < W; ++w) {
-                        const uint32_t xv = cur.d[w];
-                        const uint32_t s0 = xv & 0x07070707u;
-                        const uint32_t s1 = (xv >> 3) & 0x07070707u;
-                        const uint32_t s2 = (xv >> 6) & 0x03030303u;
-#pragma unroll
-                        for (int r = 0; r < RT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
-                    }
-                }
-            }
-        }
-        // the parity shares of the rows in use
-#pragma unroll
-        for (int r = 0; r < RT; ++r) {
-            if ((used >> r) & 1u) {
-                const Gran<VEC> y =
-                    load_any<VEC>(a.parity + ((uint64_t)g * a.R + r) * a.pitch + (uint64_t)col * VB, col, a.B, nd);
-#pragma unroll
-                for (int w = 0; w < W; ++w) acc[r][w] ^= y.d[w];
-            }
-        }
+        // resources over this workgroup's groups (wave-uniform: blockIdx and kernel arguments only)
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.data + (uint64_t)gfirst * K * a.pitch), (short)0, (int)(ng * K * a.pitch), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.parity + (uint64_t)gfirst * a.R * a.pitch), (short)0, (int)(ng * a.R * a.pitch), 0x00020000);
+        syn_loop<VEC, RT, PD>(a, acc, rd, rp, gs * K * (uint32_t)a.pitch + off, gs * a.R * (uint32_t)a.pitch + off, used,
+                              p0, rec);
     }
     __syncthreads();  // C tables
-    if (active) {
-        const uint32_t *ct = s_ct + (g - gfirst) * RT * TD;
-        const uint64_t obase = ((uint64_t)g * a.R) * a.pitch + (uint64_t)col * VB;
+    if (active) syn_final<VEC, RT>(a, acc, s_ct + gs * RT * TD, m, g, off, col);
+}
+
+// ---- ordered list of the groups with data to recover (out_idx[g * R] != 0xFF), for syn_kernel's listed
+// shape: per-chunk counts, one exclusive scan, a scatter that keeps group order.  kActChunk groups per
+// 256-thread workgroup, 4 per thread.
+constexpr uint32_t kActChunk = 1024;
+
+__device__ __forceinline__ uint32_t act_flags(uint64_t G, uint32_t R, const uint8_t *out_idx, uint64_t g0)
+{
+    uint32_t f = 0;
 #pragma unroll
-        for (int u = 0; u < RT; ++u) {
-            if ((uint32_t)u < m) {
-                uint32_t t[TD];
-                const uint4 *tv = reinterpret_cast<const uint4 *>(ct + u * TD);
-#pragma unroll
-                for (int i = 0; i < TD / 4; ++i) {
-                    const uint4 q = tv[i];
-                    t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
-                }
-                uint32_t o[W];
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    uint32_t v = 0;
-#pragma unroll
-                    for (int r = 0; r < RT; ++r) {
-                        const uint32_t yv = acc[r][w];
-                        v = perm_mac(v, t + 5 * r, yv & 0x07070707u, (yv >> 3) & 0x07070707u, (yv >> 6) & 0x03030303u);
-                    }
-                    o[w] = v;
-                }
-                store_any<VEC>(a.out + obase + (uint64_t)u * a.pitch, o, col, a.B, nd);
-            }
-        }
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t g = g0 + k;
+        if (g < G && out_idx[g * R] != 0xFF) f |= 1u << k;
     }
+    return f;
+}
+
+// exclusive prefix of v over the 256 threads of the workgroup (and the total)
+__device__ __forceinline__ uint32_t block_exclusive(uint32_t v, uint32_t *s_w, uint32_t &total)
+{
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t x = v;  // inclusive scan within the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t t = s_w[k];
+        if ((uint32_t)k < wv) before += t;
+        total += t;
+    }
+    return before + x - v;
+}
+
+__global__ void __launch_bounds__(kBlock) active_count_kernel(uint64_t G, uint32_t R, const uint8_t *out_idx,
+                                                              uint32_t *chunk_cnt)
+{
+    __shared__ uint32_t s_w[4];
+    const uint64_t g0 = (uint64_t)blockIdx.x * kActChunk + threadIdx.x * 4u;
+    uint32_t total = 0;
+    (void)block_exclusive(__popc(act_flags(G, R, out_idx, g0)), s_w, total);
+    if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = total;
+}
+
+// one workgroup: chunk counts -> exclusive chunk offsets (in place), total -> *count
+__global__ void __launch_bounds__(kBlock) active_scan_kernel(uint32_t nchunks, uint32_t *chunk_cnt, uint32_t *count)
+{
+    __shared__ uint32_t s_w[4];
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += kBlock) {
+        const uint32_t c = c0 + threadIdx.x;
+        const uint32_t v = c < nchunks ? chunk_cnt[c] : 0u;
+        uint32_t total = 0;
+        const uint32_t ex = block_exclusive(v, s_w, total);
+        if (c < nchunks) chunk_cnt[c] = carry + ex;
+        carry += total;
+        __syncthreads();  // s_w is reused by the next round
+    }
+    if (threadIdx.x == 0) *count = carry;
+}
+
+__global__ void __launch_bounds__(kBlock) active_scatter_kernel(uint64_t G, uint32_t R, const uint8_t *out_idx,
+                                                                const uint32_t *chunk_off, uint32_t *list)
+{
+    __shared__ uint32_t s_w[4];
+    const uint64_t g0 = (uint64_t)blockIdx.x * kActChunk + threadIdx.x * 4u;
+    const uint32_t f = act_flags(G, R, out_idx, g0);
+    uint32_t total = 0;
+    uint32_t at = chunk_off[blockIdx.x] + block_exclusive(__popc(f), s_w, total);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if ((f >> k) & 1u) list[at++] = (uint32_t)(g0 + k);
 }
 
 // ---------------------------------------------------------------------------------------------------
 // host-side launch helpers
 // ---------------------------------------------------------------------------------------------------
+// Batches of at most kLatencyGroups groups (the single-group drop-in calls, whose shares sit in pinned host
+// memory) run the MAC with 4-byte granules and 16 shards in flight per lane: ~8x more lanes and loads in
+// flight than the streaming shape, so the PCIe round trips of a 29 KB group overlap instead of queueing.
+constexpr int kLatencyVec = -4;
+constexpr size_t kLatencyGroups = 4;
+
 // granule of the MAC kernels: 32 B whenever the pitch and every base pointer are dword aligned (the tail
 // granule of a row is loaded / stored dword by dword), bytewise otherwise
-static int pick_vec_mac(size_t pitch, std::initializer_list<const void *> ptrs)
+static int pick_vec_mac(size_t pitch, size_t B, std::initializer_list<const void *> ptrs)
 {
     bool ok = (pitch % 4) == 0;
     for (const void *p : ptrs) ok = ok && (reinterpret_cast<uintptr_t>(p) % 4) == 0;
-    return ok ? 32 : 1;
+    if (!ok) return 1;
+    return B >= 32 ? 32 : kLatencyVec;  // (B < 32: the dword shape, one granule per dword)
 }
 
 // output rows per tile: MT = R up to 4, else 8-row tiles.  Measured at 200:55: taller tiles on
@@ -1121,11 +1303,6 @@ static int pick_vec_mac(size_t pitch, std::initializer_list<const void *> ptrs)
 // granules amortise each table read over the most bytes).
 static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
 
-// Batches of at most kLatencyGroups groups (the single-group drop-in calls, whose shares sit in pinned host
-// memory) run the MAC with 4-byte granules and 16 shards in flight per lane: ~8x more lanes and loads in
-// flight than the streaming shape, so the PCIe round trips of a 29 KB group overlap instead of queueing.
-constexpr int kLatencyVec = -4;
-constexpr size_t kLatencyGroups = 4;
 
 template <int VEC, int MT, bool DEC, int PDX = 0>
 static int run_mac(MacArgs a, hipStream_t s)
@@ -1141,12 +1318,14 @@ static int run_mac(MacArgs a, hipStream_t s)
 template <bool DEC>
 static int dispatch_mac(int vec, int mt, MacArgs a, hipStream_t s)
 {
+#if KFEC_SYN_MAX_R > 0
     if constexpr (DEC) {  // coefficient-form decode: R > 8, 8-row tiles only
         (void)mt;
         if (vec == kLatencyVec) return run_mac<4, 8, true, 16>(a, s);
         if (vec == 32) return run_mac<32, 8, true>(a, s);
         return run_mac<1, 8, true>(a, s);
     }
+#endif
     if (vec == kLatencyVec) {  // the latency shape: dword granules, 16 shards in flight per lane
         switch (mt) {
         case 1: return run_mac<4, 1, DEC, 16>(a, s);
@@ -1199,26 +1378,29 @@ static size_t syn_td(int rt)
 }
 
 template <int VEC, int RT, int PDX = 0>
-static int run_syn(SynArgs a, size_t lds, hipStream_t s)
+static int run_syn(SynArgs a, size_t lds, int cus, hipStream_t s)
 {
     const uint32_t nb = (a.total + kMacBlock - 1) / kMacBlock;
     hipLaunchKernelGGL((syn_kernel<VEC, RT, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), lds, s, a);
+    // the listed shape: persistent, ~8 workgroups per CU, at most one wave per (group, 64 columns) task
+    const uint64_t tasks = (uint64_t)a.G * (a.cols_pad / 64);
+    const uint32_t nl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((tasks + 3) / 4, (uint64_t)std::max(cus, 1) * 8));
+    hipLaunchKernelGGL((syn_list_kernel<VEC, RT, PDX>), dim3(nl), dim3(kMacBlock), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-static int dispatch_syn(int vec, int rt, SynArgs a, size_t lds, hipStream_t s)
+static int dispatch_syn(int vec, int rt, SynArgs a, size_t lds, int cus, hipStream_t s)
 {
 #define KFEC_RT_CASES(V, P)                               \
     switch (rt) {                                         \
-    case 1: return run_syn<V, 1, P>(a, lds, s);           \
-    case 2: return run_syn<V, 2, P>(a, lds, s);           \
-    case 3: return run_syn<V, 3, P>(a, lds, s);           \
-    case 4: return run_syn<V, 4, P>(a, lds, s);           \
-    default: return run_syn<V, 8, P>(a, lds, s);          \
+    case 1: return run_syn<V, 1, P>(a, lds, cus, s);      \
+    case 2: return run_syn<V, 2, P>(a, lds, cus, s);      \
+    case 3: return run_syn<V, 3, P>(a, lds, cus, s);      \
+    case 4: return run_syn<V, 4, P>(a, lds, cus, s);      \
+    default: return run_syn<V, 8, P>(a, lds, cus, s);     \
     }
     if (vec == kLatencyVec) KFEC_RT_CASES(4, 16)
-    if (vec == 32) KFEC_RT_CASES(32, 0)
-    KFEC_RT_CASES(1, 0)
+    KFEC_RT_CASES(32, 0)
 #undef KFEC_RT_CASES
 }
 
@@ -1245,7 +1427,7 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     (void)di;
     const int R = N - K;
     if (R == 0 || G == 0 || B == 0) return 0;
-    int vec = pick_vec_mac(pitch, {d_data, d_parity});
+    int vec = pick_vec_mac(pitch, B, {d_data, d_parity});
     const int mt = pick_mt(R);
     if (G <= kLatencyGroups && vec >= 4) vec = kLatencyVec;
     const int vb = vec >= 4 ? vec : 4;
@@ -1325,7 +1507,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     if (G == 0) return 0;
     uint8_t *rec = static_cast<uint8_t *>(d_workspace);
     const size_t rs = record_stride(K, R);
-    int vec = pick_vec_mac(pitch, {d_data, d_parity, d_out});
+    int vec = pick_vec_mac(pitch, B, {d_data, d_parity, d_out});
     if (G <= kLatencyGroups && vec >= 4) vec = kLatencyVec;
     const int vb = vec >= 4 ? vec : 4;
     const size_t cols = (B + vb - 1) / vb;
@@ -1334,29 +1516,51 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     const int rt = syn_rt(R);
     const size_t gmax_syn = std::min<size_t>(G, (kMacBlock - 1) / std::max<size_t>(cols, 1) + 2);
     const size_t lds_syn = gmax_syn * (size_t)rt * syn_td(rt) * 4;
-    const bool syn = R > 0 && R <= 8 && lds_syn <= kSynLdsMax;
+    // (syndrome form: whole-dword granules, and each workgroup's groups must fit one buffer resource)
+    const bool syn = R > 0 && R <= KFEC_SYN_MAX_R && lds_syn <= kSynLdsMax && vec != 1 &&
+                     gmax_syn * (size_t)K * pitch < (size_t(1) << 31) && gmax_syn * (size_t)R * pitch < (size_t(1) << 31) &&
+                     G * (size_t)R < (size_t(1) << 32);
     if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s, syn)) return -3;
     if (R == 0 || B == 0) return 0;
     if (syn) {
+        uint32_t *count = reinterpret_cast<uint32_t *>(rec + decode_list_offset(G, K, R));
+        uint32_t *chunk_cnt = count + 64;
+        uint32_t *list = chunk_cnt + decode_list_chunks(G);
+        const size_t cols_pad = (cols + 63) / 64 * 64;
+        const size_t lds = lds_syn;
         return for_group_ranges(G, cols, 1, [&](size_t g0, size_t gn) {
+            // the ordered list of this launch's groups with data to recover, and its length, on the device
+            const uint32_t nch = (uint32_t)((gn + kActChunk - 1) / kActChunk);
+            const uint8_t *oi = d_out_idx + g0 * R;
+            hipLaunchKernelGGL(active_count_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)gn, (uint32_t)R, oi, chunk_cnt);
+            hipLaunchKernelGGL(active_scan_kernel, dim3(1), dim3(kBlock), 0, s, nch, chunk_cnt, count);
+            hipLaunchKernelGGL(active_scatter_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)gn, (uint32_t)R, oi,
+                               (const uint32_t *)chunk_cnt, list);
+            if (hipGetLastError() != hipSuccess) return -3;
             SynArgs a{};
             a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
             a.parity = static_cast<const uint8_t *>(d_parity) + g0 * R * pitch;
             a.out = static_cast<uint8_t *>(d_out) + g0 * R * pitch;
             a.rec = rec + g0 * rs;
-            a.present = d_present + g0 * 4;
             a.etab = reinterpret_cast<const uint32_t *>(d_enc + enc_tab_offset(K, N));
+            a.list = list;
+            a.list_count = count;
             a.etab_rows = (uint32_t)enc_tab_rows(R);
             a.pitch = pitch;
             a.total = (uint32_t)(gn * cols);
             a.cols = (uint32_t)cols;
+            a.cols_pad = (uint32_t)cols_pad;
             a.G = (uint32_t)gn;
             a.K = K; a.R = R; a.B = (uint32_t)B;
             a.rec_stride = (uint32_t)rs;
-            return dispatch_syn(vec, rt, a, lds_syn, s);
+            return dispatch_syn(vec, rt, a, lds, di.cus, s);
         });
     }
+#if KFEC_SYN_MAX_R > 0
     const int mt = 8;  // coefficient form: R > 8 (or tiny shards), 8-row tiles
+#else
+    const int mt = pick_mt(R);  // A/B build: coefficient form for every R
+#endif
     const int tiles = (R + mt - 1) / mt;
     const size_t ent = entry_bytes(mt);
     return for_group_ranges(G, cols, tiles, [&](size_t g0, size_t gn) {
@@ -1451,7 +1655,7 @@ int launch_erasure_masks(uint64_t seed, int N, size_t g0, size_t G, size_t pool,
     if (G == 0) return 0;
     hipLaunchKernelGGL(erasure_kernel, dim3((uint32_t)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, seed,
                        (uint32_t)N, (uint64_t)g0, (uint64_t)G, (uint32_t)pool,
-                       (uint32_t)(random_count == 2 ? count_max : std::max<size_t>(count_max, 1)),
+                       (uint32_t)(random_count == 1 ? std::max<size_t>(count_max, 1) : count_max),
                        random_count, d_present);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

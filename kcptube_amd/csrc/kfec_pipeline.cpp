@@ -171,7 +171,45 @@ struct kfec_tx {
     size_t cached = 0;
 };
 
+namespace {
+
+// The queue's coder must still have the K / N the queue was sized for: a reset_martix on a live coder
+// (client.cpp:1755, relay.cpp:947) with queues still attached would make the flush kernels overrun them.
+bool kn_changed(const kfec_ctx *ctx, size_t K, size_t N) { return kfec_get_K(ctx) != K || kfec_get_N(ctx) != N; }
+
+// Move the live bytes (datagrams of every sender's partial group) to the front of the arena, in arena order
+// (every destination lies at or below its source, so memmove in that order never overwrites unread bytes).
+// Called with no group queued: after a flush, and before growing a full arena, so the bytes of destroyed
+// senders are reclaimed instead of doubling memory.  Any early upload is drained and restarted.
+int tx_compact(kfec_txq *q)
+{
+    if (q->up.cs && hipStreamSynchronize(q->up.cs) != hipSuccess) return KFEC_EHIP;
+    q->up.issued = 0;
+    struct Part {
+        uint64_t off;
+        size_t len;
+        uint64_t *rec;  // where the offset is recorded
+        bool operator<(const Part &o) const { return off < o.off; }
+    };
+    std::vector<Part> part;
+    for (kfec_tx *tx : q->txs)
+        for (size_t i = 0; i < tx->cached; ++i) part.push_back({tx->cache_off[i], tx->cache_len[i], &tx->cache_off[i]});
+    std::sort(part.begin(), part.end());
+    size_t at = 0;
+    for (const Part &p : part) {
+        if (p.len && at != p.off) std::memmove(q->h_dg.as<uint8_t>() + at, q->h_dg.as<uint8_t>() + p.off, p.len);
+        *p.rec = at;
+        at += round4(p.len);
+    }
+    q->used = at;
+    return KFEC_OK;
+}
+
+}  // namespace
+
 extern "C" {
+
+size_t kfec_txq_capacity(const kfec_txq *q) { return q ? q->cap : 0; }
 
 int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram, kfec_txq **out)
 {
@@ -249,12 +287,13 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
 {
     if (!tx || !pkt || !pkt_len || (len && !datagram)) return KFEC_EINVAL;
     kfec_txq *q = tx->q;
-    if (len > q->mtu) return KFEC_EINVAL;
+    if (len > q->mtu || kn_changed(q->ctx, q->K, q->N)) return KFEC_EINVAL;
     const bool completes = tx->conv != 0 && tx->cached + 1 == q->K;
     if (completes && q->n == q->G) return KFEC_ENOMEM;
     if (tx->conv != 0 && q->used + round4(len) > q->cap) {
         if (q->n) return KFEC_ENOMEM;  // a flush frees the queued groups' bytes
-        const int rc = grow_arena(q->h_dg, q->d_dg, q->up, q->used, round4(len), q->cap);
+        int rc = tx_compact(q);        // first reclaim what no partial group holds any more
+        if (!rc && q->used + round4(len) > q->cap) rc = grow_arena(q->h_dg, q->d_dg, q->up, q->used, round4(len), q->cap);
         if (rc) return rc;
     }
     // create_fec_data_packet (connections.cpp:395-411), sub_sn = fec_snd_sub_sn++ (client.cpp:805-806)
@@ -294,6 +333,7 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
     if (!q) return KFEC_EINVAL;
     const size_t n = q->n;
     if (n == 0) return KFEC_OK;
+    if (kn_changed(q->ctx, q->K, q->N)) return KFEC_EINVAL;  // the coder was reset: recreate the queue
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t K = q->K, R = q->R;
     const size_t B = q->mtu + KFEC_FEC_CONTAINER_HEADER, pitch = round4(B);
@@ -336,26 +376,7 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
             if (len) cb(user, q->tags[g], sn[g], (uint8_t)(K + r), pk + (g * R + r) * pkt_pitch, len);
         }
     q->n = 0;
-    // keep the partial groups: move their datagrams to the front of the arena, in arena order (every
-    // destination lies at or below its source, so memmove in that order never overwrites unread bytes)
-    struct Part {
-        uint64_t off;
-        size_t len;
-        uint64_t *rec;  // where the offset is recorded
-        bool operator<(const Part &o) const { return off < o.off; }
-    };
-    std::vector<Part> part;
-    for (kfec_tx *tx : q->txs)
-        for (size_t i = 0; i < tx->cached; ++i) part.push_back({tx->cache_off[i], tx->cache_len[i], &tx->cache_off[i]});
-    std::sort(part.begin(), part.end());
-    size_t at = 0;
-    for (const Part &p : part) {
-        if (p.len && at != p.off) std::memmove(q->h_dg.as<uint8_t>() + at, q->h_dg.as<uint8_t>() + p.off, p.len);
-        *p.rec = at;
-        at += round4(p.len);
-    }
-    q->used = at;
-    return KFEC_OK;
+    return tx_compact(q);  // keep the partial groups, at the front of the arena
 }
 
 }  // extern "C"
@@ -417,6 +438,43 @@ struct kfec_rx {
 };
 
 namespace {
+
+bool kn_changed_rx(const kfec_rxq *q) { return kfec_get_K(q->ctx) != q->K || kfec_get_N(q->ctx) != q->N; }
+
+// The receive side of tx_compact: the shards of every cached group that still waits for K shares move to
+// the front of the arena; restored groups (kept by the reference only as membership) and evicted ones free
+// their bytes.  Called with nothing queued: after a flush, and before growing a full arena -- stale-only
+// traffic (groups that never reach K shares) must not grow memory without bound.
+int rx_compact(kfec_rxq *q)
+{
+    if (q->up.cs && hipStreamSynchronize(q->up.cs) != hipSuccess) return KFEC_EHIP;
+    q->up.issued = 0;
+    struct Part {
+        uint64_t *off;
+        size_t len;
+        bool operator<(const Part &o) const { return *off < *o.off; }
+    };
+    std::vector<Part> part;
+    for (kfec_rx *rx : q->rxs)
+        for (auto &kv : rx->cache) {
+            RxGroup *x = kv.second;
+            if (x->restored) continue;
+            for (unsigned w = 0; w < 4; ++w)
+                for (uint64_t m = x->has[w]; m; m &= m - 1) {
+                    const unsigned sub = w * 64 + (unsigned)__builtin_ctzll(m);
+                    part.push_back({&x->off[sub], x->len[sub]});
+                }
+        }
+    std::sort(part.begin(), part.end());
+    size_t at = 0;
+    for (const Part &p : part) {
+        if (p.len && at != *p.off) std::memmove(q->h_arena.as<uint8_t>() + at, q->h_arena.as<uint8_t>() + *p.off, p.len);
+        *p.off = at;
+        at += round4(p.len);
+    }
+    q->used = at;
+    return KFEC_OK;
+}
 
 // a decodable group takes queue slot q->n: its shards are already in the arena
 void rx_enqueue(kfec_rxq *q, uint64_t tag, uint32_t sn, const RxGroup &grp)
@@ -482,6 +540,8 @@ void kfec_rxq_destroy(kfec_rxq *q) { delete q; }
 
 size_t kfec_rxq_pending(const kfec_rxq *q) { return q ? q->n : 0; }
 
+size_t kfec_rxq_capacity(const kfec_rxq *q) { return q ? q->cap : 0; }
+
 int kfec_rx_create(kfec_rxq *q, uint64_t tag, kfec_rx **out)
 {
     if (!out) return KFEC_EINVAL;
@@ -517,6 +577,7 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
     if (datagram) *datagram = nullptr;
     if (datagram_len) *datagram_len = 0;
     kfec_rxq *q = rx->q;
+    if (kn_changed_rx(q)) return KFEC_EINVAL;  // the coder was reset: recreate the queue
     // unpack_fec / unpack_fec_redundant (connections.cpp:488-511), dispatched on sub_sn as fec_unpack
     if (len < KFEC_PKT_DATA_HEADER) return KFEC_EINVAL;
     const uint8_t sub = pkt[8];
@@ -537,7 +598,9 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
     if (completes && q->n >= q->G) return KFEC_ENOMEM;
     if (store && q->used + round4(plen) > q->cap) {
         if (q->n) return KFEC_ENOMEM;  // a flush frees the queued groups' bytes
-        const int rc = grow_arena(q->h_arena, q->d_arena, q->up, q->used, round4(plen), q->cap);
+        int rc = rx_compact(q);        // first reclaim restored / evicted groups' bytes and overwritten duplicates
+        if (!rc && q->used + round4(plen) > q->cap)
+            rc = grow_arena(q->h_arena, q->d_arena, q->up, q->used, round4(plen), q->cap);
         if (rc) return rc;
     }
     // fec_rcv_cache[sn][sub_sn] = ... (client.cpp:869,887): a duplicate overwrites
@@ -591,6 +654,7 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
     if (!q) return KFEC_EINVAL;
     const size_t n = q->n;
     if (n == 0) return KFEC_OK;
+    if (kn_changed_rx(q)) return KFEC_EINVAL;  // the coder was reset: recreate the queue
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t N = q->N, R = q->R;
     const size_t B = q->max_shard, pitch = round4(B);
@@ -630,33 +694,7 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
             cb(user, q->tags[g], q->sns[g], idx, shard + KFEC_FEC_CONTAINER_HEADER, len);
         }
     q->n = 0;
-    // keep the shards of the groups still waiting for K shares: move them to the front of the arena, in arena
-    // order (every destination lies at or below its source, so memmove in that order overwrites nothing unread)
-    struct Part {
-        uint64_t *off;
-        size_t len;
-        bool operator<(const Part &o) const { return *off < *o.off; }
-    };
-    std::vector<Part> part;
-    for (kfec_rx *rx : q->rxs)
-        for (auto &kv : rx->cache) {
-            RxGroup *x = kv.second;
-            if (x->restored) continue;
-            for (unsigned w = 0; w < 4; ++w)
-                for (uint64_t m = x->has[w]; m; m &= m - 1) {
-                    const unsigned sub = w * 64 + (unsigned)__builtin_ctzll(m);
-                    part.push_back({&x->off[sub], x->len[sub]});
-                }
-        }
-    std::sort(part.begin(), part.end());
-    size_t at = 0;
-    for (const Part &p : part) {
-        if (p.len && at != *p.off) std::memmove(q->h_arena.as<uint8_t>() + at, q->h_arena.as<uint8_t>() + *p.off, p.len);
-        *p.off = at;
-        at += round4(p.len);
-    }
-    q->used = at;
-    return KFEC_OK;
+    return rx_compact(q);  // keep the shards of the groups still waiting for K shares
 }
 
 }  // extern "C"

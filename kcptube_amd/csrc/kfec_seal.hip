@@ -194,6 +194,7 @@ __device__ __forceinline__ uint32_t checksum16(uint32_t c)
 struct SealArgs {
     const uint32_t *src;
     uint64_t src_dw;
+    uint64_t src_bytes;
     const uint64_t *off;
     const uint32_t *len;
     uint8_t *dst;
@@ -389,7 +390,9 @@ __global__ void __launch_bounds__(kSealBlock) open_kernel(SealArgs a)
 // Checksum mode in place (kfec_seal_batch / kfec_open_batch with d_dst == NULL): the packets stay where they
 // are; seal appends the two checksum bytes after each packet, open verifies the trailer.  The CRC reads the
 // packet once and nothing else moves (separate kernels: a per-packet in-place test inside seal_kernel cost
-// its out-of-place path 24%).
+// its out-of-place path 24%).  Seal writes a trailer only where it fits the packet's slot (a.dst_pitch =
+// the slot size from d_off, e.g. pkt_pitch) and the buffer: a packet filling its slot would otherwise get
+// its trailer written over the next packet while another row is still reading that packet for its CRC.
 __global__ void __launch_bounds__(kSealBlock) seal_in_place_kernel(SealArgs a, bool open)
 {
     __shared__ uint32_t s_tab[kCrcMaps][4][256];
@@ -405,6 +408,10 @@ __global__ void __launch_bounds__(kSealBlock) seal_in_place_kernel(SealArgs a, b
                 a.out_len[p] = 0;
                 if (open) a.ok[p] = 0;
             }
+            continue;
+        }
+        if (!open && ((uint64_t)L + KFEC_SEAL_TRAILER > a.dst_pitch || off + L + KFEC_SEAL_TRAILER > a.src_bytes)) {
+            if (lane == 0) a.out_len[p] = 0;  // no room for the trailer: "does not fit", nothing written
             continue;
         }
         const uint32_t n = open ? L - KFEC_SEAL_TRAILER : L;  // bytes under the checksum
@@ -449,6 +456,7 @@ int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes
     SealArgs a{};
     a.src = static_cast<const uint32_t *>(src);
     a.src_dw = (src_bytes + 3) / 4;
+    a.src_bytes = src_bytes;
     a.off = off;
     a.len = len;
     a.dst = static_cast<uint8_t *>(dst);

@@ -95,6 +95,7 @@ def load_library():
         "kfec_txq_create": (C.c_int, [_vp, sz, sz, C.POINTER(_vp)]),
         "kfec_txq_destroy": (None, [_vp]),
         "kfec_txq_pending": (sz, [_vp]),
+        "kfec_txq_capacity": (sz, [_vp]),
         "kfec_tx_create": (C.c_int, [_vp, C.c_uint32, C.c_uint64, C.POINTER(_vp)]),
         "kfec_tx_destroy": (None, [_vp]),
         "kfec_tx_send": (C.c_int, [_vp, _u8p, sz, C.c_uint32, _u8p, _szp]),
@@ -102,6 +103,7 @@ def load_library():
         "kfec_rxq_create": (C.c_int, [_vp, sz, sz, C.POINTER(_vp)]),
         "kfec_rxq_destroy": (None, [_vp]),
         "kfec_rxq_pending": (sz, [_vp]),
+        "kfec_rxq_capacity": (sz, [_vp]),
         "kfec_rx_create": (C.c_int, [_vp, C.c_uint64, C.POINTER(_vp)]),
         "kfec_rx_destroy": (None, [_vp]),
         "kfec_rx_cached": (sz, [_vp]),
@@ -111,6 +113,8 @@ def load_library():
         "kfec_open_batch": (C.c_int, [C.c_int, sz, _vp, sz, _vp, _vp, _vp, sz, _vp, _vp, _vp]),
     }
     for name, (res, args) in proto.items():
+        if os.environ.get("KFEC_LIB") and not hasattr(lib, name):
+            continue  # an older build timed by tools/ab.py: only the coder entry points are needed
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

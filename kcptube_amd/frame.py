@@ -143,13 +143,14 @@ class FecFrame:
                "kfec_group_scatter")
 
 
-def seal(mode: int, src, off, length, dst, out_len, stream=None) -> None:
+def seal(mode: int, src, off, length, dst, out_len, stream=None, slot: int = 0) -> None:
     """encrypt_data (none / plain_xor) for P packets [off[p], off[p] + length[p]) of src (length int32 [P]):
     dst [P][dst_pitch] receives data || checksum16 (xor_forward'ed for plain_xor), out_len int32 [P].
-    dst None: checksum mode in place (the 2 checksum bytes go right after each packet in src)."""
+    dst None: checksum mode in place (the 2 checksum bytes go right after each packet in src, when they fit
+    its `slot` bytes from off[p])."""
     P = off.numel()
     _check(load_library().kfec_seal_batch(mode, P, _dptr(src), src.numel(), _dptr(off), _dptr(length), _dptr(dst),
-                                          dst.shape[-1] if dst is not None else 0, _dptr(out_len),
+                                          dst.shape[-1] if dst is not None else slot, _dptr(out_len),
                                           _stream_handle(stream)), "kfec_seal_batch")
 
 

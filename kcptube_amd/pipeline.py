@@ -35,6 +35,9 @@ class TxQueue:
     def pending(self) -> int:
         return int(self._lib.kfec_txq_pending(self._q))
 
+    def capacity(self) -> int:
+        return int(self._lib.kfec_txq_capacity(self._q))
+
     def flush(self, timestamp: int = 0) -> list[tuple[int, int, int, bytes]]:
         """Encode every queued group; returns [(tag, sn, sub_sn, redundant packet bytes)] in queue order."""
         out = []
@@ -94,6 +97,9 @@ class RxQueue:
 
     def pending(self) -> int:
         return int(self._lib.kfec_rxq_pending(self._q))
+
+    def capacity(self) -> int:
+        return int(self._lib.kfec_rxq_capacity(self._q))
 
     def flush(self) -> list[tuple[int, int, int, bytes]]:
         """Decode every queued group; returns [(tag, sn, data index, recovered datagram)] in queue order."""

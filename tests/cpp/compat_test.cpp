@@ -75,6 +75,18 @@ int main()
     bad[40] = red[0].get();
     CHECK(dflt.decode(bad, B).empty());
 
+    // share_size == 0: the reference still maps every missing data row to an (empty) block (fecpp.cpp:572-583)
+    shares[3] = group.data() + 3 * B;  // back to 17 data + 3 parity, data 0 / 7 / 19 missing
+    auto empty_blocks = dflt.decode(shares, 0);
+    CHECK(empty_blocks.size() == 3);
+    for (size_t i : {0u, 7u, 19u}) CHECK(empty_blocks.count(i) == 1 && empty_blocks[i].empty());
+    CHECK(dflt.decode(all, 0).empty());
+
+    // a failed reset (K > N) leaves the coder as it was
+    try { dflt.reset_martix(9, 8); CHECK(false); } catch (const std::invalid_argument &) {}
+    CHECK(dflt.get_K() == 20 && dflt.get_N() == 23);
+    CHECK(dflt.encode(group.data(), group.size(), B).size() == 3);
+
     // copies keep working (fec_control_data is held by value)
     fecpp::fec_code copy = dflt;
     auto red2 = copy.encode(group.data(), group.size(), B);

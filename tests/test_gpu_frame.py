@@ -642,13 +642,13 @@ def test_seal_open_in_place(dev, mode):
     flat = buf.view(-1)
     if mode == 1:
         with pytest.raises(KfecError):
-            seal(mode, flat, off, d_len, None, torch.empty(P, dtype=torch.int32, device=dev))
+            seal(mode, flat, off, d_len, None, torch.empty(P, dtype=torch.int32, device=dev), slot=pitch)
         return
     ref = torch.full((P, pitch), SENT, dtype=torch.uint8, device=dev)
     rl = torch.full((P,), -1, dtype=torch.int32, device=dev)
     seal(mode, flat, off, d_len, ref, rl)
     il = torch.full((P,), -1, dtype=torch.int32, device=dev)
-    seal(mode, flat, off, d_len, None, il)  # in place
+    seal(mode, flat, off, d_len, None, il, slot=pitch)  # in place
     torch.cuda.synchronize()
     assert torch.equal(rl, il)
     r_np, b_np, n_np = ref.cpu().numpy(), buf.cpu().numpy(), rl.cpu().numpy()
@@ -671,3 +671,28 @@ def test_seal_open_in_place(dev, mode):
     assert torch.equal(ol, ol2) and torch.equal(ok, ok2)
     assert int((ok.cpu().numpy() == 0).sum()) >= P // 4 - 2
     assert np.array_equal(buf2.cpu().numpy(), b_np)  # opening in place writes nothing into the packets
+
+
+def test_seal_in_place_respects_slots_and_buffer_end(dev):
+    """In place, a packet whose trailer would not fit its slot (a full-pitch packet from kfec_pack_batch) or
+    would pass the end of the buffer is refused (out_len 0) and nothing is written -- its neighbour's bytes
+    and the bytes past the buffer stay as they were; slot 0 is rejected."""
+    from kcptube_amd.fec import KfecError
+    from kcptube_amd.frame import seal
+    pitch, P = 64, 6
+    lens = [62, 63, 64, 10, 61, 62]  # 62 + 2 == pitch fits; 63 / 64 fill the slot; the last row ends the buffer
+    rows = np.frombuffer(random.Random(9).randbytes(P * pitch + 16), np.uint8).copy()
+    buf = torch.tensor(rows, device=dev)
+    flat = buf[: P * pitch - 1]  # the buffer ends one byte short of the last slot: its trailer cannot fit
+    off = torch.arange(P, dtype=torch.int64, device=dev) * pitch
+    d_len = torch.tensor(lens, dtype=torch.int32, device=dev)
+    ol = torch.full((P,), -1, dtype=torch.int32, device=dev)
+    seal(0, flat, off, d_len, None, ol, slot=pitch)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    assert ol.cpu().tolist() == [64, 0, 0, 12, 63, 0]
+    changed = np.nonzero(got != rows)[0].tolist()
+    allowed = set(range(62, 64)) | set(range(3 * pitch + 10, 3 * pitch + 12)) | set(range(4 * pitch + 61, 4 * pitch + 63))
+    assert set(changed) <= allowed  # only trailers of the packets that fit
+    with pytest.raises(KfecError):
+        seal(0, flat, off, d_len, None, ol, slot=0)

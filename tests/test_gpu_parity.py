@@ -268,6 +268,42 @@ def test_batch_vs_oracle(dev, oracle, K, N, B, pitch, G, erase, note):
         assert (_np(out)[:, :, hi:] == 0).all(), note
 
 
+@pytest.mark.parametrize("K,N,B,G", [(20, 23, 1440, 700), (10, 13, 1400, 500), (5, 11, 3000, 90), (3, 5, 40, 3000)])
+def test_sparse_losses_take_the_listed_shape(dev, oracle, K, N, B, G):
+    """Few groups lost data (a live link): the decode runs over the device-built list of those groups only
+    (syn_list_kernel); every other group must come back 'nothing recovered' and untouched output slots."""
+    from kcptube_amd import FecCode
+    rng = np.random.default_rng(G + K)
+    R = N - K
+    c = FecCode(K, N)
+    data_np = rng.integers(0, 256, (G, K, B), dtype=np.uint8)
+    data = torch.from_numpy(data_np).to(dev)
+    par = torch.empty((G, R, B), dtype=torch.uint8, device=dev)
+    c.encode_batch(data, par)
+    torch.cuda.synchronize()
+    exp_par = _np(par)
+    masks_np = np.zeros((G, 4), np.uint64)
+    for g in range(G):
+        lost = set(rng.choice(N, int(rng.integers(1, R + 1)), replace=False).tolist()) if g % 11 == 3 else set()
+        for s_ in range(N):
+            if s_ not in lost:
+                masks_np[g, s_ >> 6] |= np.uint64(1) << np.uint64(s_ & 63)
+    masks = torch.from_numpy(masks_np.view(np.int64)).to(dev)
+    exp_out, exp_idx, exp_st = oracle.decode_batch(K, N, data_np, exp_par, masks_np, B)
+    _scribble_absent(data, par, masks, K)
+    out = torch.full((G, R, B), 0x3C, dtype=torch.uint8, device=dev)
+    idx = torch.empty((G, R), dtype=torch.uint8, device=dev)
+    st = torch.empty((G,), dtype=torch.uint8, device=dev)
+    c.decode_batch(data, par, masks, out, idx, st, c.decode_workspace(G))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_np(st), exp_st)
+    np.testing.assert_array_equal(_np(idx), exp_idx)
+    got = _np(out)
+    used = exp_idx != 0xFF
+    np.testing.assert_array_equal(got[used], exp_out[used])
+    assert (got[~used] == 0x3C).all()  # slots of groups / rows with nothing recovered are never written
+
+
 def test_single_group_api_vs_oracle(dev, oracle):
     """fec_code-style host API (kfec_encode / kfec_decode) on random shapes, including inconsistent
     (corrupted) shares, against the oracle."""
@@ -290,6 +326,20 @@ def test_single_group_api_vs_oracle(dev, oracle):
             k = keep[int(rng.integers(len(keep)))]
             sub[k] = bytes(x ^ 0x3C for x in sub[k])
         assert c.decode(sub, B) == oracle.decode(K, N, sub, B), (K, N, B, keep)
+
+
+def test_single_group_share_size_zero(dev, oracle):
+    """decode(shares, 0) returns one empty block per missing data row, as the reference (fecpp.cpp:572-583);
+    the oracle is pinned against the compiled reference for this case (tests/test_oracle.py)."""
+    from kcptube_amd import FecCode
+    rng = np.random.default_rng(11)
+    for _ in range(40):
+        K = int(rng.integers(1, 30))
+        N = int(min(256, K + rng.integers(0, 8)))
+        c = FecCode(K, N)
+        keep = sorted(rng.choice(N + 2, int(rng.integers(max(K - 1, 0), N + 1)), replace=False).tolist())
+        sub = {s: b"" for s in keep}
+        assert c.decode(sub, 0) == oracle.decode(K, N, sub, 0), (K, N, keep)
 
 
 def test_synth_and_masks_match_oracle(dev, oracle):

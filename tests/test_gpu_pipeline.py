@@ -115,6 +115,71 @@ def test_queue_full_is_reported_without_side_effects(dev):
     assert tx.send(b"d")[8] == 1  # the refused datagram was not counted
 
 
+def _data_pkt(sn: int, sub: int, payload: bytes) -> bytes:
+    # create_fec_data_packet (connections.cpp:395-411): [LE32 ts][BE32 sn][u8 sub_sn][payload]
+    return (0).to_bytes(4, "little") + sn.to_bytes(4, "big") + bytes([sub]) + payload
+
+
+def test_receiver_stale_traffic_keeps_arena_bounded(dev):
+    """Groups that never reach K shares, and duplicates that overwrite cached shards, leave dead bytes in
+    the staging arena; with nothing queued a full arena is compacted before it may grow, so a lossy peer
+    cannot grow host + device memory without bound (the reference frees those bytes on erase)."""
+    from kcptube_amd.pipeline import FecReceiver, RxQueue
+    K, N, mtu = 20, 23, 1440
+    rq = RxQueue(_coder(K, N), max_groups=8, max_shard=mtu + 2)
+    rx = FecReceiver(rq)
+    cap0 = rq.capacity()
+    payload = bytes(range(256)) * 5 + bytes(160)  # 1440 bytes
+    for sn in range(400):  # 400 x 19 x 1444 B = 11 MB through a 266 KB arena
+        for sub in range(K - 1):
+            rx.push(_data_pkt(sn, sub, payload))
+        rx.push(_data_pkt(sn, 0, payload))  # a duplicate: overwrites, its old bytes are dead
+        assert rx.cached() <= 5
+    assert rq.pending() == 0
+    assert rq.capacity() == cap0
+
+
+def test_sender_destroyed_partial_groups_keep_arena_bounded(dev):
+    """The bytes of a sender destroyed with a partial group are reclaimed before the arena grows."""
+    from kcptube_amd.pipeline import FecSender, TxQueue
+    K, N, mtu = 20, 23, 1440
+    q = TxQueue(_coder(K, N), max_groups=2, max_datagram=mtu)
+    cap0 = q.capacity()
+    for i in range(200):
+        tx = FecSender(q, conv=9 + i)
+        for _ in range(K - 1):
+            tx.send(b"\xab" * mtu)
+        del tx  # kfec_tx_destroy with K - 1 datagrams cached
+    assert q.pending() == 0
+    assert q.capacity() == cap0
+
+
+def test_queues_refuse_work_after_the_coder_is_reset(dev):
+    """A queue is sized for its coder's K / N: after reset_martix its flush / push / send return
+    KFEC_EINVAL instead of running the kernels past its buffers."""
+    from kcptube_amd.fec import KfecError
+    from kcptube_amd.pipeline import FecReceiver, FecSender, RxQueue, TxQueue
+    c = _coder(4, 6)
+    tq, rq = TxQueue(c, 4, 64), RxQueue(c, 4, 66)
+    tx, rx = FecSender(tq, conv=3), FecReceiver(rq)
+    for _ in range(4):
+        tx.send(b"q" * 10)
+    for sub in range(4):
+        rx.push(_data_pkt(0, sub, b"r" * 10))
+    assert tq.pending() == 1 and rq.pending() == 1
+    c.reset_martix(20, 23)
+    with pytest.raises(KfecError):
+        tq.flush()
+    with pytest.raises(KfecError):
+        rq.flush()
+    with pytest.raises(KfecError):
+        tx.send(b"x")
+    with pytest.raises(KfecError):
+        rx.push(_data_pkt(1, 0, b"y"))
+    c.reset_martix(4, 6)  # back to the queue's shape: usable again
+    assert len(tq.flush()) == 2 and len(rq.flush()) == 0
+
+
 @pytest.mark.parametrize("K,N,mtu", [(20, 23, 1440), (6, 9, 300)])
 def test_receiver_matches_oracle_through_lossy_channel(dev, oracle, K, N, mtu):
     from kcptube_amd.pipeline import FecReceiver, RxQueue

@@ -206,3 +206,21 @@ def test_oracle_vs_reference_matrices_all_small(oracle):
     for K in range(1, 33):
         for N in (K, K + 1, K + 3, min(256, K + 40)):
             np.testing.assert_array_equal(oracle.enc_matrix(K, N), ref.enc_matrix(K, N))
+
+
+def test_oracle_vs_reference_share_size_zero(oracle):
+    """decode(shares, 0): the reference still maps every missing data row to an empty block
+    (fecpp.cpp:572-583); {} for too few shares or a chosen id >= N."""
+    from oracle import RefCoder
+    if not RefCoder.available():
+        pytest.skip("oracle/_ref not built")
+    ref = RefCoder()
+    rng = np.random.default_rng(5)
+    for _ in range(60):
+        K = int(rng.integers(1, 30))
+        N = int(min(256, K + rng.integers(0, 8)))
+        keep = sorted(rng.choice(N + 2, int(rng.integers(max(K - 1, 0), N + 1)), replace=False).tolist())
+        sub = {s: b"" for s in keep}
+        want = ref.decode(K, N, sub, 0)
+        assert oracle.decode(K, N, sub, 0) == want, (K, N, keep)
+        assert all(v == b"" for v in want.values())

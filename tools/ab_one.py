@@ -18,8 +18,13 @@ idx = torch.empty((G, R), dtype=torch.uint8, device=dev)
 st = torch.empty((G,), dtype=torch.uint8, device=dev)
 ws = c.decode_workspace(G)
 c.synth(data, 1)
-if os.environ.get("AB_RANDOM"):  # bench config 10:3dec: random 1..R erasures over all N shards
-    c.erasure_masks(masks, 0x5EED0001, N, R, True)
+mode = os.environ.get("AB_ERASE", "random" if os.environ.get("AB_RANDOM") else "data")
+if mode == "random":  # bench config 10:3dec: random 1..R erasures over all N shards
+    c.erasure_masks(masks, 0x5EED0001, N, R, 1)
+elif mode == "none":  # nothing lost
+    c.erasure_masks(masks, 1, K, 0, 0)
+elif mode.startswith("iid:"):  # i.i.d. loss, ppm per shard
+    c.erasure_masks(masks, 0x5EED0001, N, int(mode[4:]), 2)
 else:
     c.erasure_masks(masks, 1, K, min(R, K))
 s = torch.cuda.current_stream()
@@ -34,6 +39,6 @@ for i in range(iters + 2):
 enc.sort(); dec.sort()
 eb = G * (K + R) * B
 db = G * (K + min(R, K)) * B
-print(json.dumps({"lib": os.path.basename(os.environ.get("KFEC_LIB", "libkfec.so")), "enc_ms": enc[len(enc)//2],
+print(json.dumps({"lib": os.path.basename(os.environ.get("KFEC_LIB", "libkfec.so")), "erase": mode, "enc_ms": enc[len(enc)//2],
                   "dec_ms": dec[len(dec)//2], "enc_GBps": round(eb / enc[len(enc)//2] / 1e6, 1),
                   "dec_GBps": round(db / dec[len(dec)//2] / 1e6, 1)}), flush=True)

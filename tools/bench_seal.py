@@ -69,7 +69,7 @@ def main():
     ti, tio = [], []
     for i in range(args.steps + 2):
         e[0].record(s)
-        seal(SEAL_CHECKSUM, wflat, off, ln, None, slen)
+        seal(SEAL_CHECKSUM, wflat, off, ln, None, slen, slot=pitch)
         e[1].record(s)
         open_(SEAL_CHECKSUM, wflat, off, slen, None, plen, ok)
         e[2].record(s)

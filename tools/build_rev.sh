@@ -8,6 +8,6 @@ tmp=$(mktemp -d)
 git -C "$root" archive "$rev" kcptube_amd/csrc include | tar -x -C "$tmp"
 mkdir -p "$root/kcptube_amd/variants"
 (cd "$tmp/kcptube_amd/csrc" && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result \
-    -o "$root/kcptube_amd/variants/$name.so" kfec_kernels.hip kfec_api.cpp)
+    -o "$root/kcptube_amd/variants/$name.so" *.hip *.cpp)
 rm -rf "$tmp"
 echo "$root/kcptube_amd/variants/$name.so"
