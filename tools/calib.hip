@@ -8,7 +8,8 @@
 //                                    the MAC kernels' inner loop with the memory taken out: 32-byte granules
 //                                    (8 dwords per lane), per "shard" the three selector extractions per dword
 //                                    and `rows` perm MACs per dword with the perm tables read from LDS exactly
-//                                    as mac_kernel reads them (ds_read_b128 broadcast).  rows = 8 is the
+//                                    as mac_kernel reads them (ds_read_b128 broadcast, once per 4 granules
+//                                    here, so the LDS reads do not limit it).  rows = 8 is the
 //                                    MT = 8 row tile of the fec=200:55 kernels; the byte-MAC rate it reaches
 //                                    is the VALU ceiling those kernels are held against.
 //                                    byte-MACs per launch = blocks * 256 * iters * 32 * rows.
@@ -54,8 +55,9 @@ __global__ void __launch_bounds__(256) gfmac(uint32_t iters, uint32_t seed, uint
     for (int r = 0; r < MT; ++r)
 #pragma unroll
         for (int w = 0; w < 8; ++w) acc[r][w] = 0;
-    for (uint32_t it = 0; it < iters; ++it) {
-        const uint4 *tv = reinterpret_cast<const uint4 *>(s_tab + (it % NS) * TBL_DW);
+    // tables are read from LDS once per 4 granules, so the loop is the perm-MAC VALU work and nothing else
+    for (uint32_t it = 0; it < iters; it += 4) {
+        const uint4 *tv = reinterpret_cast<const uint4 *>(s_tab + ((it / 4) % NS) * TBL_DW);
         uint32_t t[TBL_DW];
 #pragma unroll
         for (int i = 0; i < TBL_DW / 4; ++i) {
@@ -63,11 +65,14 @@ __global__ void __launch_bounds__(256) gfmac(uint32_t iters, uint32_t seed, uint
             t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
         }
 #pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            const uint32_t xv = x[w] ^ it;  // a fresh granule each iteration (one XOR stands in for the load)
-            const uint32_t s0 = xv & 0x07070707u, s1 = (xv >> 3) & 0x07070707u, s2 = (xv >> 6) & 0x03030303u;
+        for (int k = 0; k < 4; ++k) {
 #pragma unroll
-            for (int r = 0; r < MT; ++r) acc[r][w] = kfec::perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+            for (int w = 0; w < 8; ++w) {
+                const uint32_t xv = x[w] ^ (it + k);  // a fresh granule (one XOR stands in for the load)
+                const uint32_t s0 = xv & 0x07070707u, s1 = (xv >> 3) & 0x07070707u, s2 = (xv >> 6) & 0x03030303u;
+#pragma unroll
+                for (int r = 0; r < MT; ++r) acc[r][w] = kfec::perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+            }
         }
     }
     uint32_t v = 0;

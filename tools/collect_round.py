@@ -11,12 +11,14 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 go = os.path.join(root, "gpurun_out")
 prof = os.path.join(root, "profiles")
 rnd = os.path.join(go, "round")
-for name in ("bench_203.json", "bench_103dec.json", "bench_20055.json", "wire.json", "wire_ragged.json", "seal.json",
-             "pipeline_threads.json", "latency.json", "gtest.log", "smoke.log"):
+for name in ("bench_203.json", "bench_103dec.json", "bench_20055.json", "bench_203loss1.json", "wire.json",
+             "wire_ragged.json", "seal.json", "pipeline_threads.json", "latency.json", "gtest.log", "smoke.log",
+             "box.txt"):
     src = os.path.join(rnd, name)
     if os.path.exists(src):
         shutil.copy(src, os.path.join(prof, f"{tag}_{name.replace('.log', '.txt')}"))
-for cfg, groups, ptag in (("20:3", 1 << 20, "203"), ("10:3dec", 1 << 20, "103dec"), ("200:55", 1 << 18, "20055")):
+for cfg, groups, ptag in (("20:3", 1 << 20, "203"), ("10:3dec", 1 << 20, "103dec"), ("200:55", 1 << 18, "20055"),
+                          ("20:3loss1", 1 << 20, "203loss1")):
     d = os.path.join(go, f"prof_{tag}_{ptag}")
     if os.path.isdir(d):
         subprocess.check_call([sys.executable, os.path.join(root, "tools", "pmc_summary.py"), d, f"{tag}_{ptag}",

@@ -43,7 +43,9 @@ for k, v in agg.items():
 json.dump(summary, open(os.path.join(out, f"{args.tag}_pmc.json"), "w"), indent=1)
 trf_path = os.path.join(out, "pmc_traffic.json")
 trf = json.load(open(trf_path)) if os.path.exists(trf_path) else {}
-dominant = re.compile(r"mac_kernel<\d+, \d+, %s(, \d+)?>" % ("true" if args.config.endswith("dec") else "false"))
+# the bench line's dominant kernel: the encode MAC, or for decode-only configs the syndrome-form decode MAC
+dominant = re.compile(r"syn_kernel<\d+, \d+(, \d+)?>" if args.config.endswith("dec")
+                      else r"mac_kernel<\d+, \d+, false(, \d+)?>")
 for k, d in summary.items():
     if dominant.search(k) and "hbm_bytes_per_launch" in d:
         trf[args.config] = {"groups": args.groups, "kernel": k, "hbm_bytes_per_launch": int(d["hbm_bytes_per_launch"]),
