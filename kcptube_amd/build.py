@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libkfec.so")
 COMPAT_TEST = os.path.join(PKG, "compat_test")
 
-SOURCES = ["kfec_kernels.hip", "kfec_frame.hip", "kfec_seal.hip", "kfec_api.cpp", "kfec_pipeline.cpp"]
+SOURCES = ["kfec_kernels.hip", "kfec_frame.hip", "kfec_seal.hip", "kfec_aead.hip", "kfec_api.cpp", "kfec_pipeline.cpp"]
 HEADERS = ["kfec_gf.hpp", "kfec_internal.hpp"]
 
 
@@ -37,7 +37,7 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 
 def build_lib(force: bool = False, verbose: bool = False) -> str:
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", h) for h in ("kfec.h", "kfec_frame.h", "kfec_pipeline.h")]
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", h) for h in ("kfec.h", "kfec_frame.h", "kfec_pipeline.h", "kfec_aead.h")]
     if force or _stale(LIB, deps):
         cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wno-unused-result", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
@@ -70,7 +70,7 @@ def build_tools(force: bool = False) -> list[str]:
                         ("latency_bench", [])):
         src = os.path.join(ROOT, "tools", name + ".cpp")
         exe = os.path.join(ROOT, "tools", name)
-        deps = [src, LIB] + [os.path.join(inc, h) for h in ("kfec.h", "kfec_frame.h", "kfec_pipeline.h")]
+        deps = [src, LIB] + [os.path.join(inc, h) for h in ("kfec.h", "kfec_frame.h", "kfec_pipeline.h", "kfec_aead.h")]
         if force or _stale(exe, deps):
             cmd = ["g++", "-std=c++17", "-O2", "-I", inc, src, "-o", exe, "-L", PKG, "-lkfec",
                    "-Wl,-rpath,$ORIGIN/../kcptube_amd"] + extra

@@ -39,7 +39,7 @@ _szp = C.POINTER(C.c_size_t)
 _vp = C.c_void_p
 
 
-HEADERS = [HEADER] + [os.path.join(os.path.dirname(PKG), "include", h) for h in ("kfec_frame.h", "kfec_pipeline.h")]
+HEADERS = [HEADER] + [os.path.join(os.path.dirname(PKG), "include", h) for h in ("kfec_frame.h", "kfec_pipeline.h", "kfec_aead.h")]
 
 
 def header_functions() -> list[str]:
@@ -111,6 +111,13 @@ def load_library():
         "kfec_rxq_flush": (C.c_int, [_vp, _vp, _vp, _vp]),
         "kfec_seal_batch": (C.c_int, [C.c_int, sz, _vp, sz, _vp, _vp, _vp, sz, _vp, _vp]),
         "kfec_open_batch": (C.c_int, [C.c_int, sz, _vp, sz, _vp, _vp, _vp, sz, _vp, _vp, _vp]),
+        # include/kfec_aead.h
+        "kfec_aead_create": (C.c_int, [C.c_int, C.c_char_p, sz, C.POINTER(_vp)]),
+        "kfec_aead_destroy": (None, [_vp]),
+        "kfec_aead_mode": (C.c_int, [_vp]),
+        "kfec_aead_key": (C.c_int, [_vp, _u8p]),
+        "kfec_aead_seal_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, _vp, _vp, sz, _vp, _vp]),
+        "kfec_aead_open_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, _vp, sz, _vp, _vp, _vp]),
     }
     for name, (res, args) in proto.items():
         if os.environ.get("KFEC_LIB") and not hasattr(lib, name):
