@@ -328,6 +328,10 @@ __device__ __forceinline__ void mask64(uint32_t (&o)[16], int rem)
     }
 }
 
+#ifndef KFEC_AEAD_AB
+#define KFEC_AEAD_AB 0  // timing ablations only (wrong output): bit 0 = no Poly1305 arithmetic, bit 1 = no ChaCha20 rounds
+#endif
+
 constexpr int kRow = 8;                  // lanes per packet
 constexpr int kAeadBlock = 256;          // 32 packets per workgroup
 constexpr int kRowsPerBlock = kAeadBlock / kRow;
@@ -400,7 +404,7 @@ __global__ void __launch_bounds__(kAeadBlock) aead_kernel(AeadArgs a)
         // lane j: r^(j+1); then r^8, r^16, r^24, r^32
         F5 pw = r;
 #pragma unroll
-        for (int d = 1; d < kRow; d <<= 1) {
+        for (int d = 1; d < ((KFEC_AEAD_AB & 1) ? 1 : kRow); d <<= 1) {
             const F5 y = f5_shfl_up(pw, d);
             if (lane >= d) pw = f5_mul(pw, y);
         }
@@ -425,7 +429,12 @@ __global__ void __launch_bounds__(kAeadBlock) aead_kernel(AeadArgs a)
             uint32_t ct[16];
             if (cs < n) {
                 uint32_t ks[16], in[16];
-                chacha_block(k, c + 1, nw, ks);
+                if (KFEC_AEAD_AB & 2) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) ks[i] = k[i & 7] + c;
+                } else {
+                    chacha_block(k, c + 1, nw, ks);
+                }
                 load64(a.src, a.src_dw, off + cs, in);
                 const bool part = cs + 64 > n;
                 if (part) mask64(in, (int)(n - cs));
@@ -497,7 +506,7 @@ __global__ void __launch_bounds__(kAeadBlock) aead_kernel(AeadArgs a)
                 if (b < NB) {
                     const int blen = (int)min(16u, M - 16 * b);
                     const F5 m = f5_block(msg[4 * i], msg[4 * i + 1], msg[4 * i + 2], msg[4 * i + 3], blen);
-                    if (t) acc[i] = f5_mul(acc[i], r32);
+                    if (t && !(KFEC_AEAD_AB & 1)) acc[i] = f5_mul(acc[i], r32);
                     f5_add(acc[i], m);
                     blast[i] = (int)b;
                 }
@@ -511,6 +520,11 @@ __global__ void __launch_bounds__(kAeadBlock) aead_kernel(AeadArgs a)
             F5 rp = f5_shfl(pw, e1 & 7);
             const int q = e1 >> 3;
             const F5 rq = q == 1 ? r8 : q == 2 ? r16 : r24;
+            if (KFEC_AEAD_AB & 1) {
+                f5_add(h, acc[i]);
+                f5_add(h, rq);
+                continue;
+            }
             if (q) rp = f5_mul(rp, rq);
             if (blast[i] >= 0) f5_add(h, f5_mul(acc[i], rp));
         }
