@@ -147,8 +147,9 @@ class Calib:
             self.lib.calib_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
             self.lib.calib_read_bytes.argtypes = [ctypes.c_size_t]
             self.lib.calib_read_bytes.restype = ctypes.c_size_t
-            self.lib.calib_gfmac.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
-                                             ctypes.c_void_p]
+            self.lib.calib_issue.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+            self.lib.calib_issue_instructions.argtypes = [ctypes.c_uint32]
+            self.lib.calib_issue_instructions.restype = ctypes.c_uint64
 
     def _time(self, torch, launch, reps=5):
         s = torch.cuda.current_stream()
@@ -173,14 +174,23 @@ class Calib:
         ms = self._time(torch, lambda st: self.lib.calib_read(buf.data_ptr(), n, sink.data_ptr(), st))
         return None if ms is None else self.lib.calib_read_bytes(n) / (ms * 1e-3) / 1e9
 
-    def gfmac_ceiling(self, torch, dev, rows, cus):
-        """byte-MACs/s of the MAC kernels' VALU instruction mix with no memory traffic."""
+    def gfmac_ceiling(self, torch, dev, cus):
+        """Issue bound of the perm MAC on this box, byte-MACs/s: every SIMD issuing nothing but the
+        3 v_perm_b32 + v_bitop3_b32 + v_xor_b32 that make 4 byte-MACs per lane, at the rates measured by
+        tools/calib.hip's instruction chains (8 waves per SIMD).  An upper bound for any kernel built on it."""
         if not self.lib:
             return None
         sink = torch.zeros(16, dtype=torch.int32, device=dev)
-        blocks, iters = cus * 8, 2048
-        ms = self._time(torch, lambda st: self.lib.calib_gfmac(sink.data_ptr(), blocks, iters, rows, st), reps=3)
-        return None if ms is None else blocks * 256 * iters * 32 * rows / (ms * 1e-3)
+        blocks = cus * 8
+        secs = []
+        for op in range(3):
+            ms = self._time(torch, lambda st, op=op: self.lib.calib_issue(op, sink.data_ptr(), blocks, st), reps=3)
+            if ms is None:
+                return None
+            # seconds per wave-instruction on one SIMD
+            secs.append(ms * 1e-3 / (self.lib.calib_issue_instructions(blocks) / (4.0 * cus)))
+        t_perm, t_bitop3, t_xor = secs
+        return 4 * 64 * 4 * cus / (3 * t_perm + t_bitop3 + t_xor)
 
 
 def rank_groups(groups_per_gpu: int, world: int, rank: int) -> tuple[int, int, int]:
@@ -352,9 +362,9 @@ def main():
             "step_frac_read_of_ceiling": round(step_read_gbs / read_ceiling, 4) if read_ceiling else None,
             "frac_of_ceiling": round(achieved / read_ceiling, 4) if read_ceiling else None}
     if args.config == "200:55" and rank == 0:
-        # VALU-bound: byte-MACs per second of each kernel against the same instruction mix with no memory
+        # VALU-bound: byte-MACs per second of each kernel against the perm MAC's issue bound on this box
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        ceil_mac = calib.gfmac_ceiling(torch, dev, 8, cus)
+        ceil_mac = calib.gfmac_ceiling(torch, dev, cus)
         enc_mac = G * R * K * B / (enc_ms * 1e-3)
         dec_mac = n_rec * K * B / (dec_ms * 1e-3)
         roof.update({"bound": "valu", "unit": "byte-MAC/s", "achieved": round(enc_mac, 0),
@@ -363,8 +373,8 @@ def main():
                      "decode_achieved": round(dec_mac, 0),
                      "decode_frac": round(dec_mac / ceil_mac, 4) if ceil_mac else None,
                      "hbm_achieved": round(achieved, 1), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "ceiling_kernel": "tools/calib.hip gfmac<8>: mac_kernel's perm-MAC mix, 8 rows x 32-B "
-                                       "granules, tables from LDS, no memory"})
+                     "ceiling_kernel": "issue bound: 4 byte-MACs per lane per (3 v_perm_b32 + v_bitop3_b32 + "
+                                       "v_xor_b32) at the rates tools/calib.hip measures on this box"})
 
     result = {
         "metric": METRIC,

@@ -4,20 +4,19 @@
 //   calib_read(p, bytes, stream)     linear 16-B-per-lane read of [p, p + bytes), one contiguous 16 KiB chunk
 //                                    per 256-lane workgroup (4 loads in flight per lane), non-persistent grid:
 //                                    the HBM read ceiling of this box (6.48 TB/s on r01 boxes).
-//   calib_gfmac(sink, blocks, iters, rows, stream)
-//                                    the MAC kernels' inner loop with the memory taken out: 32-byte granules
-//                                    (8 dwords per lane), per "shard" the three selector extractions per dword
-//                                    and `rows` perm MACs per dword with the perm tables read from LDS exactly
-//                                    as mac_kernel reads them (ds_read_b128 broadcast, once per 4 granules
-//                                    here, so the LDS reads do not limit it).  rows = 8 is the
-//                                    MT = 8 row tile of the fec=200:55 kernels; the byte-MAC rate it reaches
-//                                    is the VALU ceiling those kernels are held against.
-//                                    byte-MACs per launch = blocks * 256 * iters * 32 * rows.
+//   calib_issue(op, sink, blocks, stream)
+//                                    issue rate of one VALU instruction of the perm MAC (op 0 v_perm_b32,
+//                                    1 v_bitop3_b32, 2 v_xor_b32): 16 independent inline-asm chains per lane,
+//                                    kIssueIters iterations, `blocks` 256-lane workgroups (8 waves per SIMD
+//                                    at blocks = 8 x CUs).  wave-instructions per launch = blocks * 4 * 16 *
+//                                    kIssueIters.  bench.py turns the three rates into the perm MAC's issue
+//                                    bound: 4 byte-MACs per (3 v_perm + 1 v_bitop3 + 1 v_xor) per lane --
+//                                    an upper bound on any kernel built from it, since the selector
+//                                    extraction, loads, stores and address arithmetic come on top.
 // Build: hipcc --offload-arch=gfx950 -O3 -fPIC -shared -o tools/libkfec_calib.so tools/calib.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../kcptube_amd/csrc/kfec_gf.hpp"
 
 namespace {
 
@@ -34,53 +33,27 @@ __global__ void __launch_bounds__(256) read_chunk4(const uint8_t *a, size_t nchu
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) sink[0] = acc.x;  // keeps the loads alive
 }
 
-template <int MT>
-__global__ void __launch_bounds__(256) gfmac(uint32_t iters, uint32_t seed, uint32_t *sink)
+constexpr int kIssueIters = 2048;
+
+template <int OP>
+__global__ void __launch_bounds__(256) issue(uint32_t seed, uint32_t *sink)
 {
-    constexpr int TBL_DW = ((5 * MT + 3) / 4) * 4;
-    constexpr int NS = 16;  // distinct "shards" of tables (wave-uniform, as the real kernels' encode tables)
-    __shared__ __attribute__((aligned(16))) uint32_t s_tab[NS * TBL_DW];
-    for (int e = threadIdx.x; e < NS * MT; e += 256) {
-        uint32_t t[5];
-        kfec::gf_perm_tables((uint32_t)(e * 37 + seed) & 0xFFu, t);
-        const int s = e / MT, r = e - s * MT;
+    uint32_t v[16];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) s_tab[s * TBL_DW + 5 * r + i] = t[i];
-    }
-    __syncthreads();
-    uint32_t x[8], acc[MT][8];
+    for (int i = 0; i < 16; ++i) v[i] = seed * (threadIdx.x + 1) + i * 0x9E3779B9u;
+    const uint32_t a = seed ^ threadIdx.x, b = a * 3u;
+    for (int it = 0; it < kIssueIters; ++it) {
 #pragma unroll
-    for (int w = 0; w < 8; ++w) x[w] = (threadIdx.x + 1) * 0x9E3779B9u ^ (seed + w * 0x85EBCA6Bu);
-#pragma unroll
-    for (int r = 0; r < MT; ++r)
-#pragma unroll
-        for (int w = 0; w < 8; ++w) acc[r][w] = 0;
-    // tables are read from LDS once per 4 granules, so the loop is the perm-MAC VALU work and nothing else
-    for (uint32_t it = 0; it < iters; it += 4) {
-        const uint4 *tv = reinterpret_cast<const uint4 *>(s_tab + ((it / 4) % NS) * TBL_DW);
-        uint32_t t[TBL_DW];
-#pragma unroll
-        for (int i = 0; i < TBL_DW / 4; ++i) {
-            const uint4 q = tv[i];
-            t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-#pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                const uint32_t xv = x[w] ^ (it + k);  // a fresh granule (one XOR stands in for the load)
-                const uint32_t s0 = xv & 0x07070707u, s1 = (xv >> 3) & 0x07070707u, s2 = (xv >> 6) & 0x03030303u;
-#pragma unroll
-                for (int r = 0; r < MT; ++r) acc[r][w] = kfec::perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
-            }
+        for (int i = 0; i < 16; ++i) {
+            if constexpr (OP == 0) asm volatile("v_perm_b32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(a), "v"(b));
+            if constexpr (OP == 1) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(v[i]) : "v"(a), "v"(b));
+            if constexpr (OP == 2) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(v[i]) : "v"(a));
         }
     }
-    uint32_t v = 0;
+    uint32_t r = 0;
 #pragma unroll
-    for (int r = 0; r < MT; ++r)
-#pragma unroll
-        for (int w = 0; w < 8; ++w) v ^= acc[r][w];
-    if (v == 0x12345678u) sink[0] = v;
+    for (int i = 0; i < 16; ++i) r ^= v[i];
+    if (r == 0x12345678u) sink[0] = r;  // keeps the chains alive
 }
 
 }  // namespace
@@ -99,15 +72,18 @@ int calib_read(const void *p, size_t bytes, uint32_t *sink, void *stream)
 // bytes actually read by calib_read for a buffer of `bytes`
 size_t calib_read_bytes(size_t bytes) { return bytes / (4 * 256 * 16) * (4 * 256 * 16); }
 
-int calib_gfmac(uint32_t *sink, uint32_t blocks, uint32_t iters, int rows, void *stream)
+int calib_issue(int op, uint32_t *sink, uint32_t blocks, void *stream)
 {
     const hipStream_t s = (hipStream_t)stream;
-    switch (rows) {
-    case 3: hipLaunchKernelGGL(gfmac<3>, dim3(blocks), dim3(256), 0, s, iters, 0x5EEDu, sink); break;
-    case 8: hipLaunchKernelGGL(gfmac<8>, dim3(blocks), dim3(256), 0, s, iters, 0x5EEDu, sink); break;
+    switch (op) {
+    case 0: hipLaunchKernelGGL(issue<0>, dim3(blocks), dim3(256), 0, s, 0x5EEDu, sink); break;
+    case 1: hipLaunchKernelGGL(issue<1>, dim3(blocks), dim3(256), 0, s, 0x5EEDu, sink); break;
+    case 2: hipLaunchKernelGGL(issue<2>, dim3(blocks), dim3(256), 0, s, 0x5EEDu, sink); break;
     default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+uint64_t calib_issue_instructions(uint32_t blocks) { return (uint64_t)blocks * 4 * 16 * kIssueIters; }
 
 }  // extern "C"
