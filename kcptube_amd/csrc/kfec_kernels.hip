@@ -4,22 +4,23 @@
 //   matrix   fecpp.cpp:368-415, 453-490   enc = [I_K ; Vbot * Vtop^-1]  (build_matrix_kernel)
 //   encode   fecpp.cpp:495-513            parity_r = XOR_j enc[K+r][j] * D_j   (mac_kernel<.., false>)
 //   decode   fecpp.cpp:518-587            share selection + K x K inverse + m output rows
-//                                           (decode_prep_* + mac_kernel<.., true>)
+//                                           (decode_prep_* + syn_kernel / syn_list_kernel for R <= 8,
+//                                            mac_kernel<.., true> for R > 8)
 //   addmul   fecpp.cpp:170-223, fecpp_ssse3.cpp:541-575   z ^= c * x  (the "perm MAC" below)
 //
-// Design (DESIGN.md has the numbers):
+// Design (DESIGN.md section 4 has the numbers):
 // * perm MAC.  c * x for a constant c is linear over GF(2), so c*x = c*(x & 7) ^ c*(x & 0x38) ^ c*(x & 0xC0).
 //   Each term is an 8- or 4-entry table lookup, and v_perm_b32 does 4 such byte lookups (one per byte of a
-//   dword) in one VALU op.  Per data dword and coefficient: 3 v_perm_b32 + XORs; the 3 selector extractions
-//   are shared by all coefficients of a data dword.  No LDS traffic per data byte and no bank conflicts:
-//   the ~5 table dwords per coefficient are read once per shard per lane (LDS broadcast reads).
-// * Flattened work: one lane = one (group, V-byte column) item; consecutive lanes take consecutive columns
-//   (coalesced 1 KiB per wave-instruction at V = 16), wrapping into the next group.  Persistent grid-stride
-//   over items.  A workgroup iteration touches <= GMAX groups, whose per-group decode tables are expanded
-//   into LDS at the start of the iteration.
-// * Decode coefficients: per group only the m x m sub-system of the missing rows is inverted (Gauss-Jordan
-//   with LDS log/antilog tables); the rest of the K x K inverse follows by one product.  The inverse is
-//   unique, so the coefficients equal the reference's K x K Gauss-Jordan result bit for bit.
+//   dword) in one VALU op.  Per data dword and coefficient: 3 v_perm_b32 + v_bitop3_b32 + v_xor_b32; the 3
+//   selector extractions are shared by all coefficients of a data dword.  No LDS traffic per data byte.
+// * Flattened work: one lane = one (group, 32-byte column) item; consecutive lanes take consecutive columns
+//   (2 KiB per wave-instruction), wrapping into the next group.  One workgroup per 256 items (non-persistent);
+//   R > 8 runs MT = 8 row tiles numbered so that the tiles of one chunk share an XCD (block_chunk_tile).
+//   A row's last granule is end-aligned (gran_off), loads run consume-then-refill PD granules ahead.
+// * Decode for R <= 8 in syndrome form: y = parity ^ E * D_present with the encode's wave-uniform tables,
+//   then out = C * y with the per-group m x m inverse in C (syn_kernel); sparse loss takes a listed shape
+//   over the groups that lost data (syn_list_kernel), chosen on the device.  The coefficients equal the
+//   reference's K x K Gauss-Jordan result bit for bit (the inverse is unique).
 #include "kfec_gf.hpp"
 #include "kfec_internal.hpp"
 
