@@ -24,7 +24,7 @@ namespace kfec {
 
 namespace {
 
-constexpr int kSealBlock = 512;  // 16 packets share one LDS copy of the 28 KiB of tables: 4 workgroups = 32 waves per CU
+constexpr int kSealBlock = 512;  // 16 packets share one LDS copy of the tables (28 KiB): 4 workgroups = 32 waves per CU
 
 struct Crc32Tables {
     uint32_t t[4][256];
@@ -72,11 +72,54 @@ constexpr int kCrcRound = kCrcLane * kRowLanes;    // 512 B
 constexpr int kCrcBatch = KFEC_SEAL_BATCH;         // rounds whose loads are issued together
 constexpr int kRowsPerBlock = kSealBlock / kRowLanes;
 
+#ifndef KFEC_SEAL_NIB
+#define KFEC_SEAL_NIB 0  // 1: nibble-indexed tables -- no LDS bank conflicts, but +33% VALU and slower
+#endif
+
+// The CRC tables each workgroup stages into LDS.
+//  nibble form (KFEC_SEAL_NIB): every map is GF(2)-linear, so it is the XOR of one 16-entry table per input
+//    nibble.  A 16-entry table is 16 consecutive dwords -- 16 distinct banks -- and all lanes of one
+//    ds_read_b32 read the same table, so distinct entries never share a bank: no conflicts (the byte tables'
+//    256 entries over 32 banks gave ~4-5-way conflicts on random data).  The 32 chunk lookups of a 16-byte
+//    chunk are also independent of each other, where slicing-by-4 chains the four dwords of a chunk.
+//      chunk[k][v]:    raw CRC (zero init) of a 16-byte chunk holding nibble v at nibble k, zeros elsewhere
+//      shift[m][j][v]: nibble j = v of a CRC register advanced through 16 << m zero bytes (m = 5: 512)
+//      byte0[v]:       the bytewise table, for packets of fewer than 4 bytes
+//  byte form: [0] slicing-by-4 (4 x 256), [1 + m] the shift maps, each 4 x 256
+struct CrcLds {
+#if KFEC_SEAL_NIB
+    uint32_t chunk[32][16];
+    uint32_t shift[6][8][16];
+    uint32_t byte0[256];
+#else
+    uint32_t t[kCrcMaps][4][256];
+#endif
+};
+constexpr int kCrcWords = (int)(sizeof(CrcLds) / 4);
+
 __global__ void crc_tables_kernel(uint32_t *tab)
 {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;  // e = ((map * 4) + j) * 256 + v
-    if (e >= kCrcMaps * 1024) return;
-    const int map = e / 1024, j = (e / 256) & 3, v = e & 255;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kCrcWords) return;
+#if KFEC_SEAL_NIB
+    uint32_t r = 0;
+    if (e < 32 * 16) {  // chunk[k][v]
+        const int k = e / 16, v = e % 16;
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t byte = i == k / 2 ? (uint32_t)v << (4 * (k & 1)) : 0u;
+            r = (r >> 8) ^ c_crc.t[0][(r ^ byte) & 0xFFu];
+        }
+    } else if (e < 32 * 16 + 6 * 8 * 16) {  // shift[m][j][v]
+        const int f = e - 32 * 16, m = f / 128, j = (f / 16) & 7, v = f % 16;
+        r = (uint32_t)v << (4 * j);
+        const int d = kCrcLane << m;
+        for (int i = 0; i < d; ++i) r = (r >> 8) ^ c_crc.t[0][r & 0xFFu];
+    } else {
+        r = c_crc.t[0][e - 32 * 16 - 6 * 8 * 16];
+    }
+    tab[e] = r;
+#else
+    const int map = e / 1024, j = (e / 256) & 3, v = e & 255;  // e = ((map * 4) + j) * 256 + v
     if (map == 0) {
         tab[e] = c_crc.t[j][v];
         return;
@@ -85,18 +128,72 @@ __global__ void crc_tables_kernel(uint32_t *tab)
     const int d = kCrcLane << (map - 1);
     for (int i = 0; i < d; ++i) r = (r >> 8) ^ c_crc.t[0][r & 0xFFu];
     tab[e] = r;
+#endif
 }
 
+#if KFEC_SEAL_NIB
+// entry at byte offset bo (= 4 * nibble) of a 16-entry table
+__device__ __forceinline__ uint32_t nib_at(const uint32_t *t16, uint32_t bo)
+{
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(t16) + bo);
+}
+
+// raw CRC (zero init) of the 16-byte chunk o: 32 independent lookups
+__device__ __forceinline__ uint32_t crc_chunk(const CrcLds &t, const uint32_t (&o)[4])
+{
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t lo = (o[i] << 2) & 0x3C3C3C3Cu, hi = (o[i] >> 2) & 0x3C3C3C3Cu;  // 4 x nibble per byte
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            c ^= nib_at(t.chunk[8 * i + 2 * b], (lo >> (8 * b)) & 0xFFu) ^
+                 nib_at(t.chunk[8 * i + 2 * b + 1], (hi >> (8 * b)) & 0xFFu);
+    }
+    return c;
+}
+
+// map m applied to the register r
+__device__ __forceinline__ uint32_t crc_shift(const CrcLds &t, int m, uint32_t r)
+{
+    const uint32_t lo = (r << 2) & 0x3C3C3C3Cu, hi = (r >> 2) & 0x3C3C3C3Cu;
+    uint32_t c = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        c ^= nib_at(t.shift[m][2 * b], (lo >> (8 * b)) & 0xFFu) ^ nib_at(t.shift[m][2 * b + 1], (hi >> (8 * b)) & 0xFFu);
+    return c;
+}
+
+__device__ __forceinline__ uint32_t crc_byte(const CrcLds &t, uint32_t c, uint32_t byte)
+{
+    return (c >> 8) ^ t.byte0[(c ^ byte) & 0xFFu];
+}
+#else
 __device__ __forceinline__ uint32_t crc_dword(const uint32_t (*t)[256], uint32_t c, uint32_t d)
 {
     const uint32_t x = c ^ d;
     return t[3][x & 0xFFu] ^ t[2][(x >> 8) & 0xFFu] ^ t[1][(x >> 16) & 0xFFu] ^ t[0][x >> 24];
 }
 
-__device__ __forceinline__ uint32_t crc_shift(const uint32_t (*t)[256], uint32_t r)
+__device__ __forceinline__ uint32_t crc_chunk(const CrcLds &t, const uint32_t (&o)[4])
 {
-    return t[0][r & 0xFFu] ^ t[1][(r >> 8) & 0xFFu] ^ t[2][(r >> 16) & 0xFFu] ^ t[3][r >> 24];
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c = crc_dword(t.t[0], c, o[i]);
+    return c;
 }
+
+__device__ __forceinline__ uint32_t crc_shift(const CrcLds &t, int m, uint32_t r)
+{
+    const uint32_t (*s)[256] = t.t[1 + m];
+    return s[0][r & 0xFFu] ^ s[1][(r >> 8) & 0xFFu] ^ s[2][(r >> 16) & 0xFFu] ^ s[3][r >> 24];
+}
+
+__device__ __forceinline__ uint32_t crc_byte(const CrcLds &t, uint32_t c, uint32_t byte)
+{
+    return (c >> 8) ^ t.t[0][0][(c ^ byte) & 0xFFu];
+}
+#endif
 
 // 16 bytes [q0, q0 + 16) of base[start, start + len), zero outside (dword-aligned base, dwords < lim32):
 // one 16-byte load at the covering dword (dword alignment suffices on gfx950) and one more dword
@@ -132,7 +229,7 @@ __device__ __forceinline__ void chunk16(const uint32_t *base32, uint64_t lim32, 
 }
 
 // standard CRC-32 of base[start, start + len), computed by the 32 lanes of a row (all lanes get it)
-__device__ uint32_t row_crc32(const uint32_t (*tab)[4][256], const uint32_t *base32, uint64_t lim32, uint64_t start,
+__device__ __forceinline__ uint32_t row_crc32(const CrcLds &tab, const uint32_t *base32, uint64_t lim32, uint64_t start,
                               uint32_t len, uint32_t lane)
 {
     if (len < 4) {  // the init cannot be folded into message bytes: one lane, byte by byte
@@ -140,7 +237,7 @@ __device__ uint32_t row_crc32(const uint32_t (*tab)[4][256], const uint32_t *bas
         if (lane == 0) {
             uint32_t o[4];
             chunk16(base32, lim32, start, len, 0, o);
-            for (uint32_t i = 0; i < len; ++i) c = (c >> 8) ^ tab[0][0][(c ^ (o[0] >> (8 * i))) & 0xFFu];
+            for (uint32_t i = 0; i < len; ++i) c = crc_byte(tab, c, o[0] >> (8 * i));
         }
         return ~__shfl(c, 0, kRowLanes);
     }
@@ -166,11 +263,9 @@ __device__ uint32_t row_crc32(const uint32_t (*tab)[4][256], const uint32_t *bas
         }
 #pragma unroll
         for (int u = 0; u < kCrcBatch; ++u) {  // fixed trip count (a break here sent o[][] to scratch)
-            uint32_t c = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) c = crc_dword(tab[0], c, o[u][i]);
+            const uint32_t c = crc_chunk(tab, o[u]);
             // Horner over this lane's chunks: R = XOR_r shift_{(rounds-1-r)*512}(chunk CRC of round r)
-            if (r0 + u < rounds) R = crc_shift(tab[6], R) ^ c;
+            if (r0 + u < rounds) R = crc_shift(tab, 5, R) ^ c;
         }
     }
     // one butterfly per packet (not per round): by linearity the 32 lanes' Horner sums combine exactly as
@@ -179,7 +274,7 @@ __device__ uint32_t row_crc32(const uint32_t (*tab)[4][256], const uint32_t *bas
     for (int k = 0; k < 5; ++k) {
         const uint32_t other = __shfl_xor(R, 1 << k, kRowLanes);
         const bool later = lane & (1u << k);
-        R = crc_shift(tab[1 + k], later ? other : R) ^ (later ? R : other);
+        R = crc_shift(tab, k, later ? other : R) ^ (later ? R : other);
     }
     return ~R;
 }
@@ -206,10 +301,10 @@ struct SealArgs {
     int mode;
 };
 
-__device__ __forceinline__ void stage_tables(const uint32_t *tab, uint32_t (*s_tab)[4][256])
+__device__ __forceinline__ void stage_tables(const uint32_t *tab, CrcLds &s_tab)
 {
-    uint32_t *flat = &s_tab[0][0][0];
-    for (int i = threadIdx.x; i < kCrcMaps * 1024; i += kSealBlock) flat[i] = tab[i];
+    uint32_t *flat = reinterpret_cast<uint32_t *>(&s_tab);
+    for (int i = threadIdx.x; i < kCrcWords; i += kSealBlock) flat[i] = tab[i];
     __syncthreads();
 }
 
@@ -227,7 +322,7 @@ __device__ __forceinline__ void store_chunk(uint32_t *dst, uint32_t j, uint32_t 
 
 __global__ void __launch_bounds__(kSealBlock) seal_kernel(SealArgs a)
 {
-    __shared__ uint32_t s_tab[kCrcMaps][4][256];
+    __shared__ CrcLds s_tab;
     stage_tables(a.tab, s_tab);
     const uint32_t lane = threadIdx.x % kRowLanes;
     for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRowLanes; p < a.P;
@@ -283,7 +378,7 @@ __global__ void __launch_bounds__(kSealBlock) seal_kernel(SealArgs a)
 
 __global__ void __launch_bounds__(kSealBlock) open_kernel(SealArgs a)
 {
-    __shared__ uint32_t s_tab[kCrcMaps][4][256];
+    __shared__ CrcLds s_tab;
     stage_tables(a.tab, s_tab);
     const uint32_t lane = threadIdx.x % kRowLanes;
     const bool px = a.mode == KFEC_SEAL_PLAIN_XOR;
@@ -395,7 +490,7 @@ __global__ void __launch_bounds__(kSealBlock) open_kernel(SealArgs a)
 // its trailer written over the next packet while another row is still reading that packet for its CRC.
 __global__ void __launch_bounds__(kSealBlock) seal_in_place_kernel(SealArgs a, bool open)
 {
-    __shared__ uint32_t s_tab[kCrcMaps][4][256];
+    __shared__ CrcLds s_tab;
     stage_tables(a.tab, s_tab);
     const uint32_t lane = threadIdx.x % kRowLanes;
     uint8_t *base = const_cast<uint8_t *>(reinterpret_cast<const uint8_t *>(a.src));
@@ -439,8 +534,8 @@ uint32_t *crc_tables(hipStream_t s)
     std::lock_guard<std::mutex> lk(mu);
     if (!tabs[dev]) {
         uint32_t *t = nullptr;
-        if (hipMalloc(&t, kCrcMaps * 1024 * sizeof(uint32_t)) != hipSuccess) return nullptr;
-        hipLaunchKernelGGL(crc_tables_kernel, dim3((kCrcMaps * 1024 + 255) / 256), dim3(256), 0, s, t);
+        if (hipMalloc(&t, kCrcWords * sizeof(uint32_t)) != hipSuccess) return nullptr;
+        hipLaunchKernelGGL(crc_tables_kernel, dim3((kCrcWords + 255) / 256), dim3(256), 0, s, t);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return nullptr;
         tabs[dev] = t;
     }
