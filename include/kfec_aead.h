@@ -31,6 +31,7 @@ extern "C" {
 #endif
 
 /* encryption_mode values (share_defines.hpp:29) this header implements */
+#define KFEC_AEAD_AES_GCM 4    /* encryption_mode::aes_gcm: AES-256-GCM, 16-byte nonce */
 #define KFEC_AEAD_CHACHA20 6   /* encryption_mode::chacha20: ChaCha20-Poly1305, 8-byte nonce */
 #define KFEC_AEAD_XCHACHA20 7  /* encryption_mode::xchacha20: XChaCha20-Poly1305, 24-byte nonce */
 #define KFEC_AEAD_TAG 16

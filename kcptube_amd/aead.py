@@ -21,9 +21,10 @@ import ctypes as C
 
 from .fec import _check, _dptr, _stream_handle, _vp, load_library
 
-CHACHA20 = 6   # encryption_mode::chacha20 (share_defines.hpp:29)
+AES_GCM = 4    # encryption_mode::aes_gcm (share_defines.hpp:29)
+CHACHA20 = 6   # encryption_mode::chacha20
 XCHACHA20 = 7  # encryption_mode::xchacha20
-MODES = {"chacha20": CHACHA20, "xchacha20": XCHACHA20}
+MODES = {"aes_gcm": AES_GCM, "chacha20": CHACHA20, "xchacha20": XCHACHA20}
 TAG = 16
 OVERHEAD = 18
 
@@ -36,7 +37,7 @@ class AeadCipher:
         self.mode = MODES.get(mode, mode) if isinstance(mode, str) else int(mode)
         if isinstance(password, str):
             password = password.encode()
-        if self.mode not in (CHACHA20, XCHACHA20):
+        if self.mode not in (AES_GCM, CHACHA20, XCHACHA20):
             raise ValueError(f"unsupported AEAD mode {mode!r}")
         if not password:
             raise ValueError("empty password (the reference leaves its cipher objects unset)")

@@ -29,13 +29,6 @@
 #include "../../include/kfec_aead.h"
 #include "kfec_internal.hpp"
 
-struct kfec_aead {
-    int mode = 0;
-    int device = 0;
-    uint32_t key[8] = {};
-    uint32_t *d_tab = nullptr;  // per-iv entries: chacha20 {polykey[8]}, xchacha20 {subkey[8], polykey[8]}
-};
-
 namespace kfec {
 
 namespace {
@@ -582,6 +575,8 @@ int launch_aead(const kfec_aead *k, bool open, size_t P, const void *src, size_t
                 hipStream_t s)
 {
     if (P == 0) return 0;
+    if (k->mode == KFEC_AEAD_AES_GCM)
+        return launch_gcm(k, open, P, src, src_bytes, off, len, iv, dst, dst_pitch, out_len, ok, s);
     AeadArgs a{};
     a.src = static_cast<const uint32_t *>(src);
     a.src_dw = (src_bytes + 3) / 4;
@@ -610,32 +605,33 @@ int aead_setup(kfec_aead *k, const void *password, size_t len)
 {
     uint8_t *d_pw = nullptr;
     uint32_t *d_key = nullptr;
+    const bool gcm = k->mode == KFEC_AEAD_AES_GCM;
     const size_t entries = k->mode == KFEC_AEAD_XCHACHA20 ? 16 : 8;
     if (hipMalloc(&d_pw, len) != hipSuccess) return KFEC_ENOMEM;
     if (hipMalloc(&d_key, 32) != hipSuccess) {
         (void)hipFree(d_pw);
         return KFEC_ENOMEM;
     }
-    if (hipMalloc(&k->d_tab, 65536 * entries * sizeof(uint32_t)) != hipSuccess) {
-        (void)hipFree(d_pw);
-        (void)hipFree(d_key);
-        k->d_tab = nullptr;
-        return KFEC_ENOMEM;
-    }
     int rc = KFEC_OK;
-    if (hipMemcpy(d_pw, password, len, hipMemcpyHostToDevice) != hipSuccess) rc = KFEC_EHIP;
+    if (!gcm && hipMalloc(&k->d_tab, 65536 * entries * sizeof(uint32_t)) != hipSuccess) {
+        k->d_tab = nullptr;
+        rc = KFEC_ENOMEM;
+    }
+    if (rc == KFEC_OK && hipMemcpy(d_pw, password, len, hipMemcpyHostToDevice) != hipSuccess) rc = KFEC_EHIP;
     if (rc == KFEC_OK) {
         hipLaunchKernelGGL(sha3_256_kernel, dim3(1), dim3(64), 0, nullptr, d_pw, (uint64_t)len, d_key);
-        hipLaunchKernelGGL(iv_table_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, k->mode, d_key, k->d_tab);
-        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-            hipMemcpy(k->key, d_key, 32, hipMemcpyDeviceToHost) != hipSuccess)
+        if (gcm) rc = gcm_setup(k, d_key);
+        else hipLaunchKernelGGL(iv_table_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, k->mode, d_key, k->d_tab);
+        if (rc == KFEC_OK && (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+                              hipMemcpy(k->key, d_key, 32, hipMemcpyDeviceToHost) != hipSuccess))
             rc = KFEC_EHIP;
     }
     (void)hipFree(d_pw);
     (void)hipFree(d_key);
     if (rc != KFEC_OK) {
-        (void)hipFree(k->d_tab);
+        if (k->d_tab) (void)hipFree(k->d_tab);
         k->d_tab = nullptr;
+        gcm_free(k);
     }
     return rc;
 }
@@ -648,7 +644,8 @@ int kfec_aead_create(int mode, const void *password, size_t password_len, kfec_a
 {
     if (!out) return KFEC_EINVAL;
     *out = nullptr;
-    if ((mode != KFEC_AEAD_CHACHA20 && mode != KFEC_AEAD_XCHACHA20) || !password || password_len == 0)
+    if ((mode != KFEC_AEAD_AES_GCM && mode != KFEC_AEAD_CHACHA20 && mode != KFEC_AEAD_XCHACHA20) || !password ||
+        password_len == 0)
         return KFEC_EINVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return KFEC_ENODEV;
@@ -672,6 +669,7 @@ void kfec_aead_destroy(kfec_aead *a)
 {
     if (!a) return;
     if (a->d_tab) (void)hipFree(a->d_tab);
+    kfec::gcm_free(a);
     delete a;
 }
 

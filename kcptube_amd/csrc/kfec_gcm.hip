@@ -1,0 +1,476 @@
+// kfec_gcm.hip -- kcptube's aes_gcm packet mode as gfx950 kernels (include/kfec_aead.h).
+//
+// encrypt_data / decrypt_data (data_operations.cpp:171-234, 373-435) over encrypt_decrypt<aes_256_gcm>
+// (aead.hpp:237-312): Botan "AES-256/GCM" with kcptube's 16-byte nonce (iv_raw repeated 8 times), so
+// J0 = GHASH_H(IV || 0^64 || be64(128)) (NIST SP 800-38D 7.1); CTR from inc32(J0); tag = E_K(J0) xor
+// GHASH_H(AD || pad || C || pad || be64(8|AD|) || be64(8|C|)); packet = C || tag || iv_raw.
+//
+// The MI355X-first part: everything the key and the 16-bit iv_raw determine is computed once per key, on the
+// device, for all 65536 iv values -- J0, E_K(J0) and the first kKsBytes of the CTR keystream (128 MiB at
+// 2 KiB per iv, which covers kcptube's packets) -- so per packet AES is a table read; only blocks past
+// kKsBytes run AES in the kernel.  GHASH runs lane-parallel: a row of 4 lanes per packet, lane j owning
+// message blocks j, j + 4, ...; each lane keeps a Horner accumulator stepped by H^4 and ends by one multiply
+// by H^e, 1 <= e <= 4, and the row XORs the four.  A multiply by a fixed power of H is 32 lookups of
+// 16-byte entries (one 16-entry table per input nibble, Shoup) from LDS: 16 entries of 16 bytes span the
+// 64 banks once, so the lookups of one instruction never conflict.  The message block of lane j is the
+// ciphertext block the same lane just produced (the AD is exactly one block), so no data crosses lanes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../../include/kfec_aead.h"
+#include "kfec_internal.hpp"
+
+namespace kfec {
+
+namespace {
+
+#ifndef KFEC_GCM_KS_BYTES
+#define KFEC_GCM_KS_BYTES 2048  // keystream bytes tabulated per iv (multiple of 16)
+#endif
+constexpr uint32_t kKsBytes = KFEC_GCM_KS_BYTES;
+
+// ---- AES-256 (FIPS 197), byte-oriented: setup and the blocks past the table ---------------------------
+struct Sbox {
+    uint8_t s[256];
+};
+
+constexpr Sbox make_sbox()
+{
+    // inverse in GF(2^8) mod x^8 + x^4 + x^3 + x + 1 via exp / log of the generator 3, then the affine map
+    uint8_t ex[256] = {}, lg[256] = {};
+    uint32_t x = 1;
+    for (int i = 0; i < 255; ++i) {
+        ex[i] = (uint8_t)x;
+        lg[x] = (uint8_t)i;
+        uint32_t x2 = x << 1;
+        if (x2 & 0x100u) x2 ^= 0x11Bu;
+        x = (x2 ^ x) & 0xFFu;  // x * 3
+    }
+    Sbox b{};
+    for (int a = 0; a < 256; ++a) {
+        const uint32_t inv = a ? ex[(255 - lg[a]) % 255] : 0u;
+        uint32_t y = inv;
+        for (int k = 1; k < 5; ++k) y ^= ((inv << k) | (inv >> (8 - k))) & 0xFFu;
+        b.s[a] = (uint8_t)(y ^ 0x63u);
+    }
+    return b;
+}
+
+__device__ const Sbox c_sbox = make_sbox();
+
+__device__ __forceinline__ uint32_t xtime(uint32_t a) { return ((a << 1) ^ ((a & 0x80u) ? 0x1Bu : 0u)) & 0xFFu; }
+
+// rk: 240 bytes of round keys
+__device__ void aes256_encrypt(const uint8_t *rk, const uint8_t (&in)[16], uint8_t (&out)[16])
+{
+    uint8_t s[16];
+    for (int i = 0; i < 16; ++i) s[i] = in[i] ^ rk[i];
+    for (int r = 1; r <= 14; ++r) {
+        uint8_t t[16];
+        for (int i = 0; i < 16; ++i) t[i] = c_sbox.s[s[(i + 4 * (i % 4)) % 16]];  // SubBytes + ShiftRows
+        if (r < 14) {
+            for (int c = 0; c < 4; ++c) {  // MixColumns
+                const uint32_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
+                const uint32_t e = a0 ^ a1 ^ a2 ^ a3;
+                s[4 * c] = (uint8_t)(a0 ^ e ^ xtime(a0 ^ a1));
+                s[4 * c + 1] = (uint8_t)(a1 ^ e ^ xtime(a1 ^ a2));
+                s[4 * c + 2] = (uint8_t)(a2 ^ e ^ xtime(a2 ^ a3));
+                s[4 * c + 3] = (uint8_t)(a3 ^ e ^ xtime(a3 ^ a0));
+            }
+        } else {
+            for (int i = 0; i < 16; ++i) s[i] = t[i];
+        }
+        for (int i = 0; i < 16; ++i) s[i] ^= rk[16 * r + i];
+    }
+    for (int i = 0; i < 16; ++i) out[i] = s[i];
+}
+
+// ---- GHASH multiply, bit-serial (setup only): z = x * y in GF(2^128), SP 800-38D 6.3 bit order ---------
+__device__ void gf128_mul(const uint8_t (&x)[16], const uint8_t (&y)[16], uint8_t (&z)[16])
+{
+    uint8_t v[16], r[16] = {};
+    for (int i = 0; i < 16; ++i) v[i] = y[i];
+    for (int i = 0; i < 128; ++i) {
+        if ((x[i / 8] >> (7 - i % 8)) & 1)
+            for (int k = 0; k < 16; ++k) r[k] ^= v[k];
+        const uint32_t lsb = v[15] & 1u;
+        for (int k = 15; k > 0; --k) v[k] = (uint8_t)((v[k] >> 1) | (v[k - 1] << 7));
+        v[0] >>= 1;
+        if (lsb) v[0] ^= 0xE1u;
+    }
+    for (int i = 0; i < 16; ++i) z[i] = r[i];
+}
+
+// key schedule and H = E_K(0^128): one thread
+__global__ void gcm_key_kernel(const uint32_t *key, uint8_t *rk, uint8_t *h)
+{
+    if (blockIdx.x || threadIdx.x) return;
+    uint8_t w[240];
+    for (int i = 0; i < 32; ++i) w[i] = (uint8_t)(key[i / 4] >> (8 * (i % 4)));
+    uint32_t rcon = 1;
+    for (int i = 8; i < 60; ++i) {
+        uint8_t t[4] = {w[4 * i - 4], w[4 * i - 3], w[4 * i - 2], w[4 * i - 1]};
+        if (i % 8 == 0) {
+            const uint8_t t0 = t[0];
+            t[0] = (uint8_t)(c_sbox.s[t[1]] ^ rcon);
+            t[1] = c_sbox.s[t[2]];
+            t[2] = c_sbox.s[t[3]];
+            t[3] = c_sbox.s[t0];
+            rcon = xtime(rcon);
+        } else if (i % 8 == 4) {
+            for (int k = 0; k < 4; ++k) t[k] = c_sbox.s[t[k]];
+        }
+        for (int k = 0; k < 4; ++k) w[4 * i + k] = w[4 * i - 32 + k] ^ t[k];
+    }
+    for (int i = 0; i < 240; ++i) rk[i] = w[i];
+    uint8_t z[16] = {}, o[16];
+    aes256_encrypt(w, z, o);
+    for (int i = 0; i < 16; ++i) h[i] = o[i];
+}
+
+// Shoup tables of H^1 .. H^4: gh[p][k][v] = (the block whose byte k / 2 is v << 4 (k & 1), zeros elsewhere)
+// * H^(p+1), 16 bytes each; thread per entry
+__global__ void gcm_tables_kernel(const uint8_t *h, uint8_t *gh)
+{
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= 4 * 32 * 16) return;
+    const int p = e / 512, k = (e / 16) % 32, v = e % 16;
+    uint8_t hp[16], hh[16];
+    for (int i = 0; i < 16; ++i) hp[i] = hh[i] = h[i];
+    for (int q = 0; q < p; ++q) {
+        uint8_t t[16];
+        gf128_mul(hp, hh, t);
+        for (int i = 0; i < 16; ++i) hp[i] = t[i];
+    }
+    uint8_t x[16] = {}, z[16];
+    x[k / 2] = (uint8_t)(v << (4 * (k & 1)));
+    gf128_mul(x, hp, z);
+    for (int i = 0; i < 16; ++i) gh[16 * e + i] = z[i];
+}
+
+// per iv: J0 and E_K(J0) (iv table, 32 bytes per iv)
+__global__ void gcm_iv_kernel(const uint8_t *rk, const uint8_t *h, uint8_t *ivt)
+{
+    const uint32_t iv = blockIdx.x * blockDim.x + threadIdx.x;
+    if (iv >= 65536u) return;
+    uint8_t hh[16], y[16], t[16], mask[16];
+    for (int i = 0; i < 16; ++i) {
+        hh[i] = h[i];
+        y[i] = (uint8_t)(i % 2 ? iv >> 8 : iv);  // the nonce: iv_raw (little-endian) x 8
+    }
+    gf128_mul(y, hh, t);  // GHASH(IV || len block): (IV * H ^ L) * H, L = 0^64 || be64(128)
+    t[15] ^= 0x80u;
+    gf128_mul(t, hh, y);
+    aes256_encrypt(rk, y, mask);
+    for (int i = 0; i < 16; ++i) {
+        ivt[32 * (size_t)iv + i] = y[i];
+        ivt[32 * (size_t)iv + 16 + i] = mask[i];
+    }
+}
+
+// counter block i (i >= 1) of a packet: inc32^i(J0)
+__device__ __forceinline__ void ctr_block(const uint8_t *j0, uint32_t i, uint8_t (&c)[16])
+{
+    for (int k = 0; k < 12; ++k) c[k] = j0[k];
+    const uint32_t v = ((uint32_t)j0[12] << 24 | (uint32_t)j0[13] << 16 | (uint32_t)j0[14] << 8 | j0[15]) + i;
+    c[12] = (uint8_t)(v >> 24);
+    c[13] = (uint8_t)(v >> 16);
+    c[14] = (uint8_t)(v >> 8);
+    c[15] = (uint8_t)v;
+}
+
+// the first kKsBytes of keystream of every iv: thread per (iv, 16-byte block)
+__global__ void gcm_ks_kernel(const uint8_t *rk, const uint8_t *ivt, uint8_t *ks)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr uint32_t kBlocks = kKsBytes / 16;
+    if (e >= 65536ull * kBlocks) return;
+    const uint32_t iv = (uint32_t)(e / kBlocks), q = (uint32_t)(e % kBlocks);
+    uint8_t c[16], o[16];
+    ctr_block(ivt + 32 * (size_t)iv, q + 1, c);
+    aes256_encrypt(rk, c, o);
+    uint4 *d = reinterpret_cast<uint4 *>(ks + (size_t)iv * kKsBytes + 16 * (size_t)q);
+    uint32_t wv[4];
+    for (int i = 0; i < 4; ++i)
+        wv[i] = (uint32_t)o[4 * i] | (uint32_t)o[4 * i + 1] << 8 | (uint32_t)o[4 * i + 2] << 16 |
+                (uint32_t)o[4 * i + 3] << 24;
+    *d = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+}
+
+// ---- the packet kernel ---------------------------------------------------------------------------------
+constexpr int kRow = 4;  // lanes per packet
+constexpr int kGcmBlock = 256;
+constexpr int kRowsPerBlock = kGcmBlock / kRow;
+
+struct GcmArgs {
+    const uint32_t *src;
+    uint64_t src_dw;
+    const uint64_t *off;
+    const uint32_t *len;
+    const uint16_t *iv;
+    uint8_t *dst;
+    uint64_t dst_pitch;
+    uint32_t *out_len;
+    uint8_t *ok;
+    const uint4 *gh;      // [4][32][16] Shoup tables of H^1..H^4
+    const uint8_t *ivt;   // [65536][32] J0, E_K(J0)
+    const uint8_t *ks;    // [65536][kKsBytes] keystream
+    const uint8_t *rk;    // AES round keys (blocks past the table)
+    uint64_t P;
+};
+
+__device__ __forceinline__ uint4 u4_xor(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
+
+// a * H^(p+1) from the LDS tables T = s_gh[p] ([32][16] entries)
+__device__ __forceinline__ uint4 gh_mul(const uint4 (*T)[16], uint4 a)
+{
+    const uint32_t d[4] = {a.x, a.y, a.z, a.w};
+    uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t lo = (d[i] << 4) & 0xF0F0F0F0u, hi = d[i] & 0xF0F0F0F0u;  // 16 * nibble per byte
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int k = 2 * (4 * i + b);
+            const uint4 x = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(T[k]) + ((lo >> (8 * b)) & 0xFFu));
+            const uint4 y = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(T[k + 1]) + ((hi >> (8 * b)) & 0xFFu));
+            acc = u4_xor(acc, u4_xor(x, y));
+        }
+    }
+    return acc;
+}
+
+// 16 bytes at byte address a of a dword-aligned buffer of lim32 dwords (zero past it)
+__device__ __forceinline__ uint4 load16(const uint32_t *b32, uint64_t lim32, uint64_t a)
+{
+    const uint64_t w = a >> 2;
+    uint32_t d[5];
+    if (w + 5 <= lim32) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(b32 + w);
+        d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
+        d[4] = b32[w + 4];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) d[i] = w + i < lim32 ? b32[w + i] : 0u;
+    }
+    const uint32_t sh = (uint32_t)(a & 3u);
+    return make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], sh), __builtin_amdgcn_alignbyte(d[2], d[1], sh),
+                      __builtin_amdgcn_alignbyte(d[3], d[2], sh), __builtin_amdgcn_alignbyte(d[4], d[3], sh));
+}
+
+// keep the first rem bytes (0 < rem < 16)
+__device__ __forceinline__ uint4 mask16(uint4 v, uint32_t rem)
+{
+    uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = (int)rem - 4 * i;
+        d[i] = k >= 4 ? d[i] : k <= 0 ? 0u : d[i] & ((1u << (8 * k)) - 1u);
+    }
+    return make_uint4(d[0], d[1], d[2], d[3]);
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+template <bool OPEN>
+__global__ void __launch_bounds__(kGcmBlock) gcm_kernel(GcmArgs a)
+{
+    __shared__ uint4 s_gh[4][32][16];  // 32 KiB
+    {
+        uint4 *flat = &s_gh[0][0][0];
+        for (int i = threadIdx.x; i < 4 * 32 * 16; i += kGcmBlock) flat[i] = a.gh[i];
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x % kRow;
+    // the AD block: "KCP PortHopping" || 0x00 (aead.hpp:16) as little-endian dwords
+    const uint4 ad = make_uint4(0x2050434Bu, 0x74726F50u, 0x70706F48u, 0x00676E69u);
+    for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRow; p < a.P;
+         p += (uint64_t)gridDim.x * kRowsPerBlock) {
+        const uint32_t L = a.len[p];
+        const uint64_t off = a.off[p];
+        uint32_t n, iv, ptag = 0;
+        if (OPEN) {
+            if (L < KFEC_AEAD_OVERHEAD || L - KFEC_AEAD_OVERHEAD > a.dst_pitch) {
+                if (lane == 0) {
+                    a.out_len[p] = 0;
+                    a.ok[p] = 0;
+                }
+                continue;
+            }
+            n = L - KFEC_AEAD_OVERHEAD;
+            ptag = load16(a.src, a.src_dw, off + n + 4 * lane).x;  // this lane's tag dword
+            iv = load16(a.src, a.src_dw, off + n + 16).x & 0xFFFFu;
+        } else {
+            if (L == 0 || (uint64_t)L + KFEC_AEAD_OVERHEAD > a.dst_pitch) {  // "empty data" / no room
+                if (lane == 0) a.out_len[p] = 0;
+                continue;
+            }
+            n = L;
+            iv = a.iv[p];
+        }
+        const uint8_t *ivrow = a.ivt + 32 * (size_t)iv;
+        const uint4 *ksrow = reinterpret_cast<const uint4 *>(a.ks + (size_t)iv * kKsBytes);
+        const uint32_t nc = (n + 15) / 16;  // ciphertext blocks
+        const uint32_t NB = nc + 2;         // AD block, ciphertext blocks, length block
+        const uint32_t rounds = (NB + kRow - 1) / kRow;
+        uint8_t *dst = a.dst + p * a.dst_pitch;
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+        int blast = -1;
+        for (uint32_t t = 0; t < rounds; ++t) {
+            const uint32_t b = t * kRow + lane;
+            if (b >= NB) continue;
+            uint4 x;
+            if (b == 0) {
+                x = ad;
+            } else if (b == NB - 1) {  // be64(8 * 15) || be64(8 * n)
+                x = make_uint4(0u, bswap32(120u), bswap32(n >> 29), bswap32(n << 3));
+            } else {
+                const uint32_t q = b - 1, qb = 16 * q;
+                uint4 ks;
+                if (qb + 16 <= kKsBytes) {
+                    ks = ksrow[q];
+                } else {  // past the table: AES of the counter block here
+                    uint8_t c[16], o[16];
+                    ctr_block(ivrow, q + 1, c);
+                    aes256_encrypt(a.rk, c, o);
+                    ks = make_uint4((uint32_t)o[0] | o[1] << 8 | o[2] << 16 | (uint32_t)o[3] << 24,
+                                    (uint32_t)o[4] | o[5] << 8 | o[6] << 16 | (uint32_t)o[7] << 24,
+                                    (uint32_t)o[8] | o[9] << 8 | o[10] << 16 | (uint32_t)o[11] << 24,
+                                    (uint32_t)o[12] | o[13] << 8 | o[14] << 16 | (uint32_t)o[15] << 24);
+                }
+                uint4 in = load16(a.src, a.src_dw, off + qb);
+                const uint32_t rem = n - qb;  // > 0
+                if (rem < 16) in = mask16(in, rem);
+                uint4 out = u4_xor(in, ks);
+                if (rem < 16) out = mask16(out, rem);
+                x = OPEN ? in : out;
+                uint32_t *d32 = reinterpret_cast<uint32_t *>(dst + qb);
+                if (rem >= 16) {
+                    *reinterpret_cast<uint4 *>(d32) = out;
+                } else {
+                    const uint32_t o4[4] = {out.x, out.y, out.z, out.w};
+                    // open: whole dwords (the zero pad is part of the output); seal: bytes below n only
+                    const uint32_t nd = OPEN ? (rem + 3) / 4 : rem / 4;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if ((uint32_t)i < nd) d32[i] = o4[i];
+                    if (!OPEN && (rem & 3)) {
+                        const uint32_t v = o4[rem / 4];
+                        uint8_t *bp = dst + qb + 4 * (rem / 4);
+                        for (uint32_t i = 0; i < (rem & 3); ++i) bp[i] = (uint8_t)(v >> (8 * i));
+                    }
+                }
+            }
+            if (t) acc = gh_mul(s_gh[3], acc);  // * H^4
+            acc = u4_xor(acc, x);
+            blast = (int)b;
+        }
+        // * H^(NB - b_last), then the row's XOR
+        if (blast >= 0) {
+            const int e = (int)NB - blast;  // 1..4
+            acc = gh_mul(s_gh[e - 1], acc);
+        } else {
+            acc = make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int d = 1; d < kRow; d <<= 1) {
+            acc.x ^= __shfl_xor(acc.x, d, kRow);
+            acc.y ^= __shfl_xor(acc.y, d, kRow);
+            acc.z ^= __shfl_xor(acc.z, d, kRow);
+            acc.w ^= __shfl_xor(acc.w, d, kRow);
+        }
+        const uint4 mask = *reinterpret_cast<const uint4 *>(ivrow + 16);
+        const uint32_t tag[4] = {acc.x ^ mask.x, acc.y ^ mask.y, acc.z ^ mask.z, acc.w ^ mask.w};
+        if (OPEN) {
+            const uint32_t mine = lane == 0 ? tag[0] : lane == 1 ? tag[1] : lane == 2 ? tag[2] : tag[3];
+            uint32_t bad = mine != ptag ? 1u : 0u;
+#pragma unroll
+            for (int d = 1; d < kRow; d <<= 1) bad |= __shfl_xor(bad, d, kRow);
+            if (bad) {  // no unauthenticated plaintext leaves the kernel
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);
+                const uint32_t nd = (n + 3) / 4;
+                for (uint32_t i = lane; i < nd; i += kRow) d32[i] = 0u;
+            }
+            if (lane == 0) {
+                a.out_len[p] = bad ? 0u : n;
+                a.ok[p] = bad ? 0 : 1;
+            }
+        } else {
+            // tag || iv_raw || zeros to the next multiple of 4: bytes n .. n + 21, 6 per lane
+            const uint32_t end = (n + KFEC_AEAD_OVERHEAD + 3) & ~3u;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const uint32_t i = 6 * lane + q;
+                if (n + i < end) {
+                    const uint32_t w = i < 4 ? tag[0] : i < 8 ? tag[1] : i < 12 ? tag[2] : i < 16 ? tag[3] : iv;
+                    dst[n + i] = (uint8_t)(i < 18 ? (w >> (8 * (i & 3))) & 0xFFu : 0u);
+                }
+            }
+            if (lane == 0) a.out_len[p] = n + KFEC_AEAD_OVERHEAD;
+        }
+    }
+}
+
+}  // namespace
+
+int gcm_setup(kfec_aead *k, const uint32_t *d_key)
+{
+    if (hipMalloc(&k->d_rk, 240) != hipSuccess || hipMalloc(&k->d_h, 16) != hipSuccess ||
+        hipMalloc(&k->d_gh, 4 * 32 * 16 * 16) != hipSuccess || hipMalloc(&k->d_ivt, 65536 * 32) != hipSuccess ||
+        hipMalloc(&k->d_ks, (size_t)65536 * kKsBytes) != hipSuccess)
+        return KFEC_ENOMEM;
+    k->ks_bytes = kKsBytes;
+    hipLaunchKernelGGL(gcm_key_kernel, dim3(1), dim3(64), 0, nullptr, d_key, k->d_rk, k->d_h);
+    hipLaunchKernelGGL(gcm_tables_kernel, dim3(4 * 32 * 16 / 256), dim3(256), 0, nullptr, k->d_h, k->d_gh);
+    hipLaunchKernelGGL(gcm_iv_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, k->d_rk, k->d_h, k->d_ivt);
+    const uint64_t ks_threads = 65536ull * (kKsBytes / 16);
+    hipLaunchKernelGGL(gcm_ks_kernel, dim3((uint32_t)((ks_threads + 255) / 256)), dim3(256), 0, nullptr, k->d_rk,
+                       k->d_ivt, k->d_ks);
+    return hipGetLastError() == hipSuccess ? KFEC_OK : KFEC_EHIP;
+}
+
+void gcm_free(kfec_aead *k)
+{
+    for (void *p : {(void *)k->d_rk, (void *)k->d_h, (void *)k->d_gh, (void *)k->d_ivt, (void *)k->d_ks})
+        if (p) (void)hipFree(p);
+    k->d_rk = k->d_h = k->d_gh = k->d_ivt = k->d_ks = nullptr;
+}
+
+int launch_gcm(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
+               const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
+               hipStream_t s)
+{
+    if (P == 0) return 0;
+    GcmArgs a{};
+    a.src = static_cast<const uint32_t *>(src);
+    a.src_dw = (src_bytes + 3) / 4;
+    a.off = off;
+    a.len = len;
+    a.iv = iv;
+    a.dst = static_cast<uint8_t *>(dst);
+    a.dst_pitch = dst_pitch;
+    a.out_len = out_len;
+    a.ok = ok;
+    a.gh = reinterpret_cast<const uint4 *>(k->d_gh);
+    a.ivt = k->d_ivt;
+    a.ks = k->d_ks;
+    a.rk = k->d_rk;
+    a.P = P;
+    static int cus = [] {
+        int d = 0, n = 0;
+        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) !=
+                                                  hipSuccess)
+            n = 256;
+        return std::max(n, 1);
+    }();
+    // 32 KiB of GHASH tables per workgroup: 5 resident per CU; grid-stride over packets
+    const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
+    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * 5));
+    if (open) hipLaunchKernelGGL(gcm_kernel<true>, grid, dim3(kGcmBlock), 0, s, a);
+    else hipLaunchKernelGGL(gcm_kernel<false>, grid, dim3(kGcmBlock), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace kfec

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/kfec_frame.h"
+#include "../../include/kfec_aead.h"
 
 namespace kfec {
 
@@ -93,4 +94,26 @@ int launch_framed_encode(const uint8_t *d_enc, int K, int N, size_t G, const voi
 int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
                 const uint32_t *len, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok, hipStream_t s);
 
+}  // namespace kfec
+
+// a per-connection AEAD cipher (include/kfec_aead.h): the derived key and its per-iv device tables
+struct kfec_aead {
+    int mode = 0;
+    int device = 0;
+    uint32_t key[8] = {};
+    uint32_t *d_tab = nullptr;   // chacha modes: per-iv polykey (xchacha20: subkey first), kfec_aead.hip
+    uint8_t *d_rk = nullptr;     // aes_gcm (kfec_gcm.hip): AES-256 round keys
+    uint8_t *d_h = nullptr;      //   H = E_K(0)
+    uint8_t *d_gh = nullptr;     //   Shoup tables of H^1..H^4
+    uint8_t *d_ivt = nullptr;    //   per iv: J0, E_K(J0)
+    uint8_t *d_ks = nullptr;     //   per iv: the first ks_bytes of CTR keystream
+    uint32_t ks_bytes = 0;
+};
+
+namespace kfec {
+int gcm_setup(kfec_aead *k, const uint32_t *d_key);
+void gcm_free(kfec_aead *k);
+int launch_gcm(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
+               const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
+               hipStream_t s);
 }  // namespace kfec
