@@ -19,6 +19,7 @@
 #include <algorithm>
 
 #include "../../include/kfec_aead.h"
+#include "kfec_gf.hpp"
 #include "kfec_internal.hpp"
 
 namespace kfec {
@@ -29,6 +30,18 @@ namespace {
 #define KFEC_GCM_KS_BYTES 2048  // keystream bytes tabulated per iv (multiple of 16)
 #endif
 constexpr uint32_t kKsBytes = KFEC_GCM_KS_BYTES;
+#ifndef KFEC_GCM_PF
+#define KFEC_GCM_PF 0  // 1: load round t + 1's keystream and data while round t is hashed (measured: no gain)
+#endif
+#ifndef KFEC_GCM_AB
+#define KFEC_GCM_AB 0  // timing ablations only (wrong output): bit 0 = no GHASH multiplies, bit 1 = no keystream loads
+#endif
+#ifndef KFEC_GCM_DWTAIL
+#define KFEC_GCM_DWTAIL 1  // seal's tail (last partial ciphertext dword, tag, iv_raw, pad) as dword stores
+#endif
+#ifndef KFEC_GCM_NT
+#define KFEC_GCM_NT 0  // non-temporal packet loads / stores (keep the keystream table in the caches)
+#endif
 
 // ---- AES-256 (FIPS 197), byte-oriented: setup and the blocks past the table ---------------------------
 struct Sbox {
@@ -200,7 +213,10 @@ __global__ void gcm_ks_kernel(const uint8_t *rk, const uint8_t *ivt, uint8_t *ks
 
 // ---- the packet kernel ---------------------------------------------------------------------------------
 constexpr int kRow = 4;  // lanes per packet
-constexpr int kGcmBlock = 256;
+#ifndef KFEC_GCM_BLOCK
+#define KFEC_GCM_BLOCK 256
+#endif
+constexpr int kGcmBlock = KFEC_GCM_BLOCK;
 constexpr int kRowsPerBlock = kGcmBlock / kRow;
 
 struct GcmArgs {
@@ -222,24 +238,35 @@ struct GcmArgs {
 
 __device__ __forceinline__ uint4 u4_xor(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
 
-// a * H^(p+1) from the LDS tables T = s_gh[p] ([32][16] entries)
+// a * H^(p+1) from the LDS tables T = s_gh[p] ([32][16] entries): per input dword 8 lookups in flight, folded
+// in with 3-input XORs (v_bitop3_b32)
 __device__ __forceinline__ uint4 gh_mul(const uint4 (*T)[16], uint4 a)
 {
     const uint32_t d[4] = {a.x, a.y, a.z, a.w};
-    uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t lo = (d[i] << 4) & 0xF0F0F0F0u, hi = d[i] & 0xF0F0F0F0u;  // 16 * nibble per byte
+        uint4 e[8];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const int k = 2 * (4 * i + b);
-            const uint4 x = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(T[k]) + ((lo >> (8 * b)) & 0xFFu));
-            const uint4 y = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(T[k + 1]) + ((hi >> (8 * b)) & 0xFFu));
-            acc = u4_xor(acc, u4_xor(x, y));
+            e[2 * b] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(T[k]) + ((lo >> (8 * b)) & 0xFFu));
+            e[2 * b + 1] =
+                *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(T[k + 1]) + ((hi >> (8 * b)) & 0xFFu));
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            r0 = xor3(r0, e[2 * m].x, e[2 * m + 1].x);
+            r1 = xor3(r1, e[2 * m].y, e[2 * m + 1].y);
+            r2 = xor3(r2, e[2 * m].z, e[2 * m + 1].z);
+            r3 = xor3(r3, e[2 * m].w, e[2 * m + 1].w);
         }
     }
-    return acc;
+    return make_uint4(r0, r1, r2, r3);
 }
+
+typedef unsigned int u32x4n __attribute__((ext_vector_type(4)));
 
 // 16 bytes at byte address a of a dword-aligned buffer of lim32 dwords (zero past it)
 __device__ __forceinline__ uint4 load16(const uint32_t *b32, uint64_t lim32, uint64_t a)
@@ -247,9 +274,15 @@ __device__ __forceinline__ uint4 load16(const uint32_t *b32, uint64_t lim32, uin
     const uint64_t w = a >> 2;
     uint32_t d[5];
     if (w + 5 <= lim32) {
-        const uint4 q = *reinterpret_cast<const uint4 *>(b32 + w);
+        uint4 q;
+        if (KFEC_GCM_NT) {
+            const u32x4n v = __builtin_nontemporal_load(reinterpret_cast<const u32x4n *>(b32 + w));
+            q = make_uint4(v.x, v.y, v.z, v.w);
+        } else {
+            q = *reinterpret_cast<const uint4 *>(b32 + w);
+        }
         d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
-        d[4] = b32[w + 4];
+        d[4] = KFEC_GCM_NT ? __builtin_nontemporal_load(b32 + w + 4) : b32[w + 4];
     } else {
 #pragma unroll
         for (int i = 0; i < 5; ++i) d[i] = w + i < lim32 ? b32[w + i] : 0u;
@@ -273,8 +306,12 @@ __device__ __forceinline__ uint4 mask16(uint4 v, uint32_t rem)
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+#ifndef KFEC_GCM_WPE
+#define KFEC_GCM_WPE 4  // waves per SIMD the register allocation must allow
+#endif
+
 template <bool OPEN>
-__global__ void __launch_bounds__(kGcmBlock) gcm_kernel(GcmArgs a)
+__global__ void __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(KFEC_GCM_WPE))) gcm_kernel(GcmArgs a)
 {
     __shared__ uint4 s_gh[4][32][16];  // 32 KiB
     {
@@ -317,9 +354,27 @@ __global__ void __launch_bounds__(kGcmBlock) gcm_kernel(GcmArgs a)
         uint8_t *dst = a.dst + p * a.dst_pitch;
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
         int blast = -1;
+        uint32_t ctail = 0;  // seal: the ciphertext's partial last dword (KFEC_GCM_DWTAIL)
+        // keystream (from the table) and packet bytes of round t's block, when it is a ciphertext block
+        auto fetch = [&](uint32_t t, uint4 &ks, uint4 &in) {
+            const uint32_t b = t * kRow + lane;
+            if (b == 0 || b + 1 >= NB) return;
+            const uint32_t q = b - 1;
+            if (16 * q + 16 <= kKsBytes && !(KFEC_GCM_AB & 2)) ks = ksrow[q];
+            in = load16(a.src, a.src_dw, off + 16 * q);
+        };
+        const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+        uint4 cks = zero, cin = zero;
+        if (KFEC_GCM_PF) fetch(0, cks, cin);
         for (uint32_t t = 0; t < rounds; ++t) {
             const uint32_t b = t * kRow + lane;
             if (b >= NB) continue;
+            uint4 nks = zero, nin = zero;
+            if (KFEC_GCM_PF) {
+                if (t + 1 < rounds) fetch(t + 1, nks, nin);
+            } else {
+                fetch(t, cks, cin);
+            }
             uint4 x;
             if (b == 0) {
                 x = ad;
@@ -327,10 +382,8 @@ __global__ void __launch_bounds__(kGcmBlock) gcm_kernel(GcmArgs a)
                 x = make_uint4(0u, bswap32(120u), bswap32(n >> 29), bswap32(n << 3));
             } else {
                 const uint32_t q = b - 1, qb = 16 * q;
-                uint4 ks;
-                if (qb + 16 <= kKsBytes) {
-                    ks = ksrow[q];
-                } else {  // past the table: AES of the counter block here
+                uint4 ks = cks;
+                if (qb + 16 > kKsBytes) {  // past the table: AES of the counter block here
                     uint8_t c[16], o[16];
                     ctr_block(ivrow, q + 1, c);
                     aes256_encrypt(a.rk, c, o);
@@ -339,7 +392,7 @@ __global__ void __launch_bounds__(kGcmBlock) gcm_kernel(GcmArgs a)
                                     (uint32_t)o[8] | o[9] << 8 | o[10] << 16 | (uint32_t)o[11] << 24,
                                     (uint32_t)o[12] | o[13] << 8 | o[14] << 16 | (uint32_t)o[15] << 24);
                 }
-                uint4 in = load16(a.src, a.src_dw, off + qb);
+                uint4 in = cin;
                 const uint32_t rem = n - qb;  // > 0
                 if (rem < 16) in = mask16(in, rem);
                 uint4 out = u4_xor(in, ks);
@@ -347,7 +400,11 @@ __global__ void __launch_bounds__(kGcmBlock) gcm_kernel(GcmArgs a)
                 x = OPEN ? in : out;
                 uint32_t *d32 = reinterpret_cast<uint32_t *>(dst + qb);
                 if (rem >= 16) {
-                    *reinterpret_cast<uint4 *>(d32) = out;
+                    if (KFEC_GCM_NT) {
+                        u32x4n v = {out.x, out.y, out.z, out.w};
+                        __builtin_nontemporal_store(v, reinterpret_cast<u32x4n *>(d32));
+                    }
+                    else *reinterpret_cast<uint4 *>(d32) = out;
                 } else {
                     const uint32_t o4[4] = {out.x, out.y, out.z, out.w};
                     // open: whole dwords (the zero pad is part of the output); seal: bytes below n only
@@ -357,12 +414,18 @@ __global__ void __launch_bounds__(kGcmBlock) gcm_kernel(GcmArgs a)
                         if ((uint32_t)i < nd) d32[i] = o4[i];
                     if (!OPEN && (rem & 3)) {
                         const uint32_t v = o4[rem / 4];
-                        uint8_t *bp = dst + qb + 4 * (rem / 4);
-                        for (uint32_t i = 0; i < (rem & 3); ++i) bp[i] = (uint8_t)(v >> (8 * i));
+                        if (KFEC_GCM_DWTAIL) {
+                            ctail = v;  // goes out with the tag, as whole dwords
+                        } else {
+                            uint8_t *bp = dst + qb + 4 * (rem / 4);
+                            for (uint32_t i = 0; i < (rem & 3); ++i) bp[i] = (uint8_t)(v >> (8 * i));
+                        }
                     }
                 }
             }
-            if (t) acc = gh_mul(s_gh[3], acc);  // * H^4
+            cks = nks;
+            cin = nin;
+            if (t && !(KFEC_GCM_AB & 1)) acc = gh_mul(s_gh[3], acc);  // * H^4
             acc = u4_xor(acc, x);
             blast = (int)b;
         }
@@ -398,14 +461,35 @@ __global__ void __launch_bounds__(kGcmBlock) gcm_kernel(GcmArgs a)
                 a.ok[p] = bad ? 0 : 1;
             }
         } else {
-            // tag || iv_raw || zeros to the next multiple of 4: bytes n .. n + 21, 6 per lane
-            const uint32_t end = (n + KFEC_AEAD_OVERHEAD + 3) & ~3u;
+            if (KFEC_GCM_DWTAIL) {
+                // dwords from floor4(n): the ciphertext's last n % 4 bytes || tag || iv_raw || zero pad (5 or 6
+                // dwords, lane l writes dwords l and l + 4); the partial dword came from the lane that made it
+                const uint32_t o = n & 3u, n4 = n & ~3u;
+                const uint32_t cp = __shfl(ctail, (int)(nc % kRow), kRow);
+                const uint32_t cnt = (((n + KFEC_AEAD_OVERHEAD + 3u) & ~3u) - n4) / 4u;
+                const uint32_t w[7] = {o ? cp << (8 * (4 - o)) : 0u, tag[0], tag[1], tag[2], tag[3], iv, 0u};
 #pragma unroll
-            for (int q = 0; q < 6; ++q) {
-                const uint32_t i = 6 * lane + q;
-                if (n + i < end) {
-                    const uint32_t w = i < 4 ? tag[0] : i < 8 ? tag[1] : i < 12 ? tag[2] : i < 16 ? tag[3] : iv;
-                    dst[n + i] = (uint8_t)(i < 18 ? (w >> (8 * (i & 3))) & 0xFFu : 0u);
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t l = lane + kRow * h;  // dword index of the tail, 0..7
+                    uint32_t w1 = 0, w0 = 0;
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) {
+                        w1 = l == (uint32_t)i ? w[i + 1] : w1;
+                        w0 = l == (uint32_t)i ? w[i] : w0;
+                    }
+                    const uint32_t v = o ? __builtin_amdgcn_alignbyte(w1, w0, 4 - o) : w1;
+                    if (l < cnt) reinterpret_cast<uint32_t *>(dst + n4)[l] = v;
+                }
+            } else {
+                // tag || iv_raw || zeros to the next multiple of 4: bytes n .. n + 21, 6 per lane
+                const uint32_t end = (n + KFEC_AEAD_OVERHEAD + 3) & ~3u;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) {
+                    const uint32_t i = 6 * lane + q;
+                    if (n + i < end) {
+                        const uint32_t w = i < 4 ? tag[0] : i < 8 ? tag[1] : i < 12 ? tag[2] : i < 16 ? tag[3] : iv;
+                        dst[n + i] = (uint8_t)(i < 18 ? (w >> (8 * (i & 3))) & 0xFFu : 0u);
+                    }
                 }
             }
             if (lane == 0) a.out_len[p] = n + KFEC_AEAD_OVERHEAD;
@@ -465,9 +549,10 @@ int launch_gcm(const kfec_aead *k, bool open, size_t P, const void *src, size_t 
             n = 256;
         return std::max(n, 1);
     }();
-    // 32 KiB of GHASH tables per workgroup: 5 resident per CU; grid-stride over packets
+    // 32 KiB of GHASH tables per workgroup: 5 resident per CU (256 lanes; 512 lanes: 3, register-bound);
+    // grid-stride over packets
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
-    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * 5));
+    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * (kGcmBlock >= 512 ? 3 : 5)));
     if (open) hipLaunchKernelGGL(gcm_kernel<true>, grid, dim3(kGcmBlock), 0, s, a);
     else hipLaunchKernelGGL(gcm_kernel<false>, grid, dim3(kGcmBlock), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
