@@ -2,13 +2,15 @@
  * kfec_aead.h -- kcptube's AEAD packet modes on the device (the AEAD half).
  *
  * encrypt_data / decrypt_data (/root/reference/src/shares/data_operations.cpp:171-234, 373-435) for
- * encryption = aes_gcm, chacha20 and xchacha20, with the key and nonce handling of the reference's aead.hpp:
+ * encryption = aes_gcm, aes_ocb, chacha20 and xchacha20, with the key and nonce handling of the reference's
+ * aead.hpp:
  *   key    = SHA-3(256)(password)                                          (aead.hpp:405-437, 488-515)
- *   nonce  = the 16-bit iv_raw repeated: 16 bytes (aes_gcm), 8 (chacha20), 24 (xchacha20)
- *            (aead.hpp:291-311, 464-483, 542-562)
+ *   nonce  = the 16-bit iv_raw repeated: 16 bytes (aes_gcm), 12 (aes_ocb), 8 (chacha20), 24 (xchacha20)
+ *            (aead.hpp:291-311, 379-400, 464-483, 542-562)
  *   packet = ciphertext || 16-byte Poly1305 tag || iv_raw (2 bytes, little-endian)    (data_operations.cpp:214-219)
  *   associated data "KCP PortHopping"                                      (aead.hpp:16)
- * Botan's AES-256/GCM takes the 16-byte nonce through GHASH into J0 (SP 800-38D).
+ * Botan's AES-256/GCM takes the 16-byte nonce through GHASH into J0 (SP 800-38D); AES-256/OCB is RFC 7253
+ * with a 128-bit tag.
  * Botan's ChaCha20Poly1305 (the reference's library) runs the 8-byte nonce as the original construction
  * (64-bit block counter; MAC over AD || le64(|AD|) || C || le64(|C|)) and the 24-byte nonce as
  * XChaCha20-Poly1305 (HChaCha20 subkey, RFC 8439 MAC layout).  oracle/aead_oracle.py restates both and
@@ -16,8 +18,8 @@
  *
  * The nonce depends only on iv_raw, so everything the key and the nonce alone determine -- the Poly1305 key
  * (ChaCha20 block 0) and, for xchacha20, the HChaCha20 subkey; for aes_gcm J0, E_K(J0) and the first 2 KiB
- * of CTR keystream -- is computed once per key for all 65536 iv values (kfec_aead_create, on the device:
- * 2 MiB / 4 MiB / 130 MiB) and looked up per packet.
+ * of CTR keystream; for aes_ocb Offset_0 -- is computed once per key for all 65536 iv values
+ * (kfec_aead_create, on the device: 2 MiB / 4 MiB / 130 MiB / 1 MiB) and looked up per packet.
  *
  * Conventions as include/kfec.h: d_ pointers are device pointers, the stream is a hipStream_t as void*.
  */
@@ -35,6 +37,7 @@ extern "C" {
 
 /* encryption_mode values (share_defines.hpp:29) this header implements */
 #define KFEC_AEAD_AES_GCM 4    /* encryption_mode::aes_gcm: AES-256-GCM, 16-byte nonce */
+#define KFEC_AEAD_AES_OCB 5    /* encryption_mode::aes_ocb: AES-256-OCB (RFC 7253), 12-byte nonce */
 #define KFEC_AEAD_CHACHA20 6   /* encryption_mode::chacha20: ChaCha20-Poly1305, 8-byte nonce */
 #define KFEC_AEAD_XCHACHA20 7  /* encryption_mode::xchacha20: XChaCha20-Poly1305, 24-byte nonce */
 #define KFEC_AEAD_TAG 16

@@ -22,9 +22,10 @@ import ctypes as C
 from .fec import _check, _dptr, _stream_handle, _vp, load_library
 
 AES_GCM = 4    # encryption_mode::aes_gcm (share_defines.hpp:29)
+AES_OCB = 5    # encryption_mode::aes_ocb
 CHACHA20 = 6   # encryption_mode::chacha20
 XCHACHA20 = 7  # encryption_mode::xchacha20
-MODES = {"aes_gcm": AES_GCM, "chacha20": CHACHA20, "xchacha20": XCHACHA20}
+MODES = {"aes_gcm": AES_GCM, "aes_ocb": AES_OCB, "chacha20": CHACHA20, "xchacha20": XCHACHA20}
 TAG = 16
 OVERHEAD = 18
 
@@ -37,7 +38,7 @@ class AeadCipher:
         self.mode = MODES.get(mode, mode) if isinstance(mode, str) else int(mode)
         if isinstance(password, str):
             password = password.encode()
-        if self.mode not in (AES_GCM, CHACHA20, XCHACHA20):
+        if self.mode not in (AES_GCM, AES_OCB, CHACHA20, XCHACHA20):
             raise ValueError(f"unsupported AEAD mode {mode!r}")
         if not password:
             raise ValueError("empty password (the reference leaves its cipher objects unset)")

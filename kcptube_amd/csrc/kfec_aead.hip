@@ -577,6 +577,8 @@ int launch_aead(const kfec_aead *k, bool open, size_t P, const void *src, size_t
     if (P == 0) return 0;
     if (k->mode == KFEC_AEAD_AES_GCM)
         return launch_gcm(k, open, P, src, src_bytes, off, len, iv, dst, dst_pitch, out_len, ok, s);
+    if (k->mode == KFEC_AEAD_AES_OCB)
+        return launch_ocb(k, open, P, src, src_bytes, off, len, iv, dst, dst_pitch, out_len, ok, s);
     AeadArgs a{};
     a.src = static_cast<const uint32_t *>(src);
     a.src_dw = (src_bytes + 3) / 4;
@@ -605,7 +607,7 @@ int aead_setup(kfec_aead *k, const void *password, size_t len)
 {
     uint8_t *d_pw = nullptr;
     uint32_t *d_key = nullptr;
-    const bool gcm = k->mode == KFEC_AEAD_AES_GCM;
+    const bool gcm = k->mode == KFEC_AEAD_AES_GCM, ocb = k->mode == KFEC_AEAD_AES_OCB;
     const size_t entries = k->mode == KFEC_AEAD_XCHACHA20 ? 16 : 8;
     if (hipMalloc(&d_pw, len) != hipSuccess) return KFEC_ENOMEM;
     if (hipMalloc(&d_key, 32) != hipSuccess) {
@@ -613,7 +615,7 @@ int aead_setup(kfec_aead *k, const void *password, size_t len)
         return KFEC_ENOMEM;
     }
     int rc = KFEC_OK;
-    if (!gcm && hipMalloc(&k->d_tab, 65536 * entries * sizeof(uint32_t)) != hipSuccess) {
+    if (!gcm && !ocb && hipMalloc(&k->d_tab, 65536 * entries * sizeof(uint32_t)) != hipSuccess) {
         k->d_tab = nullptr;
         rc = KFEC_ENOMEM;
     }
@@ -621,6 +623,7 @@ int aead_setup(kfec_aead *k, const void *password, size_t len)
     if (rc == KFEC_OK) {
         hipLaunchKernelGGL(sha3_256_kernel, dim3(1), dim3(64), 0, nullptr, d_pw, (uint64_t)len, d_key);
         if (gcm) rc = gcm_setup(k, d_key);
+        else if (ocb) rc = ocb_setup(k, d_key);
         else hipLaunchKernelGGL(iv_table_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, k->mode, d_key, k->d_tab);
         if (rc == KFEC_OK && (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
                               hipMemcpy(k->key, d_key, 32, hipMemcpyDeviceToHost) != hipSuccess))
@@ -644,8 +647,9 @@ int kfec_aead_create(int mode, const void *password, size_t password_len, kfec_a
 {
     if (!out) return KFEC_EINVAL;
     *out = nullptr;
-    if ((mode != KFEC_AEAD_AES_GCM && mode != KFEC_AEAD_CHACHA20 && mode != KFEC_AEAD_XCHACHA20) || !password ||
-        password_len == 0)
+    if ((mode != KFEC_AEAD_AES_GCM && mode != KFEC_AEAD_AES_OCB && mode != KFEC_AEAD_CHACHA20 &&
+         mode != KFEC_AEAD_XCHACHA20) ||
+        !password || password_len == 0)
         return KFEC_EINVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return KFEC_ENODEV;

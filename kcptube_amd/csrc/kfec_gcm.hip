@@ -19,6 +19,8 @@
 #include <algorithm>
 
 #include "../../include/kfec_aead.h"
+#include "kfec_aes.hpp"
+#include "kfec_pkt.hpp"
 #include "kfec_gf.hpp"
 #include "kfec_internal.hpp"
 
@@ -39,65 +41,6 @@ constexpr uint32_t kKsBytes = KFEC_GCM_KS_BYTES;
 #ifndef KFEC_GCM_DWTAIL
 #define KFEC_GCM_DWTAIL 1  // seal's tail (last partial ciphertext dword, tag, iv_raw, pad) as dword stores
 #endif
-#ifndef KFEC_GCM_NT
-#define KFEC_GCM_NT 0  // non-temporal packet loads / stores (keep the keystream table in the caches)
-#endif
-
-// ---- AES-256 (FIPS 197), byte-oriented: setup and the blocks past the table ---------------------------
-struct Sbox {
-    uint8_t s[256];
-};
-
-constexpr Sbox make_sbox()
-{
-    // inverse in GF(2^8) mod x^8 + x^4 + x^3 + x + 1 via exp / log of the generator 3, then the affine map
-    uint8_t ex[256] = {}, lg[256] = {};
-    uint32_t x = 1;
-    for (int i = 0; i < 255; ++i) {
-        ex[i] = (uint8_t)x;
-        lg[x] = (uint8_t)i;
-        uint32_t x2 = x << 1;
-        if (x2 & 0x100u) x2 ^= 0x11Bu;
-        x = (x2 ^ x) & 0xFFu;  // x * 3
-    }
-    Sbox b{};
-    for (int a = 0; a < 256; ++a) {
-        const uint32_t inv = a ? ex[(255 - lg[a]) % 255] : 0u;
-        uint32_t y = inv;
-        for (int k = 1; k < 5; ++k) y ^= ((inv << k) | (inv >> (8 - k))) & 0xFFu;
-        b.s[a] = (uint8_t)(y ^ 0x63u);
-    }
-    return b;
-}
-
-__device__ const Sbox c_sbox = make_sbox();
-
-__device__ __forceinline__ uint32_t xtime(uint32_t a) { return ((a << 1) ^ ((a & 0x80u) ? 0x1Bu : 0u)) & 0xFFu; }
-
-// rk: 240 bytes of round keys
-__device__ void aes256_encrypt(const uint8_t *rk, const uint8_t (&in)[16], uint8_t (&out)[16])
-{
-    uint8_t s[16];
-    for (int i = 0; i < 16; ++i) s[i] = in[i] ^ rk[i];
-    for (int r = 1; r <= 14; ++r) {
-        uint8_t t[16];
-        for (int i = 0; i < 16; ++i) t[i] = c_sbox.s[s[(i + 4 * (i % 4)) % 16]];  // SubBytes + ShiftRows
-        if (r < 14) {
-            for (int c = 0; c < 4; ++c) {  // MixColumns
-                const uint32_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
-                const uint32_t e = a0 ^ a1 ^ a2 ^ a3;
-                s[4 * c] = (uint8_t)(a0 ^ e ^ xtime(a0 ^ a1));
-                s[4 * c + 1] = (uint8_t)(a1 ^ e ^ xtime(a1 ^ a2));
-                s[4 * c + 2] = (uint8_t)(a2 ^ e ^ xtime(a2 ^ a3));
-                s[4 * c + 3] = (uint8_t)(a3 ^ e ^ xtime(a3 ^ a0));
-            }
-        } else {
-            for (int i = 0; i < 16; ++i) s[i] = t[i];
-        }
-        for (int i = 0; i < 16; ++i) s[i] ^= rk[16 * r + i];
-    }
-    for (int i = 0; i < 16; ++i) out[i] = s[i];
-}
 
 // ---- GHASH multiply, bit-serial (setup only): z = x * y in GF(2^128), SP 800-38D 6.3 bit order ---------
 __device__ void gf128_mul(const uint8_t (&x)[16], const uint8_t (&y)[16], uint8_t (&z)[16])
@@ -120,22 +63,7 @@ __global__ void gcm_key_kernel(const uint32_t *key, uint8_t *rk, uint8_t *h)
 {
     if (blockIdx.x || threadIdx.x) return;
     uint8_t w[240];
-    for (int i = 0; i < 32; ++i) w[i] = (uint8_t)(key[i / 4] >> (8 * (i % 4)));
-    uint32_t rcon = 1;
-    for (int i = 8; i < 60; ++i) {
-        uint8_t t[4] = {w[4 * i - 4], w[4 * i - 3], w[4 * i - 2], w[4 * i - 1]};
-        if (i % 8 == 0) {
-            const uint8_t t0 = t[0];
-            t[0] = (uint8_t)(c_sbox.s[t[1]] ^ rcon);
-            t[1] = c_sbox.s[t[2]];
-            t[2] = c_sbox.s[t[3]];
-            t[3] = c_sbox.s[t0];
-            rcon = xtime(rcon);
-        } else if (i % 8 == 4) {
-            for (int k = 0; k < 4; ++k) t[k] = c_sbox.s[t[k]];
-        }
-        for (int k = 0; k < 4; ++k) w[4 * i + k] = w[4 * i - 32 + k] ^ t[k];
-    }
+    aes256_expand(key, w);
     for (int i = 0; i < 240; ++i) rk[i] = w[i];
     uint8_t z[16] = {}, o[16];
     aes256_encrypt(w, z, o);
@@ -236,8 +164,6 @@ struct GcmArgs {
     uint64_t P;
 };
 
-__device__ __forceinline__ uint4 u4_xor(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
-
 // a * H^(p+1) from the LDS tables T = s_gh[p] ([32][16] entries): per input dword 8 lookups in flight, folded
 // in with 3-input XORs (v_bitop3_b32)
 __device__ __forceinline__ uint4 gh_mul(const uint4 (*T)[16], uint4 a)
@@ -264,44 +190,6 @@ __device__ __forceinline__ uint4 gh_mul(const uint4 (*T)[16], uint4 a)
         }
     }
     return make_uint4(r0, r1, r2, r3);
-}
-
-typedef unsigned int u32x4n __attribute__((ext_vector_type(4)));
-
-// 16 bytes at byte address a of a dword-aligned buffer of lim32 dwords (zero past it)
-__device__ __forceinline__ uint4 load16(const uint32_t *b32, uint64_t lim32, uint64_t a)
-{
-    const uint64_t w = a >> 2;
-    uint32_t d[5];
-    if (w + 5 <= lim32) {
-        uint4 q;
-        if (KFEC_GCM_NT) {
-            const u32x4n v = __builtin_nontemporal_load(reinterpret_cast<const u32x4n *>(b32 + w));
-            q = make_uint4(v.x, v.y, v.z, v.w);
-        } else {
-            q = *reinterpret_cast<const uint4 *>(b32 + w);
-        }
-        d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
-        d[4] = KFEC_GCM_NT ? __builtin_nontemporal_load(b32 + w + 4) : b32[w + 4];
-    } else {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) d[i] = w + i < lim32 ? b32[w + i] : 0u;
-    }
-    const uint32_t sh = (uint32_t)(a & 3u);
-    return make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], sh), __builtin_amdgcn_alignbyte(d[2], d[1], sh),
-                      __builtin_amdgcn_alignbyte(d[3], d[2], sh), __builtin_amdgcn_alignbyte(d[4], d[3], sh));
-}
-
-// keep the first rem bytes (0 < rem < 16)
-__device__ __forceinline__ uint4 mask16(uint4 v, uint32_t rem)
-{
-    uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int k = (int)rem - 4 * i;
-        d[i] = k >= 4 ? d[i] : k <= 0 ? 0u : d[i] & ((1u << (8 * k)) - 1u);
-    }
-    return make_uint4(d[0], d[1], d[2], d[3]);
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -400,11 +288,7 @@ __global__ void __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(
                 x = OPEN ? in : out;
                 uint32_t *d32 = reinterpret_cast<uint32_t *>(dst + qb);
                 if (rem >= 16) {
-                    if (KFEC_GCM_NT) {
-                        u32x4n v = {out.x, out.y, out.z, out.w};
-                        __builtin_nontemporal_store(v, reinterpret_cast<u32x4n *>(d32));
-                    }
-                    else *reinterpret_cast<uint4 *>(d32) = out;
+                    *reinterpret_cast<uint4 *>(d32) = out;
                 } else {
                     const uint32_t o4[4] = {out.x, out.y, out.z, out.w};
                     // open: whole dwords (the zero pad is part of the output); seal: bytes below n only
@@ -517,9 +401,10 @@ int gcm_setup(kfec_aead *k, const uint32_t *d_key)
 
 void gcm_free(kfec_aead *k)
 {
-    for (void *p : {(void *)k->d_rk, (void *)k->d_h, (void *)k->d_gh, (void *)k->d_ivt, (void *)k->d_ks})
+    for (void *p : {(void *)k->d_rk, (void *)k->d_h, (void *)k->d_gh, (void *)k->d_ivt, (void *)k->d_ks,
+                    (void *)k->d_ocb})
         if (p) (void)hipFree(p);
-    k->d_rk = k->d_h = k->d_gh = k->d_ivt = k->d_ks = nullptr;
+    k->d_rk = k->d_h = k->d_gh = k->d_ivt = k->d_ks = k->d_ocb = nullptr;
 }
 
 int launch_gcm(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,

@@ -108,11 +108,16 @@ struct kfec_aead {
     uint8_t *d_ivt = nullptr;    //   per iv: J0, E_K(J0)
     uint8_t *d_ks = nullptr;     //   per iv: the first ks_bytes of CTR keystream
     uint32_t ks_bytes = 0;
+    uint8_t *d_ocb = nullptr;    // aes_ocb (kfec_ocb.hip): round keys, L values, AD hash, T-tables; d_ivt: Offset_0
 };
 
 namespace kfec {
 int gcm_setup(kfec_aead *k, const uint32_t *d_key);
-void gcm_free(kfec_aead *k);
+void gcm_free(kfec_aead *k);  // every AES-mode table (gcm and ocb)
+int ocb_setup(kfec_aead *k, const uint32_t *d_key);
+int launch_ocb(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
+               const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
+               hipStream_t s);
 int launch_gcm(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
                const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
                hipStream_t s);

@@ -1,0 +1,441 @@
+// kfec_ocb.hip -- kcptube's aes_ocb packet mode as gfx950 kernels (include/kfec_aead.h).
+//
+// encrypt_data / decrypt_data (data_operations.cpp:171-234, 373-435) over encrypt_decrypt<aes_256_ocb>
+// (aead.hpp:314-400): Botan "AES-256/OCB" (RFC 7253, 128-bit tag) with kcptube's 12-byte nonce (iv_raw
+// repeated 6 times); packet = C || tag || iv_raw; AD "KCP PortHopping" (aead.hpp:16).
+//
+// OCB enciphers every data block (C_i = Offset_i xor E_K(P_i xor Offset_i)), so unlike CTR the block cipher
+// cannot be tabulated; what the key and the 16-bit iv_raw alone determine is: L_*, L_$, L_0..L_31, the hash of
+// the fixed AD (HASH(K, A) = E_K((A || 0x80 || 0^) xor L_*), one block since |A| = 15) -- per key -- and
+// Offset_0 -- per iv, a 1 MiB table.  Block i's offset has a closed form, Offset_i = Offset_0 xor XOR of L_j
+// over the set bits j of gray(i) = i xor (i >> 1), so the blocks of a packet are independent: a row of 8
+// lanes per packet, lane j taking blocks j + 1, j + 9, ...; the checksum is the row's XOR of the plaintext
+// blocks, and one lane enciphers the tag.  AES runs from T-tables in LDS (Te0..Te3, and Td0..Td3 + the
+// inverse S-box for open's full blocks, the equivalent inverse cipher of FIPS 197 5.3.5), 8.5 / 13 KiB per
+// workgroup, with the round keys in LDS too (broadcast reads).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../../include/kfec_aead.h"
+#include "kfec_aes.hpp"
+#include "kfec_gf.hpp"
+#include "kfec_internal.hpp"
+#include "kfec_pkt.hpp"
+
+namespace kfec {
+
+namespace {
+
+// per-key record (ocb_key_kernel), 16-byte aligned pieces
+struct OcbKey {
+    uint4 rk[15];    // encryption round keys
+    uint4 dk[15];    // decryption round keys of the equivalent inverse cipher
+    uint4 lstar;     // L_* = E_K(0)
+    uint4 ldollar;   // L_$ = double(L_*)
+    uint4 l[32];     // L_0 = double(L_$), L_j = double(L_(j-1))
+    uint4 sad;       // HASH(K, "KCP PortHopping")
+    uint32_t te[4][256];
+    uint32_t td[4][256];
+    uint32_t isb[256];
+};
+
+__device__ __forceinline__ uint32_t gmul8(uint32_t a, uint32_t b)
+{
+    uint32_t r = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1u) r ^= a;
+        a = xtime(a);
+        b >>= 1;
+    }
+    return r;
+}
+
+__device__ __forceinline__ uint32_t pack4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3)
+{
+    return b0 | b1 << 8 | b2 << 16 | b3 << 24;
+}
+
+__device__ __forceinline__ uint4 bytes_to_u4(const uint8_t (&b)[16])
+{
+    return make_uint4(pack4(b[0], b[1], b[2], b[3]), pack4(b[4], b[5], b[6], b[7]), pack4(b[8], b[9], b[10], b[11]),
+                      pack4(b[12], b[13], b[14], b[15]));
+}
+
+__device__ __forceinline__ void u4_to_bytes(uint4 v, uint8_t (&b)[16])
+{
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (int i = 0; i < 16; ++i) b[i] = (uint8_t)(w[i / 4] >> (8 * (i % 4)));
+}
+
+// double(S) of RFC 7253: S << 1, xor 0x87 into the last byte when the first bit was set
+__device__ void ocb_double(uint8_t (&s)[16])
+{
+    const uint32_t msb = s[0] >> 7;
+    for (int i = 0; i < 15; ++i) s[i] = (uint8_t)((s[i] << 1) | (s[i + 1] >> 7));
+    s[15] = (uint8_t)((s[15] << 1) ^ (msb ? 0x87u : 0u));
+}
+
+// T-tables and inverse S-box: one workgroup of 256 threads, thread = byte value
+__global__ void ocb_tables_kernel(OcbKey *k)
+{
+    const uint32_t x = threadIdx.x;
+    if (blockIdx.x || x >= 256) return;
+    const uint32_t s = c_sbox.s[x];
+    k->te[0][x] = pack4(xtime(s), s, s, xtime(s) ^ s);
+    k->te[1][x] = pack4(xtime(s) ^ s, xtime(s), s, s);
+    k->te[2][x] = pack4(s, xtime(s) ^ s, xtime(s), s);
+    k->te[3][x] = pack4(s, s, xtime(s) ^ s, xtime(s));
+    k->isb[s] = x;
+    __syncthreads();
+    const uint32_t is = k->isb[x];
+    const uint32_t e = gmul8(is, 14), n9 = gmul8(is, 9), d = gmul8(is, 13), b = gmul8(is, 11);
+    k->td[0][x] = pack4(e, n9, d, b);
+    k->td[1][x] = pack4(b, e, n9, d);
+    k->td[2][x] = pack4(d, b, e, n9);
+    k->td[3][x] = pack4(n9, d, b, e);
+}
+
+// key schedule, the decryption round keys, L values and the AD hash: one thread
+__global__ void ocb_key_kernel(const uint32_t *key, OcbKey *k)
+{
+    if (blockIdx.x || threadIdx.x) return;
+    uint8_t w[240];
+    aes256_expand(key, w);
+    for (int r = 0; r < 15; ++r) {
+        uint8_t b[16];
+        for (int i = 0; i < 16; ++i) b[i] = w[16 * r + i];
+        k->rk[r] = bytes_to_u4(b);
+        // dk[r] = InvMixColumns(rk[14 - r]) for 0 < r < 14, the end keys unchanged
+        for (int i = 0; i < 16; ++i) b[i] = w[16 * (14 - r) + i];
+        if (r > 0 && r < 14) {
+            uint8_t m[16];
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t a0 = b[4 * c], a1 = b[4 * c + 1], a2 = b[4 * c + 2], a3 = b[4 * c + 3];
+                m[4 * c] = (uint8_t)(gmul8(a0, 14) ^ gmul8(a1, 11) ^ gmul8(a2, 13) ^ gmul8(a3, 9));
+                m[4 * c + 1] = (uint8_t)(gmul8(a0, 9) ^ gmul8(a1, 14) ^ gmul8(a2, 11) ^ gmul8(a3, 13));
+                m[4 * c + 2] = (uint8_t)(gmul8(a0, 13) ^ gmul8(a1, 9) ^ gmul8(a2, 14) ^ gmul8(a3, 11));
+                m[4 * c + 3] = (uint8_t)(gmul8(a0, 11) ^ gmul8(a1, 13) ^ gmul8(a2, 9) ^ gmul8(a3, 14));
+            }
+            for (int i = 0; i < 16; ++i) b[i] = m[i];
+        }
+        k->dk[r] = bytes_to_u4(b);
+    }
+    uint8_t z[16] = {}, ls[16], t[16];
+    aes256_encrypt(w, z, ls);  // L_*
+    k->lstar = bytes_to_u4(ls);
+    for (int i = 0; i < 16; ++i) t[i] = ls[i];
+    ocb_double(t);  // L_$
+    k->ldollar = bytes_to_u4(t);
+    for (int j = 0; j < 32; ++j) {
+        ocb_double(t);
+        k->l[j] = bytes_to_u4(t);
+    }
+    // HASH(K, A) for the 15-byte AD: no full block; E_K((A || 0x80) xor L_*)
+    const char *ad = "KCP PortHopping";
+    uint8_t in[16], o[16];
+    for (int i = 0; i < 16; ++i) in[i] = (uint8_t)((i < 15 ? (uint8_t)ad[i] : 0x80u) ^ ls[i]);
+    aes256_encrypt(w, in, o);
+    k->sad = bytes_to_u4(o);
+}
+
+// Offset_0 of every iv (RFC 7253 4.2, TAGLEN 128, 12-byte nonce): one thread per iv
+__global__ void ocb_iv_kernel(const uint32_t *key, uint4 *off0)
+{
+    const uint32_t iv = blockIdx.x * blockDim.x + threadIdx.x;
+    if (iv >= 65536u) return;
+    uint8_t w[240];
+    aes256_expand(key, w);
+    uint8_t nonce[16] = {0, 0, 0, 1};
+    for (int i = 4; i < 16; ++i) nonce[i] = (uint8_t)(i % 2 ? iv >> 8 : iv);  // iv_raw (little-endian) x 6
+    const uint32_t bottom = nonce[15] & 0x3Fu;
+    nonce[15] &= 0xC0u;
+    uint8_t ktop[16];
+    aes256_encrypt(w, nonce, ktop);
+    uint64_t hi = 0, lo = 0;
+    for (int i = 0; i < 8; ++i) {
+        hi = hi << 8 | ktop[i];
+        lo = lo << 8 | ktop[8 + i];
+    }
+    // Stretch = Ktop || (Ktop[1..64] xor Ktop[9..72]); Offset_0 = Stretch[1 + bottom .. 128 + bottom]
+    const uint64_t x = hi ^ (hi << 8 | lo >> 56);
+    uint64_t oh = hi, ol = lo;
+    if (bottom) {
+        oh = hi << bottom | lo >> (64 - bottom);
+        ol = lo << bottom | x >> (64 - bottom);
+    }
+    uint8_t o[16];
+    for (int i = 0; i < 8; ++i) {
+        o[i] = (uint8_t)(oh >> (56 - 8 * i));
+        o[8 + i] = (uint8_t)(ol >> (56 - 8 * i));
+    }
+    off0[iv] = bytes_to_u4(o);
+}
+
+// ---- per-packet kernel -------------------------------------------------------------------------------
+constexpr int kRow = 8;
+constexpr int kOcbBlock = 256;
+constexpr int kRowsPerBlock = kOcbBlock / kRow;
+
+struct OcbArgs {
+    const uint32_t *src;
+    uint64_t src_dw;
+    const uint64_t *off;
+    const uint32_t *len;
+    const uint16_t *iv;
+    uint8_t *dst;
+    uint64_t dst_pitch;
+    uint32_t *out_len;
+    uint8_t *ok;
+    const OcbKey *key;
+    const uint4 *off0;
+    uint64_t P;
+};
+
+// what one workgroup stages into LDS
+struct OcbLds {
+    uint4 rk[15];
+    uint4 dk[15];
+    uint4 l[32];
+    uint32_t te[4][256];
+    uint32_t td[4][256];
+    uint32_t isb[256];
+};
+
+__device__ __forceinline__ uint32_t b0(uint32_t x) { return x & 0xFFu; }
+__device__ __forceinline__ uint32_t b1(uint32_t x) { return (x >> 8) & 0xFFu; }
+__device__ __forceinline__ uint32_t b2(uint32_t x) { return (x >> 16) & 0xFFu; }
+__device__ __forceinline__ uint32_t b3(uint32_t x) { return x >> 24; }
+
+__device__ __forceinline__ uint4 aes_enc(const OcbLds &t, uint4 in)
+{
+    uint32_t s0 = in.x ^ t.rk[0].x, s1 = in.y ^ t.rk[0].y, s2 = in.z ^ t.rk[0].z, s3 = in.w ^ t.rk[0].w;
+#pragma unroll 1
+    for (int r = 1; r < 14; ++r) {
+        const uint4 k = t.rk[r];
+        const uint32_t t0 = xor3(t.te[0][b0(s0)], t.te[1][b1(s1)], t.te[2][b2(s2)]) ^ xor3(t.te[3][b3(s3)], k.x, 0u);
+        const uint32_t t1 = xor3(t.te[0][b0(s1)], t.te[1][b1(s2)], t.te[2][b2(s3)]) ^ xor3(t.te[3][b3(s0)], k.y, 0u);
+        const uint32_t t2 = xor3(t.te[0][b0(s2)], t.te[1][b1(s3)], t.te[2][b2(s0)]) ^ xor3(t.te[3][b3(s1)], k.z, 0u);
+        const uint32_t t3 = xor3(t.te[0][b0(s3)], t.te[1][b1(s0)], t.te[2][b2(s1)]) ^ xor3(t.te[3][b3(s2)], k.w, 0u);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    // last round: S-box only (S(x) is byte 0 of Te2, byte 1 of Te3, byte 2 of Te0, byte 3 of Te1)
+    const uint4 k = t.rk[14];
+    const uint32_t o0 = (t.te[2][b0(s0)] & 0xFFu) | (t.te[3][b1(s1)] & 0xFF00u) | (t.te[0][b2(s2)] & 0xFF0000u) |
+                        (t.te[1][b3(s3)] & 0xFF000000u);
+    const uint32_t o1 = (t.te[2][b0(s1)] & 0xFFu) | (t.te[3][b1(s2)] & 0xFF00u) | (t.te[0][b2(s3)] & 0xFF0000u) |
+                        (t.te[1][b3(s0)] & 0xFF000000u);
+    const uint32_t o2 = (t.te[2][b0(s2)] & 0xFFu) | (t.te[3][b1(s3)] & 0xFF00u) | (t.te[0][b2(s0)] & 0xFF0000u) |
+                        (t.te[1][b3(s1)] & 0xFF000000u);
+    const uint32_t o3 = (t.te[2][b0(s3)] & 0xFFu) | (t.te[3][b1(s0)] & 0xFF00u) | (t.te[0][b2(s1)] & 0xFF0000u) |
+                        (t.te[1][b3(s2)] & 0xFF000000u);
+    return make_uint4(o0 ^ k.x, o1 ^ k.y, o2 ^ k.z, o3 ^ k.w);
+}
+
+__device__ __forceinline__ uint4 aes_dec(const OcbLds &t, uint4 in)
+{
+    uint32_t s0 = in.x ^ t.dk[0].x, s1 = in.y ^ t.dk[0].y, s2 = in.z ^ t.dk[0].z, s3 = in.w ^ t.dk[0].w;
+#pragma unroll 1
+    for (int r = 1; r < 14; ++r) {
+        const uint4 k = t.dk[r];
+        // InvShiftRows: output column c row r takes input column c - r
+        const uint32_t t0 = xor3(t.td[0][b0(s0)], t.td[1][b1(s3)], t.td[2][b2(s2)]) ^ xor3(t.td[3][b3(s1)], k.x, 0u);
+        const uint32_t t1 = xor3(t.td[0][b0(s1)], t.td[1][b1(s0)], t.td[2][b2(s3)]) ^ xor3(t.td[3][b3(s2)], k.y, 0u);
+        const uint32_t t2 = xor3(t.td[0][b0(s2)], t.td[1][b1(s1)], t.td[2][b2(s0)]) ^ xor3(t.td[3][b3(s3)], k.z, 0u);
+        const uint32_t t3 = xor3(t.td[0][b0(s3)], t.td[1][b1(s2)], t.td[2][b2(s1)]) ^ xor3(t.td[3][b3(s0)], k.w, 0u);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint4 k = t.dk[14];
+    const uint32_t o0 = t.isb[b0(s0)] | t.isb[b1(s3)] << 8 | t.isb[b2(s2)] << 16 | t.isb[b3(s1)] << 24;
+    const uint32_t o1 = t.isb[b0(s1)] | t.isb[b1(s0)] << 8 | t.isb[b2(s3)] << 16 | t.isb[b3(s2)] << 24;
+    const uint32_t o2 = t.isb[b0(s2)] | t.isb[b1(s1)] << 8 | t.isb[b2(s0)] << 16 | t.isb[b3(s3)] << 24;
+    const uint32_t o3 = t.isb[b0(s3)] | t.isb[b1(s2)] << 8 | t.isb[b2(s1)] << 16 | t.isb[b3(s0)] << 24;
+    return make_uint4(o0 ^ k.x, o1 ^ k.y, o2 ^ k.z, o3 ^ k.w);
+}
+
+// Offset_i = Offset_0 xor XOR_{j in gray(i)} L_j
+__device__ __forceinline__ uint4 ocb_offset(const OcbLds &t, uint4 o0, uint32_t i)
+{
+    uint32_t g = i ^ (i >> 1);
+    while (g) {
+        o0 = u4_xor(o0, t.l[__builtin_ctz(g)]);
+        g &= g - 1;
+    }
+    return o0;
+}
+
+template <bool OPEN>
+__global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
+{
+    __shared__ OcbLds s;
+    {
+        // stage the round keys, L values and tables (open also needs the decryption half)
+        const uint32_t *k32 = reinterpret_cast<const uint32_t *>(a.key);
+        uint32_t *s32 = reinterpret_cast<uint32_t *>(&s);
+        constexpr int kKeys = (int)(offsetof(OcbLds, te) / 4);
+        for (int i = threadIdx.x; i < kKeys; i += kOcbBlock) {
+            // OcbLds: rk, dk, l -- OcbKey: rk, dk, lstar, ldollar, l
+            const int src = i < 120 ? i : i + 8;
+            s32[i] = k32[src];
+        }
+        const int nt = OPEN ? 4 * 256 + 4 * 256 + 256 : 4 * 256;
+        const uint32_t *kt = reinterpret_cast<const uint32_t *>(&a.key->te[0][0]);
+        for (int i = threadIdx.x; i < nt; i += kOcbBlock) s32[kKeys + i] = kt[i];
+        __syncthreads();
+    }
+    const uint4 lstar = a.key->lstar, ldollar = a.key->ldollar, sad = a.key->sad;
+    const uint32_t lane = threadIdx.x % kRow;
+    for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRow; p < a.P;
+         p += (uint64_t)gridDim.x * kRowsPerBlock) {
+        const uint32_t L = a.len[p];
+        const uint64_t off = a.off[p];
+        uint32_t n, iv, ptag[4] = {0u, 0u, 0u, 0u};
+        if (OPEN) {
+            if (L < KFEC_AEAD_OVERHEAD || L - KFEC_AEAD_OVERHEAD > a.dst_pitch) {
+                if (lane == 0) {
+                    a.out_len[p] = 0;
+                    a.ok[p] = 0;
+                }
+                continue;
+            }
+            n = L - KFEC_AEAD_OVERHEAD;
+            const uint4 tg = load16(a.src, a.src_dw, off + n);
+            ptag[0] = tg.x; ptag[1] = tg.y; ptag[2] = tg.z; ptag[3] = tg.w;
+            iv = load16(a.src, a.src_dw, off + n + 16).x & 0xFFFFu;
+        } else {
+            if (L == 0 || (uint64_t)L + KFEC_AEAD_OVERHEAD > a.dst_pitch) {  // "empty data" / no room
+                if (lane == 0) a.out_len[p] = 0;
+                continue;
+            }
+            n = L;
+            iv = a.iv[p];
+        }
+        const uint4 o0 = a.off0[iv];
+        const uint32_t m = n / 16, rem = n % 16, nblk = m + (rem ? 1u : 0u);
+        uint8_t *dst = a.dst + p * a.dst_pitch;
+        uint4 sum = make_uint4(0u, 0u, 0u, 0u);
+        for (uint32_t i = 1 + lane; i <= nblk; i += kRow) {  // 1-based block index
+            const uint32_t qb = 16 * (i - 1);
+            uint4 in = load16(a.src, a.src_dw, off + qb);
+            uint32_t *d32 = reinterpret_cast<uint32_t *>(dst + qb);
+            if (i <= m) {
+                const uint4 oi = ocb_offset(s, o0, i);
+                uint4 out;
+                if (OPEN) {
+                    out = u4_xor(aes_dec(s, u4_xor(in, oi)), oi);
+                    sum = u4_xor(sum, out);
+                } else {
+                    out = u4_xor(aes_enc(s, u4_xor(in, oi)), oi);
+                    sum = u4_xor(sum, in);
+                }
+                *reinterpret_cast<uint4 *>(d32) = out;
+            } else {  // the partial last block: Pad = E_K(Offset_m xor L_*)
+                const uint4 pad = aes_enc(s, u4_xor(ocb_offset(s, o0, m), lstar));
+                in = mask16(in, rem);
+                const uint4 out = mask16(u4_xor(in, pad), rem);
+                uint4 pt = OPEN ? out : in;
+                uint32_t w[4] = {pt.x, pt.y, pt.z, pt.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) w[q] |= (uint32_t)q == rem / 4 ? 0x80u << (8 * (rem % 4)) : 0u;
+                sum = u4_xor(sum, make_uint4(w[0], w[1], w[2], w[3]));
+                const uint32_t o4[4] = {out.x, out.y, out.z, out.w};
+                // open: whole dwords (the zero pad is part of the output); seal: bytes below n only
+                const uint32_t nd = OPEN ? (rem + 3) / 4 : rem / 4;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if ((uint32_t)q < nd) d32[q] = o4[q];
+                if (!OPEN && (rem & 3)) {
+                    uint8_t *bp = dst + qb + 4 * (rem / 4);
+                    for (uint32_t q = 0; q < (rem & 3); ++q) bp[q] = (uint8_t)(o4[rem / 4] >> (8 * q));
+                }
+            }
+        }
+#pragma unroll
+        for (int d = 1; d < kRow; d <<= 1) {
+            sum.x ^= __shfl_xor(sum.x, d, kRow);
+            sum.y ^= __shfl_xor(sum.y, d, kRow);
+            sum.z ^= __shfl_xor(sum.z, d, kRow);
+            sum.w ^= __shfl_xor(sum.w, d, kRow);
+        }
+        // Tag = E_K(Checksum xor Offset xor L_$) xor HASH(K, A), Offset = Offset_m (xor L_* after a partial block)
+        uint4 fo = ocb_offset(s, o0, m);
+        if (rem) fo = u4_xor(fo, lstar);
+        uint4 tg = make_uint4(0u, 0u, 0u, 0u);
+        if (lane == 0) tg = u4_xor(aes_enc(s, u4_xor(u4_xor(sum, fo), ldollar)), sad);
+        const uint32_t tag[4] = {__shfl(tg.x, 0, kRow), __shfl(tg.y, 0, kRow), __shfl(tg.z, 0, kRow),
+                                 __shfl(tg.w, 0, kRow)};
+        if (OPEN) {
+            const bool good = tag[0] == ptag[0] && tag[1] == ptag[1] && tag[2] == ptag[2] && tag[3] == ptag[3];
+            if (!good) {  // no unauthenticated plaintext leaves the kernel
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);
+                const uint32_t nd = (n + 3) / 4;
+                for (uint32_t i = lane; i < nd; i += kRow) d32[i] = 0u;
+            }
+            if (lane == 0) {
+                a.out_len[p] = good ? n : 0u;
+                a.ok[p] = good ? 1 : 0;
+            }
+        } else {
+            // tag || iv_raw || zeros to the next multiple of 4: bytes n .. n + 21, 3 per lane
+            const uint32_t end = (n + KFEC_AEAD_OVERHEAD + 3) & ~3u;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const uint32_t i = 3 * lane + q;
+                if (n + i < end) {
+                    const uint32_t w = i < 4 ? tag[0] : i < 8 ? tag[1] : i < 12 ? tag[2] : i < 16 ? tag[3] : iv;
+                    dst[n + i] = (uint8_t)(i < 18 ? (w >> (8 * (i & 3))) & 0xFFu : 0u);
+                }
+            }
+            if (lane == 0) a.out_len[p] = n + KFEC_AEAD_OVERHEAD;
+        }
+    }
+}
+
+}  // namespace
+
+int ocb_setup(kfec_aead *k, const uint32_t *d_key)
+{
+    if (hipMalloc(&k->d_ocb, sizeof(OcbKey)) != hipSuccess || hipMalloc(&k->d_ivt, 65536 * 16) != hipSuccess)
+        return KFEC_ENOMEM;
+    OcbKey *ok = reinterpret_cast<OcbKey *>(k->d_ocb);
+    hipLaunchKernelGGL(ocb_key_kernel, dim3(1), dim3(64), 0, nullptr, d_key, ok);
+    hipLaunchKernelGGL(ocb_tables_kernel, dim3(1), dim3(256), 0, nullptr, ok);
+    hipLaunchKernelGGL(ocb_iv_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, d_key,
+                       reinterpret_cast<uint4 *>(k->d_ivt));
+    return hipGetLastError() == hipSuccess ? KFEC_OK : KFEC_EHIP;
+}
+
+int launch_ocb(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
+               const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
+               hipStream_t s)
+{
+    if (P == 0) return 0;
+    OcbArgs a{};
+    a.src = static_cast<const uint32_t *>(src);
+    a.src_dw = (src_bytes + 3) / 4;
+    a.off = off;
+    a.len = len;
+    a.iv = iv;
+    a.dst = static_cast<uint8_t *>(dst);
+    a.dst_pitch = dst_pitch;
+    a.out_len = out_len;
+    a.ok = ok;
+    a.key = reinterpret_cast<const OcbKey *>(k->d_ocb);
+    a.off0 = reinterpret_cast<const uint4 *>(k->d_ivt);
+    a.P = P;
+    static int cus = [] {
+        int d = 0, n = 0;
+        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) !=
+                                                  hipSuccess)
+            n = 256;
+        return std::max(n, 1);
+    }();
+    const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
+    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * 8));
+    if (open) hipLaunchKernelGGL(ocb_kernel<true>, grid, dim3(kOcbBlock), 0, s, a);
+    else hipLaunchKernelGGL(ocb_kernel<false>, grid, dim3(kOcbBlock), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace kfec

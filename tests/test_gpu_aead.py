@@ -1,4 +1,4 @@
-"""GPU parity tests of kcptube's aes_gcm / chacha20 / xchacha20 packet modes (include/kfec_aead.h) against
+"""GPU parity tests of kcptube's aes_gcm / aes_ocb / chacha20 / xchacha20 packet modes (include/kfec_aead.h) against
 oracle/aead_oracle.py (pinned against OpenSSL's libcrypto in tests/test_aead_oracle.py).
 
 Bar: bit-exact sealed packets (ciphertext || tag || iv_raw) for every length class the kernels treat
@@ -6,7 +6,7 @@ differently -- lengths around the 16-byte MAC block, the 64-byte ChaCha20 block 
 round, with the MAC header (23 or 16 bytes) and trailer crossing chunk boundaries, and for aes_gcm past the
 2048 bytes of tabulated keystream -- at unaligned source offsets; opening restores the plaintext, and any flipped bit (ciphertext, tag or iv_raw) fails with zeroed
 output.  A 20k-packet batch is checked against libcrypto's ChaCha20 / Poly1305 / ChaCha20-Poly1305 /
-AES-256-GCM (the pure-Python oracle is too slow for it), and a 1M-packet batch round-trips on the device.
+AES-256-GCM / AES-256-OCB (the pure-Python oracle is too slow for it), and a 1M-packet batch round-trips on the device.
 """
 from __future__ import annotations
 
@@ -24,7 +24,7 @@ torch = pytest.importorskip("torch")
 from oracle import aead_oracle as ao  # noqa: E402
 from oracle import libcrypto as lc  # noqa: E402
 
-MODES = ("chacha20", "xchacha20", "aes_gcm")
+MODES = ("chacha20", "xchacha20", "aes_gcm", "aes_ocb")
 PW = b"kcptube aead test password"
 LENGTHS = ([1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 23, 24, 25, 31, 32, 33, 40, 41, 42, 47, 48, 49, 55, 56, 57, 63, 64,
             65, 100, 127, 128, 129, 191, 192, 193, 255, 256, 257, 447, 448, 449, 489, 490, 495, 496, 497, 511, 512,
@@ -98,7 +98,7 @@ def test_refuses_empty_password_and_other_modes(dev):
     with pytest.raises(ValueError):
         AeadCipher("chacha20", b"")
     with pytest.raises(ValueError):
-        AeadCipher(5, PW)  # aes_ocb: not provided by the GPU library
+        AeadCipher(3, PW)  # plain_xor: not an AEAD mode (kfec_seal_batch has it)
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -164,7 +164,9 @@ def test_lengths_the_reference_refuses(dev, mode):
     assert list(out) == [0, 21, 0]
     assert bytes(dst[1, :21]) == ao.aead_seal(mode, PW, b"abc", 2)
     key, nonce = ao.derive_key(PW), ao.nonce(mode, 9)
-    body = ao.gcm_seal(key, nonce, ao.AD, b"") if mode == "aes_gcm" else ao.chacha20poly1305_seal(key, nonce, ao.AD, b"")
+    body = (ao.gcm_seal(key, nonce, ao.AD, b"") if mode == "aes_gcm" else
+            ao.ocb_seal(key, nonce, ao.AD, b"") if mode == "aes_ocb" else
+            ao.chacha20poly1305_seal(key, nonce, ao.AD, b""))
     empty_ok = body + struct.pack("<H", 9)
     pkts = [bytes(n) for n in range(18)] + [empty_ok]
     _, out, ok = _open(c, pkts, dev)
@@ -181,6 +183,8 @@ def _libcrypto_seal(mode, key, pt, iv):
     n = ao.nonce(mode, iv)
     if mode == "aes_gcm":
         return lc.evp_seal("EVP_aes_256_gcm", key, n, ao.AD, pt) + struct.pack("<H", iv)
+    if mode == "aes_ocb":
+        return lc.evp_seal("EVP_aes_256_ocb", key, n, ao.AD, pt) + struct.pack("<H", iv)
     if mode == "chacha20":
         polykey = lc.evp_chacha20(key, bytes(8) + n, bytes(32))
         ct = lc.evp_chacha20(key, struct.pack("<II", 1, 0) + n, pt)

@@ -61,10 +61,10 @@ def main():
     ok = torch.empty(P, dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream()
     e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    res = {"metric": "AEAD packet seal/open GB/s of plaintext (chacha20 / xchacha20 / aes_gcm modes, device-resident)",
+    res = {"metric": "AEAD packet seal/open GB/s of plaintext (chacha20 / xchacha20 / aes_gcm / aes_ocb modes, device-resident)",
            "packets": P, "len": L}
     good = True
-    for name in ("chacha20", "xchacha20", "aes_gcm"):
+    for name in ("chacha20", "xchacha20", "aes_gcm", "aes_ocb"):
         c = AeadCipher(name, b"kcptube bench password")
         ts, to = [], []
         for i in range(args.steps + 2):

@@ -9,7 +9,7 @@ for round in 1 2; do
 for v in base $(cd kcptube_amd/variants && ls libkfec_aead_*.so | sed 's/libkfec_//; s/\.so//'); do
   lib=""; [ "$v" != base ] && lib=kcptube_amd/variants/libkfec_$v.so
   KFEC_LIB=$lib timeout -k 10 300 python -u tools/bench_aead.py --steps 5 --no-verify > $out/bench_$v.json 2>$out/bench_$v.err || { tail $out/bench_$v.err; exit 1; }
-  python3 -c "import json,sys; d=json.load(open('$out/bench_$v.json')); print('$round %-16s' % '$v', ' '.join('%s %.3f/%.3f' % (m, d[m]['seal_ms'], d[m]['open_ms']) for m in ('chacha20','xchacha20','aes_gcm') if m in d), 'ok' if d['verified'] else 'WRONG')"
+  python3 -c "import json,sys; d=json.load(open('$out/bench_$v.json')); print('$round %-16s' % '$v', ' '.join('%s %.3f/%.3f' % (m, d[m]['seal_ms'], d[m]['open_ms']) for m in ('chacha20','xchacha20','aes_gcm','aes_ocb') if m in d), 'ok' if d['verified'] else 'WRONG')"
 done
 done
 echo ab-done
