@@ -92,6 +92,12 @@ def build_tools(force: bool = False) -> list[str]:
         subprocess.check_call([_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-result",
                                "-Wno-unused-value", src, "-o", exe])
     out.append(exe)
+    # tools/cpu_aead: the OpenSSL CPU leg of tools/bench_aead.py (skipped where the OpenSSL headers are absent)
+    src = os.path.join(ROOT, "tools", "cpu_aead.c")
+    exe = os.path.join(ROOT, "tools", "cpu_aead")
+    if os.path.exists(src) and os.path.exists("/usr/include/openssl/evp.h") and (force or _stale(exe, [src])):
+        subprocess.check_call(["gcc", "-O2", "-pthread", "-o", exe, src, "-lcrypto"])
+        out.append(exe)
     return out
 
 
