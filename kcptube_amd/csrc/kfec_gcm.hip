@@ -32,14 +32,8 @@ namespace {
 #define KFEC_GCM_KS_BYTES 2048  // keystream bytes tabulated per iv (multiple of 16)
 #endif
 constexpr uint32_t kKsBytes = KFEC_GCM_KS_BYTES;
-#ifndef KFEC_GCM_PF
-#define KFEC_GCM_PF 0  // 1: load round t + 1's keystream and data while round t is hashed (measured: no gain)
-#endif
 #ifndef KFEC_GCM_AB
 #define KFEC_GCM_AB 0  // timing ablations only (wrong output): bit 0 = no GHASH multiplies, bit 1 = no keystream loads
-#endif
-#ifndef KFEC_GCM_DWTAIL
-#define KFEC_GCM_DWTAIL 1  // seal's tail (last partial ciphertext dword, tag, iv_raw, pad) as dword stores
 #endif
 
 // ---- GHASH multiply, bit-serial (setup only): z = x * y in GF(2^128), SP 800-38D 6.3 bit order ---------
@@ -70,18 +64,19 @@ __global__ void gcm_key_kernel(const uint32_t *key, uint8_t *rk, uint8_t *h)
     for (int i = 0; i < 16; ++i) h[i] = o[i];
 }
 
-// Shoup tables of H^1 .. H^4: gh[p][k][v] = (the block whose byte k / 2 is v << 4 (k & 1), zeros elsewhere)
-// * H^(p+1), 16 bytes each; thread per entry
+// Shoup tables of H^(2^p), p = 0..4 (H, H^2, H^4, H^8, H^16): gh[p][k][v] = (the block whose byte k / 2 is
+// v << 4 (k & 1), zeros elsewhere) * H^(2^p), 16 bytes each; thread per entry
+constexpr int kGhTables = 5;
 __global__ void gcm_tables_kernel(const uint8_t *h, uint8_t *gh)
 {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= 4 * 32 * 16) return;
+    if (e >= kGhTables * 32 * 16) return;
     const int p = e / 512, k = (e / 16) % 32, v = e % 16;
-    uint8_t hp[16], hh[16];
-    for (int i = 0; i < 16; ++i) hp[i] = hh[i] = h[i];
-    for (int q = 0; q < p; ++q) {
+    uint8_t hp[16];
+    for (int i = 0; i < 16; ++i) hp[i] = h[i];
+    for (int q = 0; q < p; ++q) {  // square p times
         uint8_t t[16];
-        gf128_mul(hp, hh, t);
+        gf128_mul(hp, hp, t);
         for (int i = 0; i < 16; ++i) hp[i] = t[i];
     }
     uint8_t x[16] = {}, z[16];
@@ -140,9 +135,9 @@ __global__ void gcm_ks_kernel(const uint8_t *rk, const uint8_t *ivt, uint8_t *ks
 }
 
 // ---- the packet kernel ---------------------------------------------------------------------------------
-constexpr int kRow = 4;  // lanes per packet
+constexpr int kRow = 16;  // lanes per packet (16 bytes each: 256 contiguous bytes per row per round)
 #ifndef KFEC_GCM_BLOCK
-#define KFEC_GCM_BLOCK 256
+#define KFEC_GCM_BLOCK 512  // 32 packets per workgroup share one LDS copy of the 40 KiB of tables
 #endif
 constexpr int kGcmBlock = KFEC_GCM_BLOCK;
 constexpr int kRowsPerBlock = kGcmBlock / kRow;
@@ -168,18 +163,20 @@ struct GcmArgs {
 // in with 3-input XORs (v_bitop3_b32)
 __device__ __forceinline__ uint4 gh_mul(const uint4 (*T)[16], uint4 a)
 {
-    const uint32_t d[4] = {a.x, a.y, a.z, a.w};
     uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-#pragma unroll
+    // a rolled loop over the input dwords: one dword's 8 lookups (32 VGPRs) in flight, where the unrolled form
+    // let the scheduler hoist all 32 (128 VGPRs) and cost a wave per SIMD
+#pragma unroll 1
     for (int i = 0; i < 4; ++i) {
-        const uint32_t lo = (d[i] << 4) & 0xF0F0F0F0u, hi = d[i] & 0xF0F0F0F0u;  // 16 * nibble per byte
+        const uint32_t d = i == 0 ? a.x : i == 1 ? a.y : i == 2 ? a.z : a.w;
+        const uint32_t lo = (d << 4) & 0xF0F0F0F0u, hi = d & 0xF0F0F0F0u;  // 16 * nibble per byte
+        const uint4(*Ti)[16] = T + 8 * i;
         uint4 e[8];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const int k = 2 * (4 * i + b);
-            e[2 * b] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(T[k]) + ((lo >> (8 * b)) & 0xFFu));
+            e[2 * b] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(Ti[2 * b]) + ((lo >> (8 * b)) & 0xFFu));
             e[2 * b + 1] =
-                *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(T[k + 1]) + ((hi >> (8 * b)) & 0xFFu));
+                *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(Ti[2 * b + 1]) + ((hi >> (8 * b)) & 0xFFu));
         }
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
@@ -194,22 +191,36 @@ __device__ __forceinline__ uint4 gh_mul(const uint4 (*T)[16], uint4 a)
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// keystream block i (i >= 1) computed here, for blocks past the table: out of line, so that its byte arrays do
+// not weigh on the packet loop's registers
+__device__ __noinline__ uint4 ctr_keystream(const uint8_t *rk, const uint8_t *j0, uint32_t i)
+{
+    uint8_t c[16], o[16];
+    ctr_block(j0, i, c);
+    aes256_encrypt(rk, c, o);
+    return make_uint4((uint32_t)o[0] | o[1] << 8 | o[2] << 16 | (uint32_t)o[3] << 24,
+                      (uint32_t)o[4] | o[5] << 8 | o[6] << 16 | (uint32_t)o[7] << 24,
+                      (uint32_t)o[8] | o[9] << 8 | o[10] << 16 | (uint32_t)o[11] << 24,
+                      (uint32_t)o[12] | o[13] << 8 | o[14] << 16 | (uint32_t)o[15] << 24);
+}
+
 #ifndef KFEC_GCM_WPE
-#define KFEC_GCM_WPE 4  // waves per SIMD the register allocation must allow
+#define KFEC_GCM_WPE 6  // waves per SIMD the register allocation must allow
 #endif
 
 template <bool OPEN>
 __global__ void __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(KFEC_GCM_WPE))) gcm_kernel(GcmArgs a)
 {
-    __shared__ uint4 s_gh[4][32][16];  // 32 KiB
+    __shared__ uint4 s_gh[kGhTables][32][16];  // 40 KiB: H, H^2, H^4, H^8, H^16
     {
         uint4 *flat = &s_gh[0][0][0];
-        for (int i = threadIdx.x; i < 4 * 32 * 16; i += kGcmBlock) flat[i] = a.gh[i];
+        for (int i = threadIdx.x; i < kGhTables * 32 * 16; i += kGcmBlock) flat[i] = a.gh[i];
         __syncthreads();
     }
     const uint32_t lane = threadIdx.x % kRow;
     // the AD block: "KCP PortHopping" || 0x00 (aead.hpp:16) as little-endian dwords
     const uint4 ad = make_uint4(0x2050434Bu, 0x74726F50u, 0x70706F48u, 0x00676E69u);
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
     for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRow; p < a.P;
          p += (uint64_t)gridDim.x * kRowsPerBlock) {
         const uint32_t L = a.len[p];
@@ -224,7 +235,7 @@ __global__ void __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(
                 continue;
             }
             n = L - KFEC_AEAD_OVERHEAD;
-            ptag = load16(a.src, a.src_dw, off + n + 4 * lane).x;  // this lane's tag dword
+            ptag = load16(a.src, a.src_dw, off + n + 4 * (lane & 3)).x;  // tag dword lane % 4
             iv = load16(a.src, a.src_dw, off + n + 16).x & 0xFFFFu;
         } else {
             if (L == 0 || (uint64_t)L + KFEC_AEAD_OVERHEAD > a.dst_pitch) {  // "empty data" / no room
@@ -236,51 +247,29 @@ __global__ void __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(
         }
         const uint8_t *ivrow = a.ivt + 32 * (size_t)iv;
         const uint4 *ksrow = reinterpret_cast<const uint4 *>(a.ks + (size_t)iv * kKsBytes);
-        const uint32_t nc = (n + 15) / 16;  // ciphertext blocks
-        const uint32_t NB = nc + 2;         // AD block, ciphertext blocks, length block
-        const uint32_t rounds = (NB + kRow - 1) / kRow;
+        const uint32_t nc = (n + 15) / 16;             // ciphertext blocks
+        const uint32_t NB = nc + 2;                    // AD block, ciphertext blocks, length block
+        const uint32_t pad = (kRow - NB % kRow) % kRow;  // leading zero blocks: the last block lands on lane 15
+        const uint32_t rounds = (NB + pad) / kRow;
         uint8_t *dst = a.dst + p * a.dst_pitch;
-        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
-        int blast = -1;
-        uint32_t ctail = 0;  // seal: the ciphertext's partial last dword (KFEC_GCM_DWTAIL)
-        // keystream (from the table) and packet bytes of round t's block, when it is a ciphertext block
-        auto fetch = [&](uint32_t t, uint4 &ks, uint4 &in) {
-            const uint32_t b = t * kRow + lane;
-            if (b == 0 || b + 1 >= NB) return;
-            const uint32_t q = b - 1;
-            if (16 * q + 16 <= kKsBytes && !(KFEC_GCM_AB & 2)) ks = ksrow[q];
-            in = load16(a.src, a.src_dw, off + 16 * q);
-        };
-        const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-        uint4 cks = zero, cin = zero;
-        if (KFEC_GCM_PF) fetch(0, cks, cin);
+        uint4 acc = zero;
+        uint32_t ctail = 0;  // seal: the ciphertext's partial last dword
         for (uint32_t t = 0; t < rounds; ++t) {
-            const uint32_t b = t * kRow + lane;
-            if (b >= NB) continue;
-            uint4 nks = zero, nin = zero;
-            if (KFEC_GCM_PF) {
-                if (t + 1 < rounds) fetch(t + 1, nks, nin);
-            } else {
-                fetch(t, cks, cin);
-            }
-            uint4 x;
+            const int b = (int)(t * kRow + lane) - (int)pad;  // message block of this lane
+            uint4 x = zero;
             if (b == 0) {
                 x = ad;
-            } else if (b == NB - 1) {  // be64(8 * 15) || be64(8 * n)
+            } else if (b == (int)NB - 1) {  // be64(8 * 15) || be64(8 * n)
                 x = make_uint4(0u, bswap32(120u), bswap32(n >> 29), bswap32(n << 3));
-            } else {
-                const uint32_t q = b - 1, qb = 16 * q;
-                uint4 ks = cks;
-                if (qb + 16 > kKsBytes) {  // past the table: AES of the counter block here
-                    uint8_t c[16], o[16];
-                    ctr_block(ivrow, q + 1, c);
-                    aes256_encrypt(a.rk, c, o);
-                    ks = make_uint4((uint32_t)o[0] | o[1] << 8 | o[2] << 16 | (uint32_t)o[3] << 24,
-                                    (uint32_t)o[4] | o[5] << 8 | o[6] << 16 | (uint32_t)o[7] << 24,
-                                    (uint32_t)o[8] | o[9] << 8 | o[10] << 16 | (uint32_t)o[11] << 24,
-                                    (uint32_t)o[12] | o[13] << 8 | o[14] << 16 | (uint32_t)o[15] << 24);
+            } else if (b > 0 && b < (int)NB - 1) {
+                const uint32_t q = (uint32_t)b - 1, qb = 16 * q;
+                uint4 ks = zero;
+                if (qb + 16 <= kKsBytes) {
+                    if (!(KFEC_GCM_AB & 2)) ks = ksrow[q];
+                } else {  // past the table: AES of the counter block here
+                    ks = ctr_keystream(a.rk, ivrow, q + 1);
                 }
-                uint4 in = cin;
+                uint4 in = load16(a.src, a.src_dw, off + qb);
                 const uint32_t rem = n - qb;  // > 0
                 if (rem < 16) in = mask16(in, rem);
                 uint4 out = u4_xor(in, ks);
@@ -291,46 +280,34 @@ __global__ void __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(
                     *reinterpret_cast<uint4 *>(d32) = out;
                 } else {
                     const uint32_t o4[4] = {out.x, out.y, out.z, out.w};
-                    // open: whole dwords (the zero pad is part of the output); seal: bytes below n only
+                    // open: whole dwords (the zero pad is part of the output); seal: whole dwords below n,
+                    // the last partial dword goes out with the tag
                     const uint32_t nd = OPEN ? (rem + 3) / 4 : rem / 4;
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
                         if ((uint32_t)i < nd) d32[i] = o4[i];
-                    if (!OPEN && (rem & 3)) {
-                        const uint32_t v = o4[rem / 4];
-                        if (KFEC_GCM_DWTAIL) {
-                            ctail = v;  // goes out with the tag, as whole dwords
-                        } else {
-                            uint8_t *bp = dst + qb + 4 * (rem / 4);
-                            for (uint32_t i = 0; i < (rem & 3); ++i) bp[i] = (uint8_t)(v >> (8 * i));
-                        }
-                    }
+                    if (!OPEN && (rem & 3)) ctail = o4[rem / 4];
                 }
             }
-            cks = nks;
-            cin = nin;
-            if (t && !(KFEC_GCM_AB & 1)) acc = gh_mul(s_gh[3], acc);  // * H^4
+            if (t && !(KFEC_GCM_AB & 1)) acc = gh_mul(s_gh[4], acc);  // * H^16
             acc = u4_xor(acc, x);
-            blast = (int)b;
         }
-        // * H^(NB - b_last), then the row's XOR
-        if (blast >= 0) {
-            const int e = (int)NB - blast;  // 1..4
-            acc = gh_mul(s_gh[e - 1], acc);
-        } else {
-            acc = make_uint4(0u, 0u, 0u, 0u);
+        // lane l's accumulator ends on padded block 16 (rounds - 1) + l, so it carries H^(16 - l): fold the 16
+        // lanes pairwise (the earlier lane of a pair of distance d times H^d), then times H
+#pragma unroll 1
+        for (int lv = 0; lv < 4; ++lv) {  // not unrolled: one multiply's 32 lookups in flight at a time
+            const int d = 1 << lv;
+            const uint4 other = make_uint4(__shfl_xor(acc.x, d, kRow), __shfl_xor(acc.y, d, kRow),
+                                           __shfl_xor(acc.z, d, kRow), __shfl_xor(acc.w, d, kRow));
+            const bool earlier = (lane & d) == 0;
+            acc = u4_xor(gh_mul(s_gh[lv], earlier ? acc : other), earlier ? other : acc);
         }
-#pragma unroll
-        for (int d = 1; d < kRow; d <<= 1) {
-            acc.x ^= __shfl_xor(acc.x, d, kRow);
-            acc.y ^= __shfl_xor(acc.y, d, kRow);
-            acc.z ^= __shfl_xor(acc.z, d, kRow);
-            acc.w ^= __shfl_xor(acc.w, d, kRow);
-        }
+        acc = gh_mul(s_gh[0], acc);
         const uint4 mask = *reinterpret_cast<const uint4 *>(ivrow + 16);
         const uint32_t tag[4] = {acc.x ^ mask.x, acc.y ^ mask.y, acc.z ^ mask.z, acc.w ^ mask.w};
         if (OPEN) {
-            const uint32_t mine = lane == 0 ? tag[0] : lane == 1 ? tag[1] : lane == 2 ? tag[2] : tag[3];
+            const uint32_t l4 = lane & 3;
+            const uint32_t mine = l4 == 0 ? tag[0] : l4 == 1 ? tag[1] : l4 == 2 ? tag[2] : tag[3];
             uint32_t bad = mine != ptag ? 1u : 0u;
 #pragma unroll
             for (int d = 1; d < kRow; d <<= 1) bad |= __shfl_xor(bad, d, kRow);
@@ -345,37 +322,20 @@ __global__ void __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(
                 a.ok[p] = bad ? 0 : 1;
             }
         } else {
-            if (KFEC_GCM_DWTAIL) {
-                // dwords from floor4(n): the ciphertext's last n % 4 bytes || tag || iv_raw || zero pad (5 or 6
-                // dwords, lane l writes dwords l and l + 4); the partial dword came from the lane that made it
-                const uint32_t o = n & 3u, n4 = n & ~3u;
-                const uint32_t cp = __shfl(ctail, (int)(nc % kRow), kRow);
-                const uint32_t cnt = (((n + KFEC_AEAD_OVERHEAD + 3u) & ~3u) - n4) / 4u;
-                const uint32_t w[7] = {o ? cp << (8 * (4 - o)) : 0u, tag[0], tag[1], tag[2], tag[3], iv, 0u};
+            // dwords from floor4(n): the ciphertext's last n % 4 bytes || tag || iv_raw || zero pad (5 or 6
+            // dwords, one per lane); the partial dword comes from the lane of ciphertext block nc - 1
+            const uint32_t o = n & 3u, n4 = n & ~3u;
+            const uint32_t cp = __shfl(ctail, (int)((nc + pad) % kRow), kRow);
+            const uint32_t cnt = (((n + KFEC_AEAD_OVERHEAD + 3u) & ~3u) - n4) / 4u;
+            const uint32_t w[7] = {o ? cp << (8 * (4 - o)) : 0u, tag[0], tag[1], tag[2], tag[3], iv, 0u};
+            uint32_t w1 = 0, w0 = 0;
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t l = lane + kRow * h;  // dword index of the tail, 0..7
-                    uint32_t w1 = 0, w0 = 0;
-#pragma unroll
-                    for (int i = 0; i < 6; ++i) {
-                        w1 = l == (uint32_t)i ? w[i + 1] : w1;
-                        w0 = l == (uint32_t)i ? w[i] : w0;
-                    }
-                    const uint32_t v = o ? __builtin_amdgcn_alignbyte(w1, w0, 4 - o) : w1;
-                    if (l < cnt) reinterpret_cast<uint32_t *>(dst + n4)[l] = v;
-                }
-            } else {
-                // tag || iv_raw || zeros to the next multiple of 4: bytes n .. n + 21, 6 per lane
-                const uint32_t end = (n + KFEC_AEAD_OVERHEAD + 3) & ~3u;
-#pragma unroll
-                for (int q = 0; q < 6; ++q) {
-                    const uint32_t i = 6 * lane + q;
-                    if (n + i < end) {
-                        const uint32_t w = i < 4 ? tag[0] : i < 8 ? tag[1] : i < 12 ? tag[2] : i < 16 ? tag[3] : iv;
-                        dst[n + i] = (uint8_t)(i < 18 ? (w >> (8 * (i & 3))) & 0xFFu : 0u);
-                    }
-                }
+            for (int i = 0; i < 6; ++i) {
+                w1 = lane == (uint32_t)i ? w[i + 1] : w1;
+                w0 = lane == (uint32_t)i ? w[i] : w0;
             }
+            const uint32_t v = o ? __builtin_amdgcn_alignbyte(w1, w0, 4 - o) : w1;
+            if (lane < cnt) reinterpret_cast<uint32_t *>(dst + n4)[lane] = v;
             if (lane == 0) a.out_len[p] = n + KFEC_AEAD_OVERHEAD;
         }
     }
@@ -386,12 +346,12 @@ __global__ void __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(
 int gcm_setup(kfec_aead *k, const uint32_t *d_key)
 {
     if (hipMalloc(&k->d_rk, 240) != hipSuccess || hipMalloc(&k->d_h, 16) != hipSuccess ||
-        hipMalloc(&k->d_gh, 4 * 32 * 16 * 16) != hipSuccess || hipMalloc(&k->d_ivt, 65536 * 32) != hipSuccess ||
+        hipMalloc(&k->d_gh, kGhTables * 32 * 16 * 16) != hipSuccess || hipMalloc(&k->d_ivt, 65536 * 32) != hipSuccess ||
         hipMalloc(&k->d_ks, (size_t)65536 * kKsBytes) != hipSuccess)
         return KFEC_ENOMEM;
     k->ks_bytes = kKsBytes;
     hipLaunchKernelGGL(gcm_key_kernel, dim3(1), dim3(64), 0, nullptr, d_key, k->d_rk, k->d_h);
-    hipLaunchKernelGGL(gcm_tables_kernel, dim3(4 * 32 * 16 / 256), dim3(256), 0, nullptr, k->d_h, k->d_gh);
+    hipLaunchKernelGGL(gcm_tables_kernel, dim3(kGhTables * 32 * 16 / 256), dim3(256), 0, nullptr, k->d_h, k->d_gh);
     hipLaunchKernelGGL(gcm_iv_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, k->d_rk, k->d_h, k->d_ivt);
     const uint64_t ks_threads = 65536ull * (kKsBytes / 16);
     hipLaunchKernelGGL(gcm_ks_kernel, dim3((uint32_t)((ks_threads + 255) / 256)), dim3(256), 0, nullptr, k->d_rk,
@@ -434,10 +394,10 @@ int launch_gcm(const kfec_aead *k, bool open, size_t P, const void *src, size_t 
             n = 256;
         return std::max(n, 1);
     }();
-    // 32 KiB of GHASH tables per workgroup: 5 resident per CU (256 lanes; 512 lanes: 3, register-bound);
+    // 40 KiB of GHASH tables per workgroup: 3 resident per CU at 512 lanes (6 waves per SIMD), 4 at 256;
     // grid-stride over packets
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
-    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * (kGcmBlock >= 512 ? 3 : 5)));
+    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * (kGcmBlock >= 512 ? 3 : 4)));
     if (open) hipLaunchKernelGGL(gcm_kernel<true>, grid, dim3(kGcmBlock), 0, s, a);
     else hipLaunchKernelGGL(gcm_kernel<false>, grid, dim3(kGcmBlock), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
