@@ -17,9 +17,10 @@
  * tests/test_aead_oracle.py pins them against OpenSSL's libcrypto.
  *
  * The nonce depends only on iv_raw, so everything the key and the nonce alone determine -- the Poly1305 key
- * (ChaCha20 block 0) and, for xchacha20, the HChaCha20 subkey; for aes_gcm J0, E_K(J0) and the first 2 KiB
- * of CTR keystream; for aes_ocb Offset_0 -- is computed once per key for all 65536 iv values
- * (kfec_aead_create, on the device: 2 MiB / 4 MiB / 130 MiB / 1 MiB) and looked up per packet.
+ * (ChaCha20 block 0), for xchacha20 the HChaCha20 subkey, and the first 2 KiB of keystream; for aes_gcm J0,
+ * E_K(J0) and the first 2 KiB of CTR keystream; for aes_ocb Offset_0 -- is computed once per key for all
+ * 65536 iv values (kfec_aead_create, on the device: 130 / 132 / 130 / 1 MiB for chacha20 / xchacha20 /
+ * aes_gcm / aes_ocb) and looked up per packet.
  *
  * Conventions as include/kfec.h: d_ pointers are device pointers, the stream is a hipStream_t as void*.
  */

@@ -28,6 +28,7 @@
 
 #include "../../include/kfec_aead.h"
 #include "kfec_internal.hpp"
+#include "kfec_pkt.hpp"
 
 namespace kfec {
 
@@ -140,6 +141,28 @@ __global__ void iv_table_kernel(int mode, const uint32_t *key, uint32_t *tab)
     uint32_t o[16];
     chacha_block(k, 0u, nw, o);
     for (int i = 0; i < 8; ++i) e[i] = o[i];
+}
+
+// keystream table (16-lane kernels): the first kChaKsBytes of every iv's keystream (blocks 1 ..), thread per
+// (iv, 64-byte block); the key is the connection's (chacha20) or the iv's HChaCha20 subkey (xchacha20)
+#ifndef KFEC_AEAD_KS
+#define KFEC_AEAD_KS 1  // 16-lane kernels read the keystream from a per-iv table (0: ChaCha20 in the kernel)
+#endif
+constexpr uint32_t kChaKsBytes = 2048;
+
+__global__ void chacha_ks_kernel(int mode, const uint32_t *key, const uint32_t *tab, uint32_t *ks)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr uint32_t kBlocks = kChaKsBytes / 64;
+    if (e >= 65536ull * kBlocks) return;
+    const uint32_t iv = (uint32_t)(e / kBlocks), blk = (uint32_t)(e % kBlocks);
+    const bool x = mode == KFEC_AEAD_XCHACHA20;
+    uint32_t k[8];
+    for (int i = 0; i < 8; ++i) k[i] = x ? tab[(size_t)iv * 16 + i] : key[i];
+    uint32_t o[16];
+    chacha_block(k, blk + 1, iv | (iv << 16), o);
+    uint4 *d = reinterpret_cast<uint4 *>(ks + ((size_t)iv * kChaKsBytes + 64 * (size_t)blk) / 4);
+    for (int i = 0; i < 4; ++i) d[i] = make_uint4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
 }
 
 // ---- Poly1305, radix 2^26 ----------------------------------------------------------------------------
@@ -321,6 +344,9 @@ __device__ __forceinline__ void mask64(uint32_t (&o)[16], int rem)
     }
 }
 
+#ifndef KFEC_AEAD_ROW16
+#define KFEC_AEAD_ROW16 1  // 16-lane rows (aead16_kernel); 0: the 8-lane rows of aead_kernel
+#endif
 #ifndef KFEC_AEAD_AB
 #define KFEC_AEAD_AB 0  // timing ablations only (wrong output): bit 0 = no Poly1305 arithmetic, bit 1 = no ChaCha20 rounds
 #endif
@@ -340,6 +366,7 @@ struct AeadArgs {
     uint32_t *out_len;
     uint8_t *ok;
     const uint32_t *tab;
+    const uint4 *ks;  // keystream table (16-lane kernels, KFEC_AEAD_KS)
     uint64_t P;
     uint32_t key[8];
 };
@@ -556,6 +583,270 @@ __global__ void __launch_bounds__(kAeadBlock) aead_kernel(AeadArgs a)
     }
 }
 
+// ---- 16-lane rows (KFEC_AEAD_ROW16) --------------------------------------------------------------------
+// A row of 16 lanes per packet, each lane moving 16 contiguous bytes per round (256 per row: the copy rate of
+// this layout is 4.1 TB/s against 2.5 for 8 lanes x 64 bytes, profiles/r02_rowcopy.json).  In round t, lane l
+// owns ciphertext piece q = 16 t + l and message block b = 16 t + l.
+//  * ChaCha20: the four lanes of a quad compute the quad's 64-byte block together, one state column each
+//    (column rounds in place; for the diagonal rounds rows 1-3 are rotated across the quad by DPP quad_perm
+//    and back), and a final quad transpose hands lane c the block's row c = its 16 keystream bytes.
+//  * Poly1305: message block b is bytes [32 - H, 48 - H) of (piece b - 2 || piece b - 1) -- the pieces of the
+//    two lanes before (the previous round's lanes 14, 15 through a carry; the MAC header before round 0).
+//    Lane l's accumulator steps by r^16 and ends times r^(NB - b_last) from the row's powers r^1..r^16
+//    (4-step scan), and the 16 accumulators are summed across the row.
+constexpr int kRow16 = 16;
+
+__device__ __forceinline__ uint32_t quad_rot(uint32_t v, int s)
+{
+    // lane c of each quad receives v from lane (c + s) % 4
+    if (s == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x39, 0xF, 0xF, false);
+    if (s == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x93, 0xF, 0xF, false);
+}
+
+#define KFEC_QR4(a, b, c, d)                                      \
+    a += b; d = __builtin_rotateleft32(d ^ a, 16);                \
+    c += d; b = __builtin_rotateleft32(b ^ c, 12);                \
+    a += b; d = __builtin_rotateleft32(d ^ a, 8);                 \
+    c += d; b = __builtin_rotateleft32(b ^ c, 7);
+
+// 16 keystream bytes: row c (= lane % 4) of ChaCha20 block (key k, counter ctr, nonce words nw, nw)
+__device__ __forceinline__ uint4 chacha_quad(const uint32_t (&k)[8], uint32_t ctr, uint32_t nw, uint32_t c)
+{
+    // two-level selects (a select chain over k[] becomes a dynamically indexed private array)
+    const bool c1 = c & 1u, c2 = c & 2u;
+    const uint32_t a0 = c2 ? (c1 ? kSigma3 : kSigma2) : (c1 ? kSigma1 : kSigma0);
+    const uint32_t b0 = c2 ? (c1 ? k[3] : k[2]) : (c1 ? k[1] : k[0]);
+    const uint32_t c0 = c2 ? (c1 ? k[7] : k[6]) : (c1 ? k[5] : k[4]);
+    const uint32_t d0 = c == 0 ? ctr : c == 1 ? 0u : nw;
+    uint32_t a = a0, b = b0, cc = c0, d = d0;
+#pragma unroll 2
+    for (int i = 0; i < 10; ++i) {
+        KFEC_QR4(a, b, cc, d)
+        b = quad_rot(b, 1); cc = quad_rot(cc, 2); d = quad_rot(d, 3);
+        KFEC_QR4(a, b, cc, d)
+        b = quad_rot(b, 3); cc = quad_rot(cc, 2); d = quad_rot(d, 1);
+    }
+    a += a0; b += b0; cc += c0; d += d0;
+    // lane j holds column j (rows a, b, cc, d); lane c wants row c: word j of it from lane j's register c
+    uint32_t row[4];
+#pragma unroll
+    for (int sft = 0; sft < 4; ++sft) {
+        // lane j sends its register (j - sft) & 3 -- the row the receiving lane (j - sft) & 3 wants
+        const uint32_t r = (c - (uint32_t)sft) & 3u;
+        const uint32_t v = r == 0 ? a : r == 1 ? b : r == 2 ? cc : d;
+        const uint32_t got = sft ? quad_rot(v, sft) : v;
+        // received from lane (c + sft) & 3: word (c + sft) & 3 of row c
+        const uint32_t w = (c + (uint32_t)sft) & 3u;
+        row[0] = w == 0 ? got : (sft ? row[0] : 0u);
+        row[1] = w == 1 ? got : (sft ? row[1] : 0u);
+        row[2] = w == 2 ? got : (sft ? row[2] : 0u);
+        row[3] = w == 3 ? got : (sft ? row[3] : 0u);
+    }
+    return make_uint4(row[0], row[1], row[2], row[3]);
+}
+#undef KFEC_QR4
+
+template <bool IETF>
+__host__ __device__ constexpr uint32_t vpiece_dword(int piece, int d)
+{
+    // dword d of virtual ciphertext piece -1 or -2: the MAC header at stream positions [-H, 0)
+    uint32_t v = 0;
+    for (int i = 0; i < 4; ++i) {
+        const int pos = 16 * piece + 4 * d + i;  // stream position (< 0)
+        const int hb = pos + (IETF ? 16 : 23);   // header byte
+        uint32_t byte = 0;
+        if (hb >= 0) byte = hb < 15 ? ad_byte(hb) : (!IETF && hb == 15) ? 15u : 0u;
+        v |= byte << (8 * i);
+    }
+    return v;
+}
+
+template <bool IETF, bool OPEN>
+__global__ void __launch_bounds__(kAeadBlock) aead16_kernel(AeadArgs a)
+{
+    constexpr int H = IETF ? 16 : 23;
+    constexpr int TL = IETF ? 16 : 8;
+    constexpr int S = 32 - H;  // message block = bytes [S, S + 16) of (piece b - 2 || piece b - 1)
+    constexpr int S4 = S / 4, SB = S % 4;
+    constexpr int rows = kAeadBlock / kRow16;
+    const uint32_t lane = threadIdx.x % kRow16, quad = lane & 3u;
+    for (uint64_t p = (uint64_t)blockIdx.x * rows + threadIdx.x / kRow16; p < a.P;
+         p += (uint64_t)gridDim.x * rows) {
+        const uint32_t L = a.len[p];
+        const uint64_t off = a.off[p];
+        uint32_t n, iv, ptag = 0;
+        if (OPEN) {
+            if (L < KFEC_AEAD_OVERHEAD || L - KFEC_AEAD_OVERHEAD > a.dst_pitch) {
+                if (lane == 0) {
+                    a.out_len[p] = 0;
+                    a.ok[p] = 0;
+                }
+                continue;
+            }
+            n = L - KFEC_AEAD_OVERHEAD;
+            ptag = load4(a.src, a.src_dw, off + n + 4 * (lane & 3));
+            iv = load4(a.src, a.src_dw, off + n + 16) & 0xFFFFu;
+        } else {
+            if (L == 0 || (uint64_t)L + KFEC_AEAD_OVERHEAD > a.dst_pitch) {
+                if (lane == 0) a.out_len[p] = 0;
+                continue;
+            }
+            n = L;
+            iv = a.iv[p];
+        }
+        const uint32_t nw = iv | (iv << 16);
+        const uint32_t *e = a.tab + (size_t)iv * (IETF ? 16 : 8);
+        uint32_t k[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) k[i] = IETF ? e[i] : a.key[i];
+        const uint32_t *pk = e + (IETF ? 8 : 0);
+        const uint32_t t0 = pk[0], t1 = pk[1], t2 = pk[2], t3 = pk[3];
+        const uint32_t sk[4] = {pk[4], pk[5], pk[6], pk[7]};
+        const F5 r{{t0 & 0x3FFFFFFu, ((t0 >> 26) | (t1 << 6)) & 0x3FFFF03u, ((t1 >> 20) | (t2 << 12)) & 0x3FFC0FFu,
+                    ((t2 >> 14) | (t3 << 18)) & 0x3F03FFFu, (t3 >> 8) & 0x00FFFFFu}};
+        // lane l: r^(l+1); r^16 from lane 15
+        F5 pw = r;
+#pragma unroll
+        for (int d = 1; d < kRow16; d <<= 1) {
+            F5 y;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) y.v[i] = __shfl_up(pw.v[i], d, kRow16);
+            if (lane >= (uint32_t)d) pw = f5_mul(pw, y);
+        }
+        F5 r16;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) r16.v[i] = __shfl(pw.v[i], kRow16 - 1, kRow16);
+
+        const uint32_t tpos = IETF ? (n + 15u) & ~15u : n;
+        const uint32_t M = H + tpos + TL, NB = (M + 15) / 16;
+        const uint32_t rounds = (NB + kRow16 - 1) / kRow16;
+        // carries: the previous round's pieces of lanes 14 and 15 (the header before round 0)
+        uint32_t c14[4], c15[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            c14[i] = vpiece_dword<IETF>(-2, i);
+            c15[i] = vpiece_dword<IETF>(-1, i);
+        }
+        F5 acc = f5_zero();
+        int blast = -1;
+        uint8_t *dst = a.dst + p * a.dst_pitch;
+        uint32_t ctail = 0;
+        for (uint32_t t = 0; t < rounds; ++t) {
+            const uint32_t q = t * kRow16 + lane, qb = 16 * q;
+            uint32_t ct[4] = {0u, 0u, 0u, 0u};
+            // the quad's ChaCha20 block (counter 4 t + lane / 4 + 1), when it holds ciphertext
+            const uint32_t blk = 4 * t + lane / 4;
+            if (64 * blk < n) {
+                uint4 ks;
+                if (KFEC_AEAD_AB & 2) ks = make_uint4(k[0] + blk, k[1], k[2], k[3]);
+                else if (KFEC_AEAD_KS && 64 * blk + 64 <= kChaKsBytes) ks = a.ks[(size_t)iv * (kChaKsBytes / 16) + q];
+                else ks = chacha_quad(k, blk + 1, nw, quad);  // the quad's block: uniform per quad
+                if (qb < n) {
+                    uint4 in = load16(a.src, a.src_dw, off + qb);
+                    const uint32_t rem = n - qb;
+                    if (rem < 16) in = mask16(in, rem);
+                    uint4 out = u4_xor(in, ks);
+                    if (rem < 16) out = mask16(out, rem);
+                    const uint4 c4 = OPEN ? in : out;
+                    ct[0] = c4.x; ct[1] = c4.y; ct[2] = c4.z; ct[3] = c4.w;
+                    uint32_t *d32 = reinterpret_cast<uint32_t *>(dst + qb);
+                    if (rem >= 16) {
+                        *reinterpret_cast<uint4 *>(d32) = out;
+                    } else {
+                        const uint32_t o4[4] = {out.x, out.y, out.z, out.w};
+                        const uint32_t nd = OPEN ? (rem + 3) / 4 : rem / 4;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if ((uint32_t)i < nd) d32[i] = o4[i];
+                        if (!OPEN && (rem & 3)) ctail = o4[rem / 4];
+                    }
+                }
+            }
+            // the MAC trailer continues the ciphertext stream at tpos (n < 2^32: its high dword is zero)
+            if (qb + 16 > tpos && qb < tpos + TL) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int kk = (int)(qb + 4 * i) - (int)tpos;
+                    if (IETF) ct[i] |= kk == 0 ? 15u : kk == 8 ? n : 0u;
+                    else if (kk > -4 && kk < 4) ct[i] |= kk >= 0 ? n >> (8 * kk) : n << (-8 * kk);
+                }
+            }
+            // pieces b - 1 and b - 2 from the lanes before (carries across the round boundary)
+            uint32_t x[8];  // piece b - 2 || piece b - 1
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t u1 = __shfl_up(ct[i], 1, kRow16), u2 = __shfl_up(ct[i], 2, kRow16);
+                x[4 + i] = lane >= 1 ? u1 : c15[i];
+                x[i] = lane >= 2 ? u2 : lane == 1 ? c15[i] : c14[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                c14[i] = __shfl(ct[i], kRow16 - 2, kRow16);
+                c15[i] = __shfl(ct[i], kRow16 - 1, kRow16);
+            }
+            uint32_t msg[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) msg[i] = SB ? __builtin_amdgcn_alignbyte(x[S4 + i + 1], x[S4 + i], SB) : x[S4 + i];
+            const uint32_t b = q;  // message block
+            if (b < NB) {
+                const int blen = (int)min(16u, M - 16 * b);
+                const F5 m = f5_block(msg[0], msg[1], msg[2], msg[3], blen);
+                if (t && !(KFEC_AEAD_AB & 1)) acc = f5_mul(acc, r16);
+                f5_add(acc, m);
+                blast = (int)b;
+            }
+        }
+        // times r^(NB - b_last), 1..16, then the row sum
+        {
+            const int e1 = blast >= 0 ? (int)NB - blast - 1 : 0;
+            F5 rp;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) rp.v[i] = __shfl(pw.v[i], e1, kRow16);
+            acc = blast >= 0 && !(KFEC_AEAD_AB & 1) ? f5_mul(acc, rp) : blast >= 0 ? acc : f5_zero();
+        }
+#pragma unroll
+        for (int d = 1; d < kRow16; d <<= 1)
+#pragma unroll
+            for (int i = 0; i < 5; ++i) acc.v[i] += __shfl_xor(acc.v[i], d, kRow16);
+        uint32_t tag[4];
+        f5_tag(acc, sk, tag);
+        if (OPEN) {
+            const uint32_t l4 = lane & 3;
+            const uint32_t mine = l4 == 0 ? tag[0] : l4 == 1 ? tag[1] : l4 == 2 ? tag[2] : tag[3];
+            uint32_t bad = mine != ptag ? 1u : 0u;
+#pragma unroll
+            for (int d = 1; d < kRow16; d <<= 1) bad |= __shfl_xor(bad, d, kRow16);
+            if (bad) {  // no unauthenticated plaintext leaves the kernel
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);
+                const uint32_t nd = (n + 3) / 4;
+                for (uint32_t i = lane; i < nd; i += kRow16) d32[i] = 0u;
+            }
+            if (lane == 0) {
+                a.out_len[p] = bad ? 0u : n;
+                a.ok[p] = bad ? 0 : 1;
+            }
+        } else {
+            // dwords from floor4(n): the ciphertext's last n % 4 bytes || tag || iv_raw || zero pad (5 or 6),
+            // one per lane; the partial dword comes from the lane of the last ciphertext piece
+            const uint32_t o = n & 3u, n4 = n & ~3u;
+            const uint32_t cp = __shfl(ctail, (int)(((n - 1) / 16) % kRow16), kRow16);
+            const uint32_t cnt = (((n + KFEC_AEAD_OVERHEAD + 3u) & ~3u) - n4) / 4u;
+            const uint32_t w[7] = {o ? cp << (8 * (4 - o)) : 0u, tag[0], tag[1], tag[2], tag[3], iv, 0u};
+            uint32_t w1 = 0, w0 = 0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                w1 = lane == (uint32_t)i ? w[i + 1] : w1;
+                w0 = lane == (uint32_t)i ? w[i] : w0;
+            }
+            const uint32_t v = o ? __builtin_amdgcn_alignbyte(w1, w0, 4 - o) : w1;
+            if (lane < cnt) reinterpret_cast<uint32_t *>(dst + n4)[lane] = v;
+            if (lane == 0) a.out_len[p] = n + KFEC_AEAD_OVERHEAD;
+        }
+    }
+}
+
 int aead_cus()
 {
     static int cus = [] {
@@ -590,11 +881,21 @@ int launch_aead(const kfec_aead *k, bool open, size_t P, const void *src, size_t
     a.out_len = out_len;
     a.ok = ok;
     a.tab = k->d_tab;
+    a.ks = reinterpret_cast<const uint4 *>(k->d_ks);
     a.P = P;
     for (int i = 0; i < 8; ++i) a.key[i] = k->key[i];
+    const bool x = k->mode == KFEC_AEAD_XCHACHA20;
+    if (KFEC_AEAD_ROW16) {
+        const uint64_t rows = kAeadBlock / kRow16;
+        const dim3 grid16((uint32_t)std::min<uint64_t>((P + rows - 1) / rows, (uint64_t)aead_cus() * 16));
+        if (x && open) hipLaunchKernelGGL((aead16_kernel<true, true>), grid16, dim3(kAeadBlock), 0, s, a);
+        else if (x) hipLaunchKernelGGL((aead16_kernel<true, false>), grid16, dim3(kAeadBlock), 0, s, a);
+        else if (open) hipLaunchKernelGGL((aead16_kernel<false, true>), grid16, dim3(kAeadBlock), 0, s, a);
+        else hipLaunchKernelGGL((aead16_kernel<false, false>), grid16, dim3(kAeadBlock), 0, s, a);
+        return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
     const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)aead_cus() * 16));
-    const bool x = k->mode == KFEC_AEAD_XCHACHA20;
     if (x && open) hipLaunchKernelGGL((aead_kernel<true, true>), grid, dim3(kAeadBlock), 0, s, a);
     else if (x) hipLaunchKernelGGL((aead_kernel<true, false>), grid, dim3(kAeadBlock), 0, s, a);
     else if (open) hipLaunchKernelGGL((aead_kernel<false, true>), grid, dim3(kAeadBlock), 0, s, a);
@@ -622,9 +923,24 @@ int aead_setup(kfec_aead *k, const void *password, size_t len)
     if (rc == KFEC_OK && hipMemcpy(d_pw, password, len, hipMemcpyHostToDevice) != hipSuccess) rc = KFEC_EHIP;
     if (rc == KFEC_OK) {
         hipLaunchKernelGGL(sha3_256_kernel, dim3(1), dim3(64), 0, nullptr, d_pw, (uint64_t)len, d_key);
-        if (gcm) rc = gcm_setup(k, d_key);
-        else if (ocb) rc = ocb_setup(k, d_key);
-        else hipLaunchKernelGGL(iv_table_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, k->mode, d_key, k->d_tab);
+        if (gcm) {
+            rc = gcm_setup(k, d_key);
+        } else if (ocb) {
+            rc = ocb_setup(k, d_key);
+        } else {
+            hipLaunchKernelGGL(iv_table_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, k->mode, d_key, k->d_tab);
+            if (KFEC_AEAD_ROW16 && KFEC_AEAD_KS) {
+                if (hipMalloc(&k->d_ks, (size_t)65536 * kChaKsBytes) != hipSuccess) {
+                    k->d_ks = nullptr;
+                    rc = KFEC_ENOMEM;
+                } else {
+                    k->ks_bytes = kChaKsBytes;
+                    const uint64_t th = 65536ull * (kChaKsBytes / 64);
+                    hipLaunchKernelGGL(chacha_ks_kernel, dim3((uint32_t)((th + 255) / 256)), dim3(256), 0, nullptr,
+                                       k->mode, d_key, k->d_tab, reinterpret_cast<uint32_t *>(k->d_ks));
+                }
+            }
+        }
         if (rc == KFEC_OK && (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
                               hipMemcpy(k->key, d_key, 32, hipMemcpyDeviceToHost) != hipSuccess))
             rc = KFEC_EHIP;
