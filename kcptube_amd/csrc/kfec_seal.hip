@@ -24,7 +24,7 @@ namespace kfec {
 
 namespace {
 
-constexpr int kSealBlock = 512;  // 16 packets share one LDS copy of the tables (28 KiB): 4 workgroups = 32 waves per CU
+constexpr int kSealBlock = 512;  // 16 packets share one LDS copy of the tables
 
 struct Crc32Tables {
     uint32_t t[4][256];
@@ -46,17 +46,15 @@ constexpr Crc32Tables make_crc32_tables()
 __constant__ Crc32Tables c_crc = make_crc32_tables();
 
 // ---- parallel CRC-32 -------------------------------------------------------------------------------
-// Half a wave (32 lanes) per packet.  The message is right-aligned into 512-byte rounds (leading zero bytes
-// leave a CRC computed from a zero register unchanged); lane l takes the 16-byte chunk l of a round and
-// computes its raw CRC (zero init, slicing-by-4) and folds it into its own running sum across rounds
-// (Horner with shift_512); the 32 lanes' sums are combined once per packet in 5 butterfly levels:
+// Half a wave (32 lanes) per packet; lane l takes the 16-byte chunk l of each 512-byte round, computes its raw
+// CRC (zero init, slicing-by-16) and folds it into its own running sum across rounds (Horner with shift_512);
+// the 32 lanes' sums are combined once per packet:
 //   CRC(A || B) = shift_|B|(CRC(A)) ^ CRC(B),   shift_d(r) = r advanced through d zero bytes,
-// a GF(2)-linear map applied as 4 byte-indexed table lookups (linearity makes the per-lane sums combine
-// exactly like one round's chunk CRCs).  The
-// standard 0xFFFFFFFF init is folded in by complementing the first 4 message bytes (messages >= 4 bytes;
-// shorter ones run serially on one lane), and the result is complemented at the end.
-//   tables: [0] slicing-by-4 (4 x 256), [1 + k] shift by 16 << k bytes (k = 0..5), each 4 x 256 u32
-constexpr int kCrcMaps = 7;
+// a GF(2)-linear map (linearity makes the per-lane sums combine exactly like one round's chunk CRCs).  The
+// streaming rows right-align the message into the rounds (leading zero bytes leave a CRC computed from a zero
+// register unchanged); the register rows left-align it and take the trailing zeros back out at the end
+// (unshift).  The standard 0xFFFFFFFF init is folded in by complementing the first 4 message bytes (messages
+// >= 4 bytes; shorter ones run serially on one lane), and the result is complemented at the end.
 constexpr int kRowLanes = 32;
 constexpr int kCrcLane = 16;                       // bytes of a round per lane
 constexpr int kCrcRound = kCrcLane * kRowLanes;    // 512 B
@@ -72,128 +70,149 @@ constexpr int kCrcRound = kCrcLane * kRowLanes;    // 512 B
 constexpr int kCrcBatch = KFEC_SEAL_BATCH;         // rounds whose loads are issued together
 constexpr int kRowsPerBlock = kSealBlock / kRowLanes;
 
-#ifndef KFEC_SEAL_NIB
-#define KFEC_SEAL_NIB 0  // 1: nibble-indexed tables -- no LDS bank conflicts, but +33% VALU and slower
+#ifndef KFEC_SEAL_REG
+#define KFEC_SEAL_REG 1  // 0: every packet takes the streaming rows (A/B knob)
 #endif
 
-// The CRC tables each workgroup stages into LDS.
-//  nibble form (KFEC_SEAL_NIB): every map is GF(2)-linear, so it is the XOR of one 16-entry table per input
-//    nibble.  A 16-entry table is 16 consecutive dwords -- 16 distinct banks -- and all lanes of one
-//    ds_read_b32 read the same table, so distinct entries never share a bank: no conflicts (the byte tables'
-//    256 entries over 32 banks gave ~4-5-way conflicts on random data).  The 32 chunk lookups of a 16-byte
-//    chunk are also independent of each other, where slicing-by-4 chains the four dwords of a chunk.
-//      chunk[k][v]:    raw CRC (zero init) of a 16-byte chunk holding nibble v at nibble k, zeros elsewhere
-//      shift[m][j][v]: nibble j = v of a CRC register advanced through 16 << m zero bytes (m = 5: 512)
-//      byte0[v]:       the bytewise table, for packets of fewer than 4 bytes
-//  byte form: [0] slicing-by-4 (4 x 256), [1 + m] the shift maps, each 4 x 256
-struct CrcLds {
-#if KFEC_SEAL_NIB
-    uint32_t chunk[32][16];
-    uint32_t shift[6][8][16];
-    uint32_t byte0[256];
-#else
-    uint32_t t[kCrcMaps][4][256];
+#ifndef KFEC_SEAL_PREFETCH
+#define KFEC_SEAL_PREFETCH 1  // 0: no kernel prefetches the next packet (A/B knob)
 #endif
+
+// The CRC tables each workgroup stages into LDS (60 KiB; all maps GF(2)-linear, so table lookups of the
+// input's bytes XORed together):
+//   diag[v][s]:  slot s holds s16(s & 15, v), the raw CRC (zero init) of a 16-byte chunk with byte v at position
+//                s & 15 and zeros elsewhere (slicing-by-16: a chunk's CRC is 16 independent lookups).  At step k
+//                row lane l looks up its byte at position (l + k) & 15 in slot l + k: a row of 64 dwords puts
+//                slot s in bank s mod 32, so the 32 lanes of a read hit 32 different banks whatever their
+//                bytes -- no conflicts (one table per position shared by all lanes gave 2.3 LDS cycles per read
+//                on random bytes) -- and the step is the read's immediate offset (4 k)
+//   sh[j][v]:    byte j = v of a CRC register advanced through 512 zero bytes (Horner over rounds)
+//   col[i][l]:   register bit i of row lane l advanced past the 31 - l chunks of its round after it, so the
+//                row's 32 lane sums combine as XOR_l XOR_i bit_i(R_l) col[i][l]: one conflict-free lookup
+//                per bit (lane l reads bank l) and no dependent chain, instead of a 5-level tree of shifts
+// Measured and dropped: slicing-by-4 (4 dependent steps per chunk), per-lane copies of the
+// bytewise table (conflict-free, 16 dependent steps per chunk: slower), nibble tables (conflict-free, twice
+// the lookups and a third more VALU: slower).
+#ifndef KFEC_SEAL_DIAG
+#define KFEC_SEAL_DIAG 0  // 1: the diagonal, conflict-free layout below (+20% VALU for the rotation: slower)
+#endif
+constexpr int kDiagPitch = 2 * kRowLanes;
+struct CrcLds {
+#if KFEC_SEAL_DIAG
+    uint32_t diag[256][kDiagPitch];
+#else
+    uint32_t s16[16][256];
+#endif
+    uint32_t sh[4][256];
+    uint32_t col[32][kRowLanes];
 };
 constexpr int kCrcWords = (int)(sizeof(CrcLds) / 4);
+// after the LDS tables, in global memory only (one row of 32 dwords read per packet): unshift[d][i] = the CRC
+// register 1 << i taken back through d zero bytes (d < 512) -- the inverse of advancing it, which exists
+// because the reflected CRC-32 table's top bytes T[v] >> 24 are a permutation of v
+constexpr int kUnshiftWords = kCrcRound * 32;
+constexpr int kTabWords = kCrcWords + kUnshiftWords;
+
+struct InvTop {
+    uint8_t v[256];
+};
+constexpr InvTop make_inv_top()
+{
+    InvTop r{};
+    const Crc32Tables c = make_crc32_tables();
+    for (uint32_t i = 0; i < 256; ++i) r.v[c.t[0][i] >> 24] = (uint8_t)i;
+    return r;
+}
+__constant__ InvTop c_inv_top = make_inv_top();
+
+__device__ uint32_t advance(uint32_t r, int d)  // r through d zero bytes
+{
+    for (int i = 0; i < d; ++i) r = (r >> 8) ^ c_crc.t[0][r & 0xFFu];
+    return r;
+}
 
 __global__ void crc_tables_kernel(uint32_t *tab)
 {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= kCrcWords) return;
-#if KFEC_SEAL_NIB
-    uint32_t r = 0;
-    if (e < 32 * 16) {  // chunk[k][v]
-        const int k = e / 16, v = e % 16;
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t byte = i == k / 2 ? (uint32_t)v << (4 * (k & 1)) : 0u;
-            r = (r >> 8) ^ c_crc.t[0][(r ^ byte) & 0xFFu];
+    constexpr int kS16 = KFEC_SEAL_DIAG ? 256 * kDiagPitch : 16 * 256, kSh = kS16 + 4 * 256;
+    uint32_t r;
+    if (e < kS16) {
+#if KFEC_SEAL_DIAG  // diag[v][s]
+        r = advance(c_crc.t[0][e / kDiagPitch], 15 - (e % kDiagPitch & 15));
+#else  // s16[k][v]
+        r = advance(c_crc.t[0][e & 255], 15 - e / 256);
+#endif
+    } else if (e < kSh) {
+        const int f = e - kS16, j = f / 256, v = f & 255;
+        r = advance((uint32_t)v << (8 * j), kCrcRound);
+    } else if (e < kCrcWords) {
+        const int f = e - kSh, i = f / kRowLanes, l = f % kRowLanes;
+        r = advance(1u << i, kCrcLane * (kRowLanes - 1 - l));
+    } else if (e < kTabWords) {  // unshift[d][i]: undo d single-byte steps r' = (r >> 8) ^ T[r & 0xFF]
+        const int d = (e - kCrcWords) / 32, i = (e - kCrcWords) % 32;
+        r = 1u << i;
+        for (int k = 0; k < d; ++k) {
+            const uint32_t b = c_inv_top.v[r >> 24];
+            r = ((r ^ c_crc.t[0][b]) << 8) | b;
         }
-    } else if (e < 32 * 16 + 6 * 8 * 16) {  // shift[m][j][v]
-        const int f = e - 32 * 16, m = f / 128, j = (f / 16) & 7, v = f % 16;
-        r = (uint32_t)v << (4 * j);
-        const int d = kCrcLane << m;
-        for (int i = 0; i < d; ++i) r = (r >> 8) ^ c_crc.t[0][r & 0xFFu];
     } else {
-        r = c_crc.t[0][e - 32 * 16 - 6 * 8 * 16];
-    }
-    tab[e] = r;
-#else
-    const int map = e / 1024, j = (e / 256) & 3, v = e & 255;  // e = ((map * 4) + j) * 256 + v
-    if (map == 0) {
-        tab[e] = c_crc.t[j][v];
         return;
     }
-    uint32_t r = (uint32_t)v << (8 * j);
-    const int d = kCrcLane << (map - 1);
-    for (int i = 0; i < d; ++i) r = (r >> 8) ^ c_crc.t[0][r & 0xFFu];
     tab[e] = r;
-#endif
 }
 
-#if KFEC_SEAL_NIB
-// entry at byte offset bo (= 4 * nibble) of a 16-entry table
-__device__ __forceinline__ uint32_t nib_at(const uint32_t *t16, uint32_t bo)
+// raw CRC (zero init) of the 16-byte chunk o on row lane l: 16 independent, conflict-free lookups (diag)
+__device__ __forceinline__ uint32_t crc_chunk(const CrcLds &t, const uint32_t (&o)[4], uint32_t lane)
 {
-    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(t16) + bo);
-}
-
-// raw CRC (zero init) of the 16-byte chunk o: 32 independent lookups
-__device__ __forceinline__ uint32_t crc_chunk(const CrcLds &t, const uint32_t (&o)[4])
-{
+#if KFEC_SEAL_DIAG
+    // rotate the chunk right by q = l & 15 bytes, so that step k finds byte (k + q) & 15 at byte k
+    const uint32_t q = lane & 15u;
+    uint32_t e[4], d[4], x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) e[i] = q & 8u ? o[(i + 2) & 3] : o[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = q & 4u ? e[(i + 1) & 3] : e[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_alignbyte(d[(i + 1) & 3], d[i], q & 3u);
     uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t lo = (o[i] << 2) & 0x3C3C3C3Cu, hi = (o[i] >> 2) & 0x3C3C3C3Cu;  // 4 x nibble per byte
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-            c ^= nib_at(t.chunk[8 * i + 2 * b], (lo >> (8 * b)) & 0xFFu) ^
-                 nib_at(t.chunk[8 * i + 2 * b + 1], (hi >> (8 * b)) & 0xFFu);
-    }
+    for (int k = 0; k < 16; ++k) c ^= t.diag[(x[k >> 2] >> (8 * (k & 3))) & 0xFFu][lane + k];
     return c;
-}
-
-// map m applied to the register r
-__device__ __forceinline__ uint32_t crc_shift(const CrcLds &t, int m, uint32_t r)
-{
-    const uint32_t lo = (r << 2) & 0x3C3C3C3Cu, hi = (r >> 2) & 0x3C3C3C3Cu;
-    uint32_t c = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-        c ^= nib_at(t.shift[m][2 * b], (lo >> (8 * b)) & 0xFFu) ^ nib_at(t.shift[m][2 * b + 1], (hi >> (8 * b)) & 0xFFu);
-    return c;
-}
-
-__device__ __forceinline__ uint32_t crc_byte(const CrcLds &t, uint32_t c, uint32_t byte)
-{
-    return (c >> 8) ^ t.byte0[(c ^ byte) & 0xFFu];
-}
 #else
-__device__ __forceinline__ uint32_t crc_dword(const uint32_t (*t)[256], uint32_t c, uint32_t d)
-{
-    const uint32_t x = c ^ d;
-    return t[3][x & 0xFFu] ^ t[2][(x >> 8) & 0xFFu] ^ t[1][(x >> 16) & 0xFFu] ^ t[0][x >> 24];
-}
-
-__device__ __forceinline__ uint32_t crc_chunk(const CrcLds &t, const uint32_t (&o)[4])
-{
-    uint32_t c = 0;
+    uint32_t c[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) c = crc_dword(t.t[0], c, o[i]);
-    return c;
+    for (int i = 0; i < 4; ++i)
+        c[i] = t.s16[4 * i][o[i] & 0xFFu] ^ t.s16[4 * i + 1][(o[i] >> 8) & 0xFFu] ^
+               t.s16[4 * i + 2][(o[i] >> 16) & 0xFFu] ^ t.s16[4 * i + 3][o[i] >> 24];
+    return c[0] ^ c[1] ^ c[2] ^ c[3];
+#endif
 }
 
-__device__ __forceinline__ uint32_t crc_shift(const CrcLds &t, int m, uint32_t r)
+// the register r advanced through 512 zero bytes
+__device__ __forceinline__ uint32_t crc_shift512(const CrcLds &t, uint32_t r)
 {
-    const uint32_t (*s)[256] = t.t[1 + m];
-    return s[0][r & 0xFFu] ^ s[1][(r >> 8) & 0xFFu] ^ s[2][(r >> 16) & 0xFFu] ^ s[3][r >> 24];
+    return t.sh[0][r & 0xFFu] ^ t.sh[1][(r >> 8) & 0xFFu] ^ t.sh[2][(r >> 16) & 0xFFu] ^ t.sh[3][r >> 24];
+}
+
+// the 32 lane sums of a row, each advanced past the chunks after it in the round (col), XORed over the row
+__device__ __forceinline__ uint32_t row_combine(const CrcLds &t, uint32_t R, uint32_t lane)
+{
+    uint32_t Z = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) Z ^= (uint32_t)((int32_t)(R << (31 - i)) >> 31) & t.col[i][lane];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) Z ^= __shfl_xor(Z, 1 << k, kRowLanes);
+    return Z;
 }
 
 __device__ __forceinline__ uint32_t crc_byte(const CrcLds &t, uint32_t c, uint32_t byte)
 {
-    return (c >> 8) ^ t.t[0][0][(c ^ byte) & 0xFFu];
-}
+#if KFEC_SEAL_DIAG
+    return (c >> 8) ^ t.diag[(c ^ byte) & 0xFFu][15];
+#else
+    return (c >> 8) ^ t.s16[15][(c ^ byte) & 0xFFu];
 #endif
+}
 
 // 16 bytes [q0, q0 + 16) of base[start, start + len), zero outside (dword-aligned base, dwords < lim32):
 // one 16-byte load at the covering dword (dword alignment suffices on gfx950) and one more dword
@@ -263,19 +282,13 @@ __device__ __forceinline__ uint32_t row_crc32(const CrcLds &tab, const uint32_t 
         }
 #pragma unroll
         for (int u = 0; u < kCrcBatch; ++u) {  // fixed trip count (a break here sent o[][] to scratch)
-            const uint32_t c = crc_chunk(tab, o[u]);
+            const uint32_t c = crc_chunk(tab, o[u], lane);
             // Horner over this lane's chunks: R = XOR_r shift_{(rounds-1-r)*512}(chunk CRC of round r)
-            if (r0 + u < rounds) R = crc_shift(tab, 5, R) ^ c;
+            if (r0 + u < rounds) R = crc_shift512(tab, R) ^ c;
         }
     }
-    // one butterfly per packet (not per round): by linearity the 32 lanes' Horner sums combine exactly as
-    // one round's chunk CRCs do.  Level k: the lane holding the earlier block A shifts it past the later
-    // block B (16 << k bytes): A' = shift(A) ^ B -- one table shift per lane, the operands picked by lane bit
-    for (int k = 0; k < 5; ++k) {
-        const uint32_t other = __shfl_xor(R, 1 << k, kRowLanes);
-        const bool later = lane & (1u << k);
-        R = crc_shift(tab, k, later ? other : R) ^ (later ? R : other);
-    }
+    // by linearity the 32 lanes' Horner sums combine exactly as one round's chunk CRCs do
+    R = row_combine(tab, R, lane);
     return ~R;
 }
 
@@ -284,6 +297,117 @@ __device__ __forceinline__ uint32_t row_crc32(const CrcLds &tab, const uint32_t 
 __device__ __forceinline__ uint32_t checksum16(uint32_t c)
 {
     return (((c >> 24) ^ (c >> 8)) & 0xFFu) | ((((c >> 16) ^ c) & 0xFFu) << 8);
+}
+
+// ---- register-resident rows -------------------------------------------------------------------------
+// A packet of up to kRegRounds rounds (2 KiB, every kcptube datagram at its MTUs) is loaded whole into
+// left-aligned chunks -- lane l holds chunk j = 32 r + l = bytes [16 j, 16 j + 16) of round r -- with every
+// load of the row issued before any arithmetic, and the CRC, the xor modes and the output all come from
+// those registers: the packet is read once and written once.  (The rows above stream round by round, one
+// round in flight per row, and read each packet twice: latency-bound.)  Longer packets take those rows.
+constexpr int kRegRounds = 4;
+constexpr uint32_t kRegBytes = kRegRounds * kCrcRound;
+
+__device__ uint4 g_zero16;  // never written: the target of the loads a register row does not need
+
+  // never written: the target of the loads a register row does not need
+
+// The register rows load without a branch: both loads of a chunk are always issued, a chunk past the packet
+// (or a dword it does not need) reading g_zero16 instead.  A load under a branch makes the compiler wait for
+// it at the join (the loaded value is a phi there), which serialised every chunk of a row behind the one
+// before.  The bytes past len in the packet's last partial chunk are left for mask_tail(); every window read
+// must lie inside the buffer, so row_fits() is checked for the row first.
+__device__ __forceinline__ bool row_fits(uint64_t start, uint32_t len, uint64_t lim32)
+{
+    return ((start + 16 * (uint64_t)((len + 15) / 16)) >> 2) + 1 <= lim32;
+}
+
+__device__ __forceinline__ void load_row(const uint32_t *base32, uint64_t start, uint32_t len, uint32_t lane,
+                                         uint32_t (&o)[kRegRounds][4])
+{
+    const uint32_t sh = (uint32_t)(start & 3u);
+    const uint32_t *rp = base32 + (start >> 2) + 4 * lane;  // chunk r of this lane: the 5 dwords at rp + 128 r
+#pragma unroll
+    for (int r = 0; r < kRegRounds; ++r) {
+        const bool any = (uint32_t)(r * kCrcRound) + kCrcLane * lane < len;
+        const uint4 x = *(any ? reinterpret_cast<const uint4 *>(rp + 128 * r) : &g_zero16);
+        const uint32_t x4 = *(any && sh ? rp + 128 * r + 4 : &g_zero16.x);
+        o[r][0] = __builtin_amdgcn_alignbyte(x.y, x.x, sh);
+        o[r][1] = __builtin_amdgcn_alignbyte(x.z, x.y, sh);
+        o[r][2] = __builtin_amdgcn_alignbyte(x.w, x.z, sh);
+        o[r][3] = __builtin_amdgcn_alignbyte(x4, x.w, sh);
+    }
+}
+
+// keep the bytes of chunk o (at packet position q0 >= 0) below len
+__device__ __forceinline__ void mask_chunk(uint32_t (&o)[4], int32_t q0, uint32_t len)
+{
+    const int32_t hi = min(16, max(0, (int32_t)len - q0));
+    const uint32_t M = (1u << hi) - 1u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t nib = (M >> (4 * i)) & 0xFu;
+        o[i] &= ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
+    }
+}
+
+// zero the bytes at and past len (only the chunk holding position len has any that are not zero already)
+__device__ __forceinline__ void mask_tail(uint32_t (&o)[kRegRounds][4], uint32_t len, uint32_t lane)
+{
+#pragma unroll
+    for (int r = 0; r < kRegRounds; ++r) {
+        const int32_t q0 = (int32_t)(r * kCrcRound + kCrcLane * lane);
+        if (q0 < (int32_t)len && (int32_t)len < q0 + 16) mask_chunk(o[r], q0, len);
+    }
+}
+
+// byte pos (0 <= pos < 16) of chunk o, through a 128-bit shift: any form that selects o[i] by pos (o[pos >> 2],
+// or the selects / conditional updates LLVM turns back into it) sends the whole row to scratch
+__device__ __forceinline__ unsigned __int128 as128(const uint32_t (&o)[4])
+{
+    return (unsigned __int128)o[0] | ((unsigned __int128)o[1] << 32) | ((unsigned __int128)o[2] << 64) |
+           ((unsigned __int128)o[3] << 96);
+}
+
+__device__ __forceinline__ uint32_t get_byte(const uint32_t (&o)[4], int32_t pos)
+{
+    return (uint32_t)(as128(o) >> (8 * pos)) & 0xFFu;
+}
+
+__device__ __forceinline__ void or_byte(uint32_t (&o)[4], int32_t pos, uint32_t byte)
+{
+    const unsigned __int128 v = (unsigned __int128)byte << (8 * pos);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] |= (uint32_t)(v >> (32 * i));
+}
+
+// standard CRC-32 of the first n bytes held left-aligned in o (bytes at and past n zero).  Horner over the
+// rounds and the row combine of row_crc32 give the raw CRC of M || 0^pad, pad = rounds * 512 - n the zero bytes
+// that close the last round; one linear map, the unshift by pad (u = row pad of the unshift table on lane i
+// (the caller reads it early), bit i of the register on lane i), takes it back to the raw CRC of M.
+__device__ __forceinline__ uint32_t crc_regs(const CrcLds &tab, uint32_t u, const uint32_t (&o)[kRegRounds][4],
+                                             uint32_t n, uint32_t lane)
+{
+    if (n < 4) {  // the init cannot be folded into message bytes: byte by byte from lane 0's first dword
+        uint32_t c = 0xFFFFFFFFu;
+        for (uint32_t i = 0; i < n; ++i) c = crc_byte(tab, c, o[0][0] >> (8 * i));
+        return ~__shfl(c, 0, kRowLanes);
+    }
+    const uint32_t rounds = (n + kCrcRound - 1) / kCrcRound;
+    uint32_t R = 0;
+#pragma unroll
+    for (int r = 0; r < kRegRounds; ++r) {
+        if ((uint32_t)r < rounds) {
+            const uint32_t x[4] = {o[r][0] ^ (r == 0 && lane == 0 ? 0xFFFFFFFFu : 0u), o[r][1], o[r][2], o[r][3]};
+            const uint32_t c = crc_chunk(tab, x, lane);
+            R = r == 0 ? c : crc_shift512(tab, R) ^ c;  // Horner: R = shift_512(R) ^ chunk CRC
+        }
+    }
+    R = row_combine(tab, R, lane);
+    uint32_t v = (R >> lane) & 1u ? u : 0u;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v ^= __shfl_xor(v, 1 << k, kRowLanes);
+    return ~v;
 }
 
 struct SealArgs {
@@ -297,9 +421,15 @@ struct SealArgs {
     uint32_t *out_len;
     uint8_t *ok;
     const uint32_t *tab;
+    const uint32_t *unshift;  // tab + kCrcWords
     uint64_t P;
     int mode;
 };
+
+__device__ __forceinline__ uint32_t *dst_row(const SealArgs &a, uint64_t p)
+{
+    return reinterpret_cast<uint32_t *>(a.dst + p * a.dst_pitch);
+}
 
 __device__ __forceinline__ void stage_tables(const uint32_t *tab, CrcLds &s_tab)
 {
@@ -320,166 +450,335 @@ __device__ __forceinline__ void store_chunk(uint32_t *dst, uint32_t j, uint32_t 
     }
 }
 
-__global__ void __launch_bounds__(kSealBlock) seal_kernel(SealArgs a)
+// ---- the streaming rows: packets longer than the register rows hold ------------------------------------
+__device__ __forceinline__ void seal_stream_row(const SealArgs &a, const CrcLds &s_tab, uint64_t p, uint32_t L,
+                                                uint64_t off, uint32_t lane)
+{
+    const uint32_t n = L + KFEC_SEAL_TRAILER, nd = (n + 3) / 4;
+    uint32_t *dst = dst_row(a, p);
+    const uint32_t cs = checksum16(row_crc32(s_tab, a.src, a.src_dw, off, L, lane));
+    for (uint32_t j0 = 0; 16 * j0 < n; j0 += kRowLanes) {  // whole rounds: the shuffle needs every lane
+        const uint32_t j = j0 + lane;
+        uint32_t o[5];
+        uint32_t q[4];
+        chunk16(a.src, a.src_dw, off, L, 16 * (int32_t)j, q);
+        o[0] = q[0]; o[1] = q[1]; o[2] = q[2]; o[3] = q[3];
+        // the checksum bytes at S positions L and L + 1 (positions relative to the chunk: c, c + 1)
+        const int32_t c = (int32_t)L - 16 * (int32_t)j;
+        o[4] = 0u;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int32_t t = 4 * i + b - c;  // checksum byte index at chunk position 4i + b
+                if (t == 0 || t == 1) o[i] |= ((cs >> (8 * t)) & 0xFFu) << (8 * b);
+            }
+        if (a.mode == KFEC_SEAL_PLAIN_XOR) {
+            // S[16j + 16]: the next chunk's first byte -- the next lane's, or a load for the round's last lane
+            uint32_t nx = KFEC_SEAL_SHFL ? __shfl_down(o[0], 1, kRowLanes) & 0xFFu : 0u;
+            if (!KFEC_SEAL_SHFL || lane == kRowLanes - 1) {
+                uint32_t t4[4];
+                chunk16(a.src, a.src_dw, off, L, 16 * (int32_t)j + 16, t4);
+                nx = t4[0] & 0xFFu;
+                const int32_t t0 = c - 16;  // position of S byte L (checksum byte 0) inside the next chunk
+                if (t0 == 0) nx = cs & 0xFFu;
+                else if (t0 == -1) nx = (cs >> 8) & 0xFFu;
+            }
+            o[4] |= nx;
+        }
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            w[i] = a.mode == KFEC_SEAL_PLAIN_XOR ? o[i] ^ ((o[i] >> 8) | (o[i + 1] << 24)) : o[i];
+        if (16 * j < n) store_chunk(dst, j, nd, w);
+    }    if (lane == 0) a.out_len[p] = n;
+}
+
+__device__ __forceinline__ void open_stream_row(const SealArgs &a, const CrcLds &s_tab, uint64_t p, uint32_t L,
+                                                uint64_t off, uint32_t lane)
+{
+    const bool px = a.mode == KFEC_SEAL_PLAIN_XOR;
+    const uint32_t n = L - KFEC_SEAL_TRAILER, nd = (n + 3) / 4;
+    // xor_backward: plain[i] = T ^ (XOR of cipher[0..i)), T = XOR of every cipher byte
+    uint32_t T = 0;
+    if (px) {
+        uint32_t x = 0;
+        for (uint32_t j = lane; 16 * j < L; j += kRowLanes) {
+            uint32_t o[4];
+            chunk16(a.src, a.src_dw, off, L, 16 * (int32_t)j, o);
+            x ^= o[0] ^ o[1] ^ o[2] ^ o[3];
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) x ^= __shfl_xor(x, 1 << k, kRowLanes);
+        x ^= x >> 16;
+        x ^= x >> 8;
+        T = (x & 0xFFu) * 0x01010101u;
+    }
+    uint32_t *dst = reinterpret_cast<uint32_t *>(a.dst + p * a.dst_pitch);
+    uint32_t carry = 0;    // XOR of the cipher bytes before this round (broadcast byte)
+    uint32_t trailer = 0;  // plaintext bytes n, n + 1 (little-endian u16), gathered from the owning lanes
+    for (uint32_t j0 = 0; 16 * j0 < L; j0 += kRowLanes) {
+        const uint32_t j = j0 + lane;
+        uint32_t o[4];
+        chunk16(a.src, a.src_dw, off, L, 16 * (int32_t)j, o);
+        if (px) {
+            // exclusive prefix XOR of the round's chunks across lanes, then bytewise inside the chunk
+            uint32_t cx = o[0] ^ o[1] ^ o[2] ^ o[3];
+            cx ^= cx >> 16;
+            cx ^= cx >> 8;
+            cx = (cx & 0xFFu) * 0x01010101u;  // this chunk's XOR, broadcast
+            uint32_t incl = cx;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const uint32_t v = __shfl_up(incl, 1 << k, kRowLanes);
+                if (lane >= (1u << k)) incl ^= v;
+            }
+            uint32_t run = carry ^ incl ^ cx;  // bytes before this chunk
+            carry ^= __shfl(incl, kRowLanes - 1, kRowLanes);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t in = o[i] ^ (o[i] << 8);
+                in ^= in << 16;  // byte b: XOR of bytes 0..b of this dword
+                const uint32_t x = T ^ run ^ (in << 8);
+                run ^= (in >> 24) * 0x01010101u;
+                o[i] = x;
+            }
+            // mask to the packet
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t b0 = 16 * (int64_t)j + 4 * i;
+                const int64_t k = (int64_t)L - b0;
+                if (k <= 0) o[i] = 0u;
+                else if (k < 4) o[i] &= (1u << (8 * k)) - 1u;
+            }
+        }
+        // trailer bytes n and n + 1
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int64_t t = 16 * (int64_t)j + 4 * i + b - n;  // trailer byte index at this position
+                if (t == 0 || t == 1) trailer |= ((o[i] >> (8 * b)) & 0xFFu) << (8 * t);
+            }
+        // plaintext bytes below n
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t k = (int64_t)n - (16 * (int64_t)j + 4 * i);
+            if (k <= 0) o[i] = 0u;
+            else if (k < 4) o[i] &= (1u << (8 * k)) - 1u;
+        }
+        if (16 * j < n) store_chunk(dst, j, nd, o);
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) trailer |= __shfl_xor(trailer, 1 << k, kRowLanes);
+    // CRC of the plaintext: for "none" it is the packet's own first n bytes; for plain_xor the plaintext
+    // just written (same wave: drain the stores first)
+    uint32_t crc;
+    if (px) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        crc = row_crc32(s_tab, dst, nd, 0, n, lane);
+    } else {
+        crc = row_crc32(s_tab, a.src, a.src_dw, off, n, lane);
+    }    if (lane == 0) {
+        a.out_len[p] = n;
+        a.ok[p] = checksum16(crc) == trailer;
+    }
+}
+
+// ---- the row walker ------------------------------------------------------------------------------------
+// Each row takes packets p, p + S, p + 2S, ... (S = the grid's rows) and keeps the next packet's bytes in
+// flight while it computes the current one: (len, off) are read two packets ahead, the bytes one ahead
+// (load_len(L) of them: 0 for a packet the streaming rows take, or none), and the unshift row of the
+// current packet is read before that prefetch is issued, so that waiting for it (vmcnt counts in issue
+// order) does not wait for the prefetch.  body(p, L, off, o, u) gets the packet's registers.  PF = false
+// loads the packet when the row reaches it (fewer VGPRs: measured faster for open and the in-place kernel,
+// prefetch faster for seal).
+template <bool PF, class LoadLen, class CrcLen, class Body>
+__device__ __forceinline__ void for_each_row(const SealArgs &a, uint32_t lane, LoadLen load_len, CrcLen crc_len, Body body)
+{
+    const uint64_t S = (uint64_t)gridDim.x * kRowsPerBlock;
+    uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRowLanes;
+    uint32_t L1 = 0, L2 = 0;
+    uint64_t off1 = 0, off2 = 0;
+    if (p < a.P) {
+        L1 = a.len[p];
+        off1 = a.off[p];
+    }
+    if (p + S < a.P) {
+        L2 = a.len[p + S];
+        off2 = a.off[p + S];
+    }
+    uint32_t nx[kRegRounds][4];
+    if (PF) load_row(a.src, off1, p < a.P ? load_len(L1, off1) : 0u, lane, nx);
+    for (; p < a.P; p += S) {
+        const uint32_t L = L1;
+        const uint64_t off = off1;
+        uint32_t o[kRegRounds][4];
+#pragma unroll
+        for (int r = 0; r < kRegRounds; ++r)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[r][i] = nx[r][i];
+        const uint32_t nc = crc_len(L);
+        const uint32_t pad = (kCrcRound - nc % kCrcRound) % kCrcRound;
+        const uint32_t u = load_len(L, off) && nc >= 4 ? a.unshift[pad * 32 + lane] : 0u;
+        L1 = L2;
+        off1 = off2;
+        if (p + 2 * S < a.P) {
+            L2 = a.len[p + 2 * S];
+            off2 = a.off[p + 2 * S];
+        }
+        if (PF) load_row(a.src, off1, p + S < a.P ? load_len(L1, off1) : 0u, lane, nx);
+        else load_row(a.src, off, load_len(L, off), lane, o);
+        body(p, L, off, o, u);
+    }
+}
+
+// the plaintext bytes n, n + 1 (a little-endian u16) from the lanes holding them, on every lane of the row
+__device__ __forceinline__ uint32_t row_trailer(const uint32_t (&o)[kRegRounds][4], uint32_t n, uint32_t lane)
+{
+    uint32_t t = 0;
+#pragma unroll
+    for (int r = 0; r < kRegRounds; ++r) {
+        const int32_t c = (int32_t)n - (int32_t)(r * kCrcRound + kCrcLane * lane);
+        if (c >= -1 && c < 16) {
+            if (c >= 0) t |= get_byte(o[r], c);
+            if (c + 1 < 16) t |= get_byte(o[r], c + 1) << 8;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t |= __shfl_xor(t, 1 << k, kRowLanes);
+    return t;
+}
+
+__global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu(4))) seal_kernel(SealArgs a)
 {
     __shared__ CrcLds s_tab;
     stage_tables(a.tab, s_tab);
     const uint32_t lane = threadIdx.x % kRowLanes;
-    for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRowLanes; p < a.P;
-         p += (uint64_t)gridDim.x * kRowsPerBlock) {
-        const uint32_t L = a.len[p];
-        const uint64_t off = a.off[p];
-        if (L == 0 || L + KFEC_SEAL_TRAILER > a.dst_pitch) {  // encrypt_data: "empty data" (:173-174); no room
+    // encrypt_data: "empty data" (:173-174), or no room in dst
+    auto valid = [&](uint32_t L) { return L != 0 && L + KFEC_SEAL_TRAILER <= a.dst_pitch; };
+    auto load_len = [&](uint32_t L, uint64_t off) {
+        return KFEC_SEAL_REG && valid(L) && L + KFEC_SEAL_TRAILER <= kRegBytes && row_fits(off, L, a.src_dw) ? L : 0u;
+    };
+    auto crc_len = [](uint32_t L) { return L; };
+    for_each_row<KFEC_SEAL_PREFETCH != 0>(a, lane, load_len, crc_len, [&](uint64_t p, uint32_t L, uint64_t off, uint32_t (&o)[kRegRounds][4], uint32_t u) {
+        if (!valid(L)) {
             if (lane == 0) a.out_len[p] = 0;
-            continue;
+            return;
         }
-        const uint32_t cs = checksum16(row_crc32(s_tab, a.src, a.src_dw, off, L, lane));
+        if (!load_len(L, off)) {
+            seal_stream_row(a, s_tab, p, L, off, lane);
+            return;
+        }
         // sealed packet S = data || cs, xor_forward'ed for plain_xor (out[i] = S[i] ^ S[i + 1])
         const uint32_t n = L + KFEC_SEAL_TRAILER, nd = (n + 3) / 4;
-        uint32_t *dst = reinterpret_cast<uint32_t *>(a.dst + p * a.dst_pitch);
-        for (uint32_t j0 = 0; 16 * j0 < n; j0 += kRowLanes) {  // whole rounds: the shuffle needs every lane
-            const uint32_t j = j0 + lane;
-            uint32_t o[5];
-            uint32_t q[4];
-            chunk16(a.src, a.src_dw, off, L, 16 * (int32_t)j, q);
-            o[0] = q[0]; o[1] = q[1]; o[2] = q[2]; o[3] = q[3];
-            // the checksum bytes at S positions L and L + 1 (positions relative to the chunk: c, c + 1)
-            const int32_t c = (int32_t)L - 16 * (int32_t)j;
-            o[4] = 0u;
+        mask_tail(o, L, lane);
+        const uint32_t cs = checksum16(crc_regs(s_tab, u, o, L, lane));
 #pragma unroll
-            for (int i = 0; i < 5; ++i)
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int32_t t = 4 * i + b - c;  // checksum byte index at chunk position 4i + b
-                    if (t == 0 || t == 1) o[i] |= ((cs >> (8 * t)) & 0xFFu) << (8 * b);
-                }
-            if (a.mode == KFEC_SEAL_PLAIN_XOR) {
-                // S[16j + 16]: the next chunk's first byte -- the next lane's, or a load for the round's last lane
-                uint32_t nx = KFEC_SEAL_SHFL ? __shfl_down(o[0], 1, kRowLanes) & 0xFFu : 0u;
-                if (!KFEC_SEAL_SHFL || lane == kRowLanes - 1) {
-                    uint32_t t4[4];
-                    chunk16(a.src, a.src_dw, off, L, 16 * (int32_t)j + 16, t4);
-                    nx = t4[0] & 0xFFu;
-                    const int32_t t0 = c - 16;  // position of S byte L (checksum byte 0) inside the next chunk
-                    if (t0 == 0) nx = cs & 0xFFu;
-                    else if (t0 == -1) nx = (cs >> 8) & 0xFFu;
-                }
-                o[4] |= nx;
+        for (int r = 0; r < kRegRounds; ++r) {
+            const int32_t c = (int32_t)L - (int32_t)(r * kCrcRound + kCrcLane * lane);  // cs byte 0 at chunk position c
+            if (c >= -1 && c < 16) {
+                if (c >= 0) or_byte(o[r], c, cs & 0xFFu);
+                if (c + 1 < 16) or_byte(o[r], c + 1, cs >> 8);
             }
-            uint32_t w[4];
+        }
+        uint32_t *dst = dst_row(a, p);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                w[i] = a.mode == KFEC_SEAL_PLAIN_XOR ? o[i] ^ ((o[i] >> 8) | (o[i + 1] << 24)) : o[i];
+        for (int r = 0; r < kRegRounds; ++r) {
+            uint32_t w[4] = {o[r][0], o[r][1], o[r][2], o[r][3]};
+            if (a.mode == KFEC_SEAL_PLAIN_XOR) {
+                // S[16 j + 16]: the next lane's first byte; for the row's last lane, lane 0's of the next round
+                const uint32_t down = __shfl_down(o[r][0], 1, kRowLanes);
+                const uint32_t wrap = r + 1 < kRegRounds ? __shfl(o[r + 1 < kRegRounds ? r + 1 : r][0], 0, kRowLanes) : 0u;
+                const uint32_t next[4] = {o[r][1], o[r][2], o[r][3], (lane == kRowLanes - 1 ? wrap : down) & 0xFFu};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[i] ^= (o[r][i] >> 8) | (next[i] << 24);
+            }
+            const uint32_t j = r * kRowLanes + lane;
             if (16 * j < n) store_chunk(dst, j, nd, w);
         }
         if (lane == 0) a.out_len[p] = n;
-    }
+    });
 }
 
-__global__ void __launch_bounds__(kSealBlock) open_kernel(SealArgs a)
+__global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu(4))) open_kernel(SealArgs a)
 {
     __shared__ CrcLds s_tab;
     stage_tables(a.tab, s_tab);
     const uint32_t lane = threadIdx.x % kRowLanes;
     const bool px = a.mode == KFEC_SEAL_PLAIN_XOR;
-    for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRowLanes; p < a.P;
-         p += (uint64_t)gridDim.x * kRowsPerBlock) {
-        const uint32_t L = a.len[p];
-        const uint64_t off = a.off[p];
-        if (L <= KFEC_SEAL_TRAILER || L - KFEC_SEAL_TRAILER > a.dst_pitch) {  // decrypt_data: bad length
+    // decrypt_data: bad length (nothing besides the trailer), or no room in dst
+    auto valid = [&](uint32_t L) { return L > KFEC_SEAL_TRAILER && L - KFEC_SEAL_TRAILER <= a.dst_pitch; };
+    auto load_len = [&](uint32_t L, uint64_t off) {
+        return KFEC_SEAL_REG && valid(L) && L <= kRegBytes && row_fits(off, L, a.src_dw) ? L : 0u;
+    };
+    auto crc_len = [](uint32_t L) { return L - KFEC_SEAL_TRAILER; };
+    for_each_row<false>(a, lane, load_len, crc_len, [&](uint64_t p, uint32_t L, uint64_t off, uint32_t (&o)[kRegRounds][4], uint32_t u) {
+        if (!valid(L)) {
             if (lane == 0) {
                 a.out_len[p] = 0;
                 a.ok[p] = 0;
             }
-            continue;
+            return;
+        }
+        if (!load_len(L, off)) {
+            open_stream_row(a, s_tab, p, L, off, lane);
+            return;
         }
         const uint32_t n = L - KFEC_SEAL_TRAILER, nd = (n + 3) / 4;
-        // xor_backward: plain[i] = T ^ (XOR of cipher[0..i)), T = XOR of every cipher byte
-        uint32_t T = 0;
-        if (px) {
+        if (px) {  // xor_backward: plain[i] = T ^ (XOR of cipher[0..i)), T = XOR of every cipher byte
+            mask_tail(o, L, lane);
             uint32_t x = 0;
-            for (uint32_t j = lane; 16 * j < L; j += kRowLanes) {
-                uint32_t o[4];
-                chunk16(a.src, a.src_dw, off, L, 16 * (int32_t)j, o);
-                x ^= o[0] ^ o[1] ^ o[2] ^ o[3];
-            }
+#pragma unroll
+            for (int r = 0; r < kRegRounds; ++r) x ^= o[r][0] ^ o[r][1] ^ o[r][2] ^ o[r][3];
 #pragma unroll
             for (int k = 0; k < 5; ++k) x ^= __shfl_xor(x, 1 << k, kRowLanes);
             x ^= x >> 16;
             x ^= x >> 8;
-            T = (x & 0xFFu) * 0x01010101u;
-        }
-        uint32_t *dst = reinterpret_cast<uint32_t *>(a.dst + p * a.dst_pitch);
-        uint32_t carry = 0;    // XOR of the cipher bytes before this round (broadcast byte)
-        uint32_t trailer = 0;  // plaintext bytes n, n + 1 (little-endian u16), gathered from the owning lanes
-        for (uint32_t j0 = 0; 16 * j0 < L; j0 += kRowLanes) {
-            const uint32_t j = j0 + lane;
-            uint32_t o[4];
-            chunk16(a.src, a.src_dw, off, L, 16 * (int32_t)j, o);
-            if (px) {
+            const uint32_t T = (x & 0xFFu) * 0x01010101u;
+            uint32_t carry = 0;  // XOR of the cipher bytes of the rounds before (broadcast byte)
+#pragma unroll
+            for (int r = 0; r < kRegRounds; ++r) {
                 // exclusive prefix XOR of the round's chunks across lanes, then bytewise inside the chunk
-                uint32_t cx = o[0] ^ o[1] ^ o[2] ^ o[3];
+                uint32_t cx = o[r][0] ^ o[r][1] ^ o[r][2] ^ o[r][3];
                 cx ^= cx >> 16;
                 cx ^= cx >> 8;
-                cx = (cx & 0xFFu) * 0x01010101u;  // this chunk's XOR, broadcast
+                cx = (cx & 0xFFu) * 0x01010101u;
                 uint32_t incl = cx;
 #pragma unroll
                 for (int k = 0; k < 5; ++k) {
                     const uint32_t v = __shfl_up(incl, 1 << k, kRowLanes);
                     if (lane >= (1u << k)) incl ^= v;
                 }
-                uint32_t run = carry ^ incl ^ cx;  // bytes before this chunk
+                uint32_t run = carry ^ incl ^ cx;
                 carry ^= __shfl(incl, kRowLanes - 1, kRowLanes);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    uint32_t in = o[i] ^ (o[i] << 8);
+                    uint32_t in = o[r][i] ^ (o[r][i] << 8);
                     in ^= in << 16;  // byte b: XOR of bytes 0..b of this dword
-                    const uint32_t x = T ^ run ^ (in << 8);
+                    const uint32_t y = T ^ run ^ (in << 8);
                     run ^= (in >> 24) * 0x01010101u;
-                    o[i] = x;
-                }
-                // mask to the packet
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int64_t b0 = 16 * (int64_t)j + 4 * i;
-                    const int64_t k = (int64_t)L - b0;
-                    if (k <= 0) o[i] = 0u;
-                    else if (k < 4) o[i] &= (1u << (8 * k)) - 1u;
+                    o[r][i] = y;
                 }
             }
-            // trailer bytes n and n + 1
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int64_t t = 16 * (int64_t)j + 4 * i + b - n;  // trailer byte index at this position
-                    if (t == 0 || t == 1) trailer |= ((o[i] >> (8 * b)) & 0xFFu) << (8 * t);
-                }
-            // plaintext bytes below n
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int64_t k = (int64_t)n - (16 * (int64_t)j + 4 * i);
-                if (k <= 0) o[i] = 0u;
-                else if (k < 4) o[i] &= (1u << (8 * k)) - 1u;
-            }
-            if (16 * j < n) store_chunk(dst, j, nd, o);
         }
+        const uint32_t trailer = row_trailer(o, n, lane);
+        uint32_t *dst = dst_row(a, p);
 #pragma unroll
-        for (int k = 0; k < 5; ++k) trailer |= __shfl_xor(trailer, 1 << k, kRowLanes);
-        // CRC of the plaintext: for "none" it is the packet's own first n bytes; for plain_xor the plaintext
-        // just written (same wave: drain the stores first)
-        uint32_t crc;
-        if (px) {
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            crc = row_crc32(s_tab, dst, nd, 0, n, lane);
-        } else {
-            crc = row_crc32(s_tab, a.src, a.src_dw, off, n, lane);
+        for (int r = 0; r < kRegRounds; ++r) {
+            // past the plaintext: the trailer, and for plain_xor the scan's bytes past L (chunks after the one
+            // holding n are zeroed whole)
+            const int32_t q0 = (int32_t)(r * kCrcRound + kCrcLane * lane);
+            if ((int32_t)n < q0 + 16) mask_chunk(o[r], q0, n);
+            const uint32_t j = r * kRowLanes + lane;
+            if (16 * j < n) store_chunk(dst, j, nd, o[r]);
         }
+        const uint32_t crc = crc_regs(s_tab, u, o, n, lane);
         if (lane == 0) {
             a.out_len[p] = n;
             a.ok[p] = checksum16(crc) == trailer;
         }
-    }
+    });
 }
 
 // Checksum mode in place (kfec_seal_batch / kfec_open_batch with d_dst == NULL): the packets stay where they
@@ -488,41 +787,59 @@ __global__ void __launch_bounds__(kSealBlock) open_kernel(SealArgs a)
 // its out-of-place path 24%).  Seal writes a trailer only where it fits the packet's slot (a.dst_pitch =
 // the slot size from d_off, e.g. pkt_pitch) and the buffer: a packet filling its slot would otherwise get
 // its trailer written over the next packet while another row is still reading that packet for its CRC.
-__global__ void __launch_bounds__(kSealBlock) seal_in_place_kernel(SealArgs a, bool open)
+__global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu(4))) seal_in_place_kernel(SealArgs a, bool open)
 {
     __shared__ CrcLds s_tab;
     stage_tables(a.tab, s_tab);
     const uint32_t lane = threadIdx.x % kRowLanes;
     uint8_t *base = const_cast<uint8_t *>(reinterpret_cast<const uint8_t *>(a.src));
-    for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRowLanes; p < a.P;
-         p += (uint64_t)gridDim.x * kRowsPerBlock) {
-        const uint32_t L = a.len[p];
-        const uint64_t off = a.off[p];
-        if (open ? L <= KFEC_SEAL_TRAILER : L == 0) {  // decrypt_data: bad length / encrypt_data: empty data
+    // decrypt_data: bad length / encrypt_data: empty data, or no room for the trailer
+    auto valid = [&](uint32_t L, uint64_t off) {
+        return open ? L > KFEC_SEAL_TRAILER
+                    : L != 0 && (uint64_t)L + KFEC_SEAL_TRAILER <= a.dst_pitch && off + L + KFEC_SEAL_TRAILER <= a.src_bytes;
+    };
+    // open keeps the trailer in the registers too (a load of it after the prefetch would wait for the prefetch)
+    auto load_len = [&](uint32_t L, uint64_t off) {
+        return KFEC_SEAL_REG && L != 0 && L <= kRegBytes && row_fits(off, L, a.src_dw) ? L : 0u;
+    };
+    auto crc_len = [&](uint32_t L) { return open ? L - KFEC_SEAL_TRAILER : L; };
+    for_each_row<false>(a, lane, load_len, crc_len, [&](uint64_t p, uint32_t L, uint64_t off, uint32_t (&o)[kRegRounds][4], uint32_t u) {
+        if (!valid(L, off)) {
             if (lane == 0) {
                 a.out_len[p] = 0;
                 if (open) a.ok[p] = 0;
             }
-            continue;
+            return;
         }
-        if (!open && ((uint64_t)L + KFEC_SEAL_TRAILER > a.dst_pitch || off + L + KFEC_SEAL_TRAILER > a.src_bytes)) {
-            if (lane == 0) a.out_len[p] = 0;  // no room for the trailer: "does not fit", nothing written
-            continue;
-        }
-        const uint32_t n = open ? L - KFEC_SEAL_TRAILER : L;  // bytes under the checksum
-        const uint32_t cs = checksum16(row_crc32(s_tab, a.src, a.src_dw, off, n, lane));
-        if (lane == 0) {
-            uint8_t *t = base + off + n;
+        const uint32_t n = crc_len(L);  // bytes under the checksum
+        uint32_t cs, trailer = 0;
+        if (load_len(L, off)) {
+            if (!open) mask_tail(o, n, lane);
             if (open) {
-                a.ok[p] = cs == ((uint32_t)t[0] | ((uint32_t)t[1] << 8));
+                trailer = row_trailer(o, n, lane);
+#pragma unroll
+                for (int r = 0; r < kRegRounds; ++r) {
+                    const int32_t q0 = (int32_t)(r * kCrcRound + kCrcLane * lane);
+                    if ((int32_t)n < q0 + 16) mask_chunk(o[r], q0, n);
+                }
+            }
+            cs = checksum16(crc_regs(s_tab, u, o, n, lane));
+        } else {
+            cs = checksum16(row_crc32(s_tab, a.src, a.src_dw, off, n, lane));
+            if (open && lane == 0) trailer = (uint32_t)base[off + n] | ((uint32_t)base[off + n + 1] << 8);
+        }
+        if (lane == 0) {
+            if (open) {
+                a.ok[p] = cs == trailer;
                 a.out_len[p] = n;
             } else {
+                uint8_t *t = base + off + n;
                 t[0] = (uint8_t)cs;
                 t[1] = (uint8_t)(cs >> 8);
                 a.out_len[p] = L + KFEC_SEAL_TRAILER;
             }
         }
-    }
+    });
 }
 
 uint32_t *crc_tables(hipStream_t s)
@@ -534,8 +851,8 @@ uint32_t *crc_tables(hipStream_t s)
     std::lock_guard<std::mutex> lk(mu);
     if (!tabs[dev]) {
         uint32_t *t = nullptr;
-        if (hipMalloc(&t, kCrcWords * sizeof(uint32_t)) != hipSuccess) return nullptr;
-        hipLaunchKernelGGL(crc_tables_kernel, dim3((kCrcWords + 255) / 256), dim3(256), 0, s, t);
+        if (hipMalloc(&t, kTabWords * sizeof(uint32_t)) != hipSuccess) return nullptr;
+        hipLaunchKernelGGL(crc_tables_kernel, dim3((kTabWords + 255) / 256), dim3(256), 0, s, t);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return nullptr;
         tabs[dev] = t;
     }
@@ -562,6 +879,7 @@ int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes
     a.mode = mode;
     a.tab = crc_tables(s);
     if (!a.tab) return -3;
+    a.unshift = a.tab + kCrcWords;
     static int cus = [] {
         int d = 0, n = 0;
         if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) !=
@@ -569,9 +887,19 @@ int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes
             n = 256;
         return std::max(n, 1);
     }();
-    // 28 KiB of tables per 512-thread workgroup: 4 resident per CU; each loops over rows of 16 packets
+    // one workgroup per resident slot (the LDS tables and the VGPRs decide how many fit on a CU); each loops
+    // over rows of 16 packets
+    const void *fn = !dst ? reinterpret_cast<const void *>(&seal_in_place_kernel)
+                          : open ? reinterpret_cast<const void *>(&open_kernel) : reinterpret_cast<const void *>(&seal_kernel);
+    static int per_cu[3] = {0, 0, 0};
+    int &fit = per_cu[!dst ? 0 : open ? 1 : 2];
+    if (fit == 0) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kSealBlock, 0) != hipSuccess || b < 1) b = 1;
+        fit = b;
+    }
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
-    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * 4));
+    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * fit));
     if (!dst) hipLaunchKernelGGL(seal_in_place_kernel, grid, dim3(kSealBlock), 0, s, a, open);  // checksum mode
     else if (open) hipLaunchKernelGGL(open_kernel, grid, dim3(kSealBlock), 0, s, a);
     else hipLaunchKernelGGL(seal_kernel, grid, dim3(kSealBlock), 0, s, a);

@@ -382,11 +382,13 @@ def test_seal_open_match_oracle(dev, mode):
     offsets, empty / 1-3 byte packets, corrupted packets (checksum must fail), and a full round trip."""
     from kcptube_amd.frame import open_, seal
     rng = random.Random(100 + mode)
-    pk = [b"", b"\x01", b"ab", b"abc", b"1234"] + [rng.randbytes(rng.choice([5, 1440, 1442, rng.randint(1, 1500)]))
-                                                   for _ in range(400)]
+    # register rows up to 2 KiB sealed (both sides of every 512-byte round edge), streaming rows past it
+    edges = [e + d for e in (512, 1024, 1536, 2048) for d in range(-4, 3)]
+    pk = [b"", b"\x01", b"ab", b"abc", b"1234", b"12345"] + [rng.randbytes(n) for n in edges + [3000, 4094, 4096]]
+    pk += [rng.randbytes(rng.choice([5, 1440, 1442, rng.randint(1, 1500), rng.randint(1, 4100)])) for _ in range(400)]
     src, off, lens = _arena(pk, dev)
     P = len(pk)
-    pitch = 1504
+    pitch = 4096
     d_len = torch.tensor(lens, dtype=torch.int32, device=dev)
     dst = torch.full((P, pitch), SENT, dtype=torch.uint8, device=dev)
     olen = torch.full((P,), -1, dtype=torch.int32, device=dev)
@@ -629,8 +631,9 @@ def test_seal_open_in_place(dev, mode):
     from kcptube_amd.fec import KfecError
     from kcptube_amd.frame import open_, seal
     rng = random.Random(300 + mode)
-    pitch = 1472
-    lens = [1, 2, 3, 4, 5, 1449, 1450, 1451, 1452] + [rng.randint(1, 1460) for _ in range(300)]
+    pitch = 2600
+    lens = [1, 2, 3, 4, 5, 1449, 1450, 1451, 1452, 2046, 2047, 2048, 2049, 2050, 2051, 2590, 2598]
+    lens += [rng.randint(1, 1460) for _ in range(300)] + [rng.randint(1, 2598) for _ in range(100)]
     P = len(lens)
     rows = np.zeros((P, pitch), np.uint8)
     for p, n in enumerate(lens):
