@@ -77,6 +77,15 @@ constexpr int kRowsPerBlock = kSealBlock / kRowLanes;
 #ifndef KFEC_SEAL_PREFETCH
 #define KFEC_SEAL_PREFETCH 1  // 0: no kernel prefetches the next packet (A/B knob)
 #endif
+#ifndef KFEC_SEAL_OPEN_PF
+#define KFEC_SEAL_OPEN_PF 1  // 0: open loads each packet when it reaches it (A/B knob)
+#endif
+#ifndef KFEC_SEAL_INPLACE_PF
+#define KFEC_SEAL_INPLACE_PF 0  // 1: the in-place kernel prefetches too (A/B knob)
+#endif
+#ifndef KFEC_SEAL_AB
+#define KFEC_SEAL_AB 0  // ablation (timing only, wrong results): 1 = the register rows skip the CRC
+#endif
 
 // The CRC tables each workgroup stages into LDS (60 KiB; all maps GF(2)-linear, so table lookups of the
 // input's bytes XORed together):
@@ -388,6 +397,7 @@ __device__ __forceinline__ void or_byte(uint32_t (&o)[4], int32_t pos, uint32_t 
 __device__ __forceinline__ uint32_t crc_regs(const CrcLds &tab, uint32_t u, const uint32_t (&o)[kRegRounds][4],
                                              uint32_t n, uint32_t lane)
 {
+    if (KFEC_SEAL_AB == 1) return u;
     if (n < 4) {  // the init cannot be folded into message bytes: byte by byte from lane 0's first dword
         uint32_t c = 0xFFFFFFFFu;
         for (uint32_t i = 0; i < n; ++i) c = crc_byte(tab, c, o[0][0] >> (8 * i));
@@ -713,7 +723,7 @@ __global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu
         return KFEC_SEAL_REG && valid(L) && L <= kRegBytes && row_fits(off, L, a.src_dw) ? L : 0u;
     };
     auto crc_len = [](uint32_t L) { return L - KFEC_SEAL_TRAILER; };
-    for_each_row<false>(a, lane, load_len, crc_len, [&](uint64_t p, uint32_t L, uint64_t off, uint32_t (&o)[kRegRounds][4], uint32_t u) {
+    for_each_row<KFEC_SEAL_OPEN_PF != 0>(a, lane, load_len, crc_len, [&](uint64_t p, uint32_t L, uint64_t off, uint32_t (&o)[kRegRounds][4], uint32_t u) {
         if (!valid(L)) {
             if (lane == 0) {
                 a.out_len[p] = 0;
@@ -803,7 +813,7 @@ __global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu
         return KFEC_SEAL_REG && L != 0 && L <= kRegBytes && row_fits(off, L, a.src_dw) ? L : 0u;
     };
     auto crc_len = [&](uint32_t L) { return open ? L - KFEC_SEAL_TRAILER : L; };
-    for_each_row<false>(a, lane, load_len, crc_len, [&](uint64_t p, uint32_t L, uint64_t off, uint32_t (&o)[kRegRounds][4], uint32_t u) {
+    for_each_row<KFEC_SEAL_INPLACE_PF != 0>(a, lane, load_len, crc_len, [&](uint64_t p, uint32_t L, uint64_t off, uint32_t (&o)[kRegRounds][4], uint32_t u) {
         if (!valid(L, off)) {
             if (lane == 0) {
                 a.out_len[p] = 0;
