@@ -5,7 +5,7 @@
 //     then, for plain_xor, xor_forward over data + checksum (data_operations.cpp:120-128).
 //   decrypt_data (data_operations.cpp:373-435): plain_xor first undoes xor_backward (:140-148), then the
 //     trailing two bytes are compared with checksum16 of the rest.
-// The AEAD modes (AES-GCM/OCB, (X)ChaCha20-Poly1305) need Botan, which is absent here: out of scope.
+// (The AEAD modes are kfec_aead.hip / kfec_gcm.hip / kfec_ocb.hip.)
 //
 // Half a wave per packet (see "parallel CRC-32" below): each lane owns 16-byte chunks, chunk CRCs are
 // combined with GF(2)-linear shift tables, so a packet's bytes are read with 16-byte loads by consecutive
