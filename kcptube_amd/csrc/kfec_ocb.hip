@@ -10,9 +10,8 @@
 // Offset_0 -- per iv, a 1 MiB table.  Block i's offset has a closed form, Offset_i = Offset_0 xor XOR of L_j
 // over the set bits j of gray(i) = i xor (i >> 1), so the blocks of a packet are independent: a row of 8
 // lanes per packet, lane j taking blocks j + 1, j + 9, ...; the checksum is the row's XOR of the plaintext
-// blocks, and one lane enciphers the tag.  AES runs from T-tables in LDS (Te0..Te3, and Td0..Td3 + the
-// inverse S-box for open's full blocks, the equivalent inverse cipher of FIPS 197 5.3.5), 8.5 / 13 KiB per
-// workgroup, with the round keys in LDS too (broadcast reads).
+// blocks, and one lane enciphers the tag.  AES runs from T-tables in LDS, replicated per bank so that the
+// byte-indexed reads of a row never conflict (OcbLds below), with the round keys in LDS too (broadcast reads).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -174,7 +173,7 @@ __global__ void ocb_iv_kernel(const uint32_t *key, uint4 *off0)
 
 // ---- per-packet kernel -------------------------------------------------------------------------------
 constexpr int kRow = 8;
-constexpr int kOcbBlock = 256;
+constexpr int kOcbBlock = 512;
 constexpr int kRowsPerBlock = kOcbBlock / kRow;
 
 struct OcbArgs {
@@ -192,69 +191,139 @@ struct OcbArgs {
     uint64_t P;
 };
 
-// what one workgroup stages into LDS
-struct OcbLds {
+// What one workgroup stages into LDS.  AES is LDS-bound here: 16 byte-indexed table reads per round on random
+// bytes, and with one table shared by the 32 lanes of a read (32 banks) those reads took ~2.3 LDS cycles
+// each.  Tables are kept in 32 copies laid out so that copy c sits in bank c -- row lane c reads rep[v][c],
+// and the 32 lanes of a read hit 32 different banks whatever their bytes: no conflicts.  Te2 / Te3 are Te0 /
+// Te1 rotated by 16 bits (Td likewise), so a column is T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d]) ^ k: two
+// replicated tables and one rotate per column.
+//   seal: te[j][v][c] = Te_j[v], j = 0, 1 (64 KiB).  open: td[j][v][c] = Td_j[v] (64 KiB), isb[w][c] = the
+//   inverse S-box bytes 4w .. 4w + 3 (8 KiB), and Te0 once (the pad of a partial block and the tag: at most
+//   two blocks per packet).
+constexpr int kRep = 32;
+template <bool OPEN>
+struct OcbLds;
+template <>
+struct OcbLds<false> {
     uint4 rk[15];
     uint4 dk[15];
     uint4 l[32];
-    uint32_t te[4][256];
-    uint32_t td[4][256];
-    uint32_t isb[256];
+    uint32_t te[2][256][kRep];
+};
+template <>
+struct OcbLds<true> {
+    uint4 rk[15];
+    uint4 dk[15];
+    uint4 l[32];
+    uint32_t td[2][256][kRep];
+    uint32_t isb[64][kRep];
+    uint32_t te0[256];
 };
 
 __device__ __forceinline__ uint32_t b0(uint32_t x) { return x & 0xFFu; }
 __device__ __forceinline__ uint32_t b1(uint32_t x) { return (x >> 8) & 0xFFu; }
 __device__ __forceinline__ uint32_t b2(uint32_t x) { return (x >> 16) & 0xFFu; }
 __device__ __forceinline__ uint32_t b3(uint32_t x) { return x >> 24; }
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int k) { return __builtin_amdgcn_alignbit(x, x, 32 - k); }
 
-__device__ __forceinline__ uint4 aes_enc(const OcbLds &t, uint4 in)
+// T[byte k of x][c] of a replicated table: the byte offset v * 128 + 4 c built as one shift and one and-or
+template <int K>
+__device__ __forceinline__ uint32_t rep_at(const uint32_t (*T)[kRep], uint32_t x, uint32_t c4)
+{
+    const uint32_t sh = K == 0 ? x << 7 : x >> (8 * K - 7);
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(T) + ((sh & 0x7F80u) | c4));
+}
+
+// one column of a round: T0[b0(a)] ^ T1[b1(b)] ^ rotl16(T0[b2(cc)] ^ T1[b3(d)]) ^ k
+__device__ __forceinline__ uint32_t tcol(const uint32_t (*T)[256][kRep], uint32_t c4, uint32_t a, uint32_t b, uint32_t cc,
+                                         uint32_t d, uint32_t k)
+{
+    const uint32_t hi = rep_at<2>(T[0], cc, c4) ^ rep_at<3>(T[1], d, c4);
+    return xor3(rep_at<0>(T[0], a, c4), rep_at<1>(T[1], b, c4), rotl(hi, 16)) ^ k;
+}
+
+// Te0 holds S(x) in byte 1 (Te0[x] = {2S, S, S, 3S})
+__device__ __forceinline__ uint32_t sbox_col(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3)
+{
+    return ((w0 >> 8) & 0xFFu) | (w1 & 0xFF00u) | ((w2 << 8) & 0xFF0000u) | ((w3 << 16) & 0xFF000000u);
+}
+
+// encryption from the replicated tables (seal), row lane c (c4 = 4 c)
+__device__ __forceinline__ uint4 aes_enc(const OcbLds<false> &t, uint32_t c4, uint4 in)
 {
     uint32_t s0 = in.x ^ t.rk[0].x, s1 = in.y ^ t.rk[0].y, s2 = in.z ^ t.rk[0].z, s3 = in.w ^ t.rk[0].w;
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
         const uint4 k = t.rk[r];
-        const uint32_t t0 = xor3(t.te[0][b0(s0)], t.te[1][b1(s1)], t.te[2][b2(s2)]) ^ xor3(t.te[3][b3(s3)], k.x, 0u);
-        const uint32_t t1 = xor3(t.te[0][b0(s1)], t.te[1][b1(s2)], t.te[2][b2(s3)]) ^ xor3(t.te[3][b3(s0)], k.y, 0u);
-        const uint32_t t2 = xor3(t.te[0][b0(s2)], t.te[1][b1(s3)], t.te[2][b2(s0)]) ^ xor3(t.te[3][b3(s1)], k.z, 0u);
-        const uint32_t t3 = xor3(t.te[0][b0(s3)], t.te[1][b1(s0)], t.te[2][b2(s1)]) ^ xor3(t.te[3][b3(s2)], k.w, 0u);
+        const uint32_t t0 = tcol(t.te, c4, s0, s1, s2, s3, k.x);
+        const uint32_t t1 = tcol(t.te, c4, s1, s2, s3, s0, k.y);
+        const uint32_t t2 = tcol(t.te, c4, s2, s3, s0, s1, k.z);
+        const uint32_t t3 = tcol(t.te, c4, s3, s0, s1, s2, k.w);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
-    // last round: S-box only (S(x) is byte 0 of Te2, byte 1 of Te3, byte 2 of Te0, byte 3 of Te1)
     const uint4 k = t.rk[14];
-    const uint32_t o0 = (t.te[2][b0(s0)] & 0xFFu) | (t.te[3][b1(s1)] & 0xFF00u) | (t.te[0][b2(s2)] & 0xFF0000u) |
-                        (t.te[1][b3(s3)] & 0xFF000000u);
-    const uint32_t o1 = (t.te[2][b0(s1)] & 0xFFu) | (t.te[3][b1(s2)] & 0xFF00u) | (t.te[0][b2(s3)] & 0xFF0000u) |
-                        (t.te[1][b3(s0)] & 0xFF000000u);
-    const uint32_t o2 = (t.te[2][b0(s2)] & 0xFFu) | (t.te[3][b1(s3)] & 0xFF00u) | (t.te[0][b2(s0)] & 0xFF0000u) |
-                        (t.te[1][b3(s1)] & 0xFF000000u);
-    const uint32_t o3 = (t.te[2][b0(s3)] & 0xFFu) | (t.te[3][b1(s0)] & 0xFF00u) | (t.te[0][b2(s1)] & 0xFF0000u) |
-                        (t.te[1][b3(s2)] & 0xFF000000u);
+    const uint32_t (*T)[kRep] = t.te[0];
+    const uint32_t o0 = sbox_col(rep_at<0>(T, s0, c4), rep_at<1>(T, s1, c4), rep_at<2>(T, s2, c4), rep_at<3>(T, s3, c4));
+    const uint32_t o1 = sbox_col(rep_at<0>(T, s1, c4), rep_at<1>(T, s2, c4), rep_at<2>(T, s3, c4), rep_at<3>(T, s0, c4));
+    const uint32_t o2 = sbox_col(rep_at<0>(T, s2, c4), rep_at<1>(T, s3, c4), rep_at<2>(T, s0, c4), rep_at<3>(T, s1, c4));
+    const uint32_t o3 = sbox_col(rep_at<0>(T, s3, c4), rep_at<1>(T, s0, c4), rep_at<2>(T, s1, c4), rep_at<3>(T, s2, c4));
     return make_uint4(o0 ^ k.x, o1 ^ k.y, o2 ^ k.z, o3 ^ k.w);
 }
 
-__device__ __forceinline__ uint4 aes_dec(const OcbLds &t, uint4 in)
+// encryption from the single Te0 (open: the partial block's pad and the tag only)
+__device__ __forceinline__ uint4 aes_enc(const OcbLds<true> &t, uint32_t, uint4 in)
+{
+    const uint32_t *T = t.te0;
+    uint32_t s0 = in.x ^ t.rk[0].x, s1 = in.y ^ t.rk[0].y, s2 = in.z ^ t.rk[0].z, s3 = in.w ^ t.rk[0].w;
+#pragma unroll 1
+    for (int r = 1; r < 14; ++r) {
+        const uint4 k = t.rk[r];
+        const uint32_t t0 = xor3(T[b0(s0)], rotl(T[b1(s1)], 8), rotl(T[b2(s2)], 16)) ^ xor3(rotl(T[b3(s3)], 24), k.x, 0u);
+        const uint32_t t1 = xor3(T[b0(s1)], rotl(T[b1(s2)], 8), rotl(T[b2(s3)], 16)) ^ xor3(rotl(T[b3(s0)], 24), k.y, 0u);
+        const uint32_t t2 = xor3(T[b0(s2)], rotl(T[b1(s3)], 8), rotl(T[b2(s0)], 16)) ^ xor3(rotl(T[b3(s1)], 24), k.z, 0u);
+        const uint32_t t3 = xor3(T[b0(s3)], rotl(T[b1(s0)], 8), rotl(T[b2(s1)], 16)) ^ xor3(rotl(T[b3(s2)], 24), k.w, 0u);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint4 k = t.rk[14];
+    const uint32_t o0 = sbox_col(T[b0(s0)], T[b1(s1)], T[b2(s2)], T[b3(s3)]);
+    const uint32_t o1 = sbox_col(T[b0(s1)], T[b1(s2)], T[b2(s3)], T[b3(s0)]);
+    const uint32_t o2 = sbox_col(T[b0(s2)], T[b1(s3)], T[b2(s0)], T[b3(s1)]);
+    const uint32_t o3 = sbox_col(T[b0(s3)], T[b1(s0)], T[b2(s1)], T[b3(s2)]);
+    return make_uint4(o0 ^ k.x, o1 ^ k.y, o2 ^ k.z, o3 ^ k.w);
+}
+
+// inverse S-box byte K of x from the replicated packed table
+template <int K>
+__device__ __forceinline__ uint32_t isb(const OcbLds<true> &t, uint32_t c4, uint32_t x)
+{
+    const uint32_t v = (x >> (8 * K)) & 0xFFu;
+    return (t.isb[v >> 2][c4 >> 2] >> (8 * (v & 3u))) & 0xFFu;
+}
+
+// the equivalent inverse cipher (FIPS 197 5.3.5) from the replicated Td0 / Td1, row lane c (c4 = 4 c)
+__device__ __forceinline__ uint4 aes_dec(const OcbLds<true> &t, uint32_t c4, uint4 in)
 {
     uint32_t s0 = in.x ^ t.dk[0].x, s1 = in.y ^ t.dk[0].y, s2 = in.z ^ t.dk[0].z, s3 = in.w ^ t.dk[0].w;
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
         const uint4 k = t.dk[r];
         // InvShiftRows: output column c row r takes input column c - r
-        const uint32_t t0 = xor3(t.td[0][b0(s0)], t.td[1][b1(s3)], t.td[2][b2(s2)]) ^ xor3(t.td[3][b3(s1)], k.x, 0u);
-        const uint32_t t1 = xor3(t.td[0][b0(s1)], t.td[1][b1(s0)], t.td[2][b2(s3)]) ^ xor3(t.td[3][b3(s2)], k.y, 0u);
-        const uint32_t t2 = xor3(t.td[0][b0(s2)], t.td[1][b1(s1)], t.td[2][b2(s0)]) ^ xor3(t.td[3][b3(s3)], k.z, 0u);
-        const uint32_t t3 = xor3(t.td[0][b0(s3)], t.td[1][b1(s2)], t.td[2][b2(s1)]) ^ xor3(t.td[3][b3(s0)], k.w, 0u);
+        const uint32_t t0 = tcol(t.td, c4, s0, s3, s2, s1, k.x);
+        const uint32_t t1 = tcol(t.td, c4, s1, s0, s3, s2, k.y);
+        const uint32_t t2 = tcol(t.td, c4, s2, s1, s0, s3, k.z);
+        const uint32_t t3 = tcol(t.td, c4, s3, s2, s1, s0, k.w);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     const uint4 k = t.dk[14];
-    const uint32_t o0 = t.isb[b0(s0)] | t.isb[b1(s3)] << 8 | t.isb[b2(s2)] << 16 | t.isb[b3(s1)] << 24;
-    const uint32_t o1 = t.isb[b0(s1)] | t.isb[b1(s0)] << 8 | t.isb[b2(s3)] << 16 | t.isb[b3(s2)] << 24;
-    const uint32_t o2 = t.isb[b0(s2)] | t.isb[b1(s1)] << 8 | t.isb[b2(s0)] << 16 | t.isb[b3(s3)] << 24;
-    const uint32_t o3 = t.isb[b0(s3)] | t.isb[b1(s2)] << 8 | t.isb[b2(s1)] << 16 | t.isb[b3(s0)] << 24;
+    const uint32_t o0 = isb<0>(t, c4, s0) | isb<1>(t, c4, s3) << 8 | isb<2>(t, c4, s2) << 16 | isb<3>(t, c4, s1) << 24;
+    const uint32_t o1 = isb<0>(t, c4, s1) | isb<1>(t, c4, s0) << 8 | isb<2>(t, c4, s3) << 16 | isb<3>(t, c4, s2) << 24;
+    const uint32_t o2 = isb<0>(t, c4, s2) | isb<1>(t, c4, s1) << 8 | isb<2>(t, c4, s0) << 16 | isb<3>(t, c4, s3) << 24;
+    const uint32_t o3 = isb<0>(t, c4, s3) | isb<1>(t, c4, s2) << 8 | isb<2>(t, c4, s1) << 16 | isb<3>(t, c4, s0) << 24;
     return make_uint4(o0 ^ k.x, o1 ^ k.y, o2 ^ k.z, o3 ^ k.w);
 }
 
-// Offset_i = Offset_0 xor XOR_{j in gray(i)} L_j
-__device__ __forceinline__ uint4 ocb_offset(const OcbLds &t, uint4 o0, uint32_t i)
+template <class Lds>
+__device__ __forceinline__ uint4 ocb_offset(const Lds &t, uint4 o0, uint32_t i)
 {
     uint32_t g = i ^ (i >> 1);
     while (g) {
@@ -267,24 +336,34 @@ __device__ __forceinline__ uint4 ocb_offset(const OcbLds &t, uint4 o0, uint32_t 
 template <bool OPEN>
 __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
 {
-    __shared__ OcbLds s;
+    __shared__ OcbLds<OPEN> s;
     {
-        // stage the round keys, L values and tables (open also needs the decryption half)
+        // stage the round keys, L values and tables (open: the decryption half and Te0 once)
         const uint32_t *k32 = reinterpret_cast<const uint32_t *>(a.key);
         uint32_t *s32 = reinterpret_cast<uint32_t *>(&s);
-        constexpr int kKeys = (int)(offsetof(OcbLds, te) / 4);
+        constexpr int kKeys = (int)(offsetof(OcbLds<OPEN>, l) / 4) + 32 * 4;
         for (int i = threadIdx.x; i < kKeys; i += kOcbBlock) {
             // OcbLds: rk, dk, l -- OcbKey: rk, dk, lstar, ldollar, l
             const int src = i < 120 ? i : i + 8;
             s32[i] = k32[src];
         }
-        const int nt = OPEN ? 4 * 256 + 4 * 256 + 256 : 4 * 256;
-        const uint32_t *kt = reinterpret_cast<const uint32_t *>(&a.key->te[0][0]);
-        for (int i = threadIdx.x; i < nt; i += kOcbBlock) s32[kKeys + i] = kt[i];
+        if constexpr (OPEN) {
+            for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
+                s.td[i / (256 * kRep)][i / kRep % 256][i % kRep] = a.key->td[i / (256 * kRep)][i / kRep % 256];
+            for (int i = threadIdx.x; i < 64 * kRep; i += kOcbBlock) {
+                const int w = i / kRep;
+                s.isb[w][i % kRep] = a.key->isb[4 * w] | a.key->isb[4 * w + 1] << 8 | a.key->isb[4 * w + 2] << 16 |
+                                     a.key->isb[4 * w + 3] << 24;
+            }
+            for (int i = threadIdx.x; i < 256; i += kOcbBlock) s.te0[i] = a.key->te[0][i];
+        } else {
+            for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
+                s.te[i / (256 * kRep)][i / kRep % 256][i % kRep] = a.key->te[i / (256 * kRep)][i / kRep % 256];
+        }
         __syncthreads();
     }
     const uint4 lstar = a.key->lstar, ldollar = a.key->ldollar, sad = a.key->sad;
-    const uint32_t lane = threadIdx.x % kRow;
+    const uint32_t lane = threadIdx.x % kRow, c = 4 * (threadIdx.x % kRep);  // c: this lane's table copy, in bytes
     for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRow; p < a.P;
          p += (uint64_t)gridDim.x * kRowsPerBlock) {
         const uint32_t L = a.len[p];
@@ -321,16 +400,16 @@ __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
             if (i <= m) {
                 const uint4 oi = ocb_offset(s, o0, i);
                 uint4 out;
-                if (OPEN) {
-                    out = u4_xor(aes_dec(s, u4_xor(in, oi)), oi);
+                if constexpr (OPEN) {
+                    out = u4_xor(aes_dec(s, c, u4_xor(in, oi)), oi);
                     sum = u4_xor(sum, out);
                 } else {
-                    out = u4_xor(aes_enc(s, u4_xor(in, oi)), oi);
+                    out = u4_xor(aes_enc(s, c, u4_xor(in, oi)), oi);
                     sum = u4_xor(sum, in);
                 }
                 *reinterpret_cast<uint4 *>(d32) = out;
             } else {  // the partial last block: Pad = E_K(Offset_m xor L_*)
-                const uint4 pad = aes_enc(s, u4_xor(ocb_offset(s, o0, m), lstar));
+                const uint4 pad = aes_enc(s, c, u4_xor(ocb_offset(s, o0, m), lstar));
                 in = mask16(in, rem);
                 const uint4 out = mask16(u4_xor(in, pad), rem);
                 uint4 pt = OPEN ? out : in;
@@ -361,7 +440,7 @@ __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
         uint4 fo = ocb_offset(s, o0, m);
         if (rem) fo = u4_xor(fo, lstar);
         uint4 tg = make_uint4(0u, 0u, 0u, 0u);
-        if (lane == 0) tg = u4_xor(aes_enc(s, u4_xor(u4_xor(sum, fo), ldollar)), sad);
+        if (lane == 0) tg = u4_xor(aes_enc(s, c, u4_xor(u4_xor(sum, fo), ldollar)), sad);
         const uint32_t tag[4] = {__shfl(tg.x, 0, kRow), __shfl(tg.y, 0, kRow), __shfl(tg.z, 0, kRow),
                                  __shfl(tg.w, 0, kRow)};
         if (OPEN) {
@@ -431,8 +510,16 @@ int launch_ocb(const kfec_aead *k, bool open, size_t P, const void *src, size_t 
             n = 256;
         return std::max(n, 1);
     }();
+    // one workgroup per resident slot (LDS tables and VGPRs decide how many fit on a CU)
+    static int fit[2] = {0, 0};
+    if (!fit[open]) {
+        int b = 0;
+        const void *fn = open ? reinterpret_cast<const void *>(&ocb_kernel<true>) : reinterpret_cast<const void *>(&ocb_kernel<false>);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kOcbBlock, 0) != hipSuccess || b < 1) b = 1;
+        fit[open] = b;
+    }
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
-    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * 8));
+    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * fit[open]));
     if (open) hipLaunchKernelGGL(ocb_kernel<true>, grid, dim3(kOcbBlock), 0, s, a);
     else hipLaunchKernelGGL(ocb_kernel<false>, grid, dim3(kOcbBlock), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
