@@ -808,9 +808,11 @@ __global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu
         return open ? L > KFEC_SEAL_TRAILER
                     : L != 0 && (uint64_t)L + KFEC_SEAL_TRAILER <= a.dst_pitch && off + L + KFEC_SEAL_TRAILER <= a.src_bytes;
     };
-    // open keeps the trailer in the registers too (a load of it after the prefetch would wait for the prefetch)
+    // the bytes under the checksum go to the registers; open reads the trailer with one more load
     auto load_len = [&](uint32_t L, uint64_t off) {
-        return KFEC_SEAL_REG && L != 0 && L <= kRegBytes && row_fits(off, L, a.src_dw) ? L : 0u;
+        const uint32_t n = open ? L - KFEC_SEAL_TRAILER : L;
+        return KFEC_SEAL_REG && L > (open ? KFEC_SEAL_TRAILER : 0u) && n <= kRegBytes && row_fits(off, n, a.src_dw) ? n
+                                                                                                                 : 0u;
     };
     auto crc_len = [&](uint32_t L) { return open ? L - KFEC_SEAL_TRAILER : L; };
     for_each_row<KFEC_SEAL_INPLACE_PF != 0>(a, lane, load_len, crc_len, [&](uint64_t p, uint32_t L, uint64_t off, uint32_t (&o)[kRegRounds][4], uint32_t u) {
@@ -824,15 +826,12 @@ __global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu
         const uint32_t n = crc_len(L);  // bytes under the checksum
         uint32_t cs, trailer = 0;
         if (load_len(L, off)) {
-            if (!open) mask_tail(o, n, lane);
-            if (open) {
-                trailer = row_trailer(o, n, lane);
-#pragma unroll
-                for (int r = 0; r < kRegRounds; ++r) {
-                    const int32_t q0 = (int32_t)(r * kCrcRound + kCrcLane * lane);
-                    if ((int32_t)n < q0 + 16) mask_chunk(o[r], q0, n);
-                }
+            if (open) {  // bytes n, n + 1: the dwords holding them lie inside the packet, so inside the buffer
+                const uint32_t *b32 = a.src;
+                const uint32_t w0 = b32[(off + n) >> 2], w1 = b32[(off + n + 1) >> 2];
+                trailer = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)((off + n) & 3u)) & 0xFFFFu;
             }
+            mask_tail(o, n, lane);
             cs = checksum16(crc_regs(s_tab, u, o, n, lane));
         } else {
             cs = checksum16(row_crc32(s_tab, a.src, a.src_dw, off, n, lane));
