@@ -1151,17 +1151,34 @@ __global__ void __launch_bounds__(kMacBlock) syn_list_kernel(SynArgs a)
     }
 }
 
+#ifndef KFEC_SYN_WAVE_CT
+#define KFEC_SYN_WAVE_CT 1  // 0: one set of C tables per workgroup behind a workgroup barrier (A/B knob)
+#endif
+// groups one wave of 64 consecutive items can touch
+__host__ __device__ constexpr uint32_t syn_wave_groups(size_t cols) { return (uint32_t)(63 / (cols ? cols : 1) + 2); }
+
 template <int VEC, int RT, int PDX = 0>
 __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a)
 {
     constexpr int W = Gran<VEC>::W;
     constexpr int PD = PDX ? PDX : (VEC >= 32 ? KFEC_PD : 2 * KFEC_PD);
     constexpr int TD = SynLayout<RT>::TD;
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_ct[];  // [group slot][RT][TD]
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ct[];  // [wave][group slot][RT][TD] or [group slot][RT][TD]
     if (syn_listed(a, *a.list_count)) return;  // the listed kernel has it (whole workgroup)
     const uint32_t base = blockIdx.x * kMacBlock;
     const uint32_t cols = a.cols, K = a.K;
     const uint32_t gfirst = base / cols;
+#if KFEC_SYN_WAVE_CT
+    // C tables of the groups this wave touches, built and read by this wave only: no workgroup barrier, so a
+    // wave that finishes its shards does not wait for the slowest wave of the workgroup
+    const uint32_t wbase = min(base + (threadIdx.x & ~63u), a.total - 1);
+    const uint32_t wfirst = wbase / cols, wlast = min(wbase + 63, a.total - 1) / cols;
+    uint32_t *ctw = s_ct + (threadIdx.x / 64) * syn_wave_groups(cols) * RT * TD;
+    for (uint32_t e = threadIdx.x & 63u; e < (wlast - wfirst + 1) * RT * RT; e += 64) {
+        const uint32_t gs = e / (RT * RT);
+        syn_expand_one<RT>(a.rec + (uint64_t)(wfirst + gs) * a.rec_stride, e - gs * (RT * RT), ctw + gs * RT * TD);
+    }
+#else
     const uint32_t glast = min(base + kMacBlock - 1, a.total - 1) / cols;
     const uint32_t ng = glast - gfirst + 1;
     // C tables of the workgroup's groups
@@ -1169,6 +1186,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
         const uint32_t gs = e / (RT * RT);
         syn_expand_one<RT>(a.rec + (uint64_t)(gfirst + gs) * a.rec_stride, e - gs * (RT * RT), s_ct + gs * RT * TD);
     }
+#endif
     const uint32_t item = base + threadIdx.x;
     const bool in = item < a.total;
     const uint32_t g = in ? item / cols : gfirst;
@@ -1190,15 +1208,23 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
     uint32_t acc[RT][W];
     if (active) {
         // resources over this workgroup's groups (wave-uniform: blockIdx and kernel arguments only)
+        const uint32_t ngr = min(base + kMacBlock - 1, a.total - 1) / cols - gfirst + 1;
         const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(a.data + (uint64_t)gfirst * K * a.pitch), (short)0, (int)(ng * K * a.pitch), 0x00020000);
+            (void *)(a.data + (uint64_t)gfirst * K * a.pitch), (short)0, (int)(ngr * K * a.pitch), 0x00020000);
         const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(a.parity + (uint64_t)gfirst * a.R * a.pitch), (short)0, (int)(ng * a.R * a.pitch), 0x00020000);
+            (void *)(a.parity + (uint64_t)gfirst * a.R * a.pitch), (short)0, (int)(ngr * a.R * a.pitch), 0x00020000);
         syn_loop<VEC, RT, PD>(a, acc, rd, rp, gs * K * (uint32_t)a.pitch + off, gs * a.R * (uint32_t)a.pitch + off, used,
                               p0, rec);
     }
+#if KFEC_SYN_WAVE_CT
+    // written by lanes of this wave: LDS operations of one wave complete in order; the fence keeps the
+    // compiler from moving the reads above the writes
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (active) syn_final<VEC, RT>(a, acc, ctw + (g - wfirst) * RT * TD, m, g, off, col);
+#else
     __syncthreads();  // C tables
     if (active) syn_final<VEC, RT>(a, acc, s_ct + gs * RT * TD, m, g, off, col);
+#endif
 }
 
 // ---- ordered list of the groups with data to recover (out_idx[g * R] != 0xFF), for syn_kernel's listed
@@ -1516,7 +1542,8 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     // per workgroup)
     const int rt = syn_rt(R);
     const size_t gmax_syn = std::min<size_t>(G, (kMacBlock - 1) / std::max<size_t>(cols, 1) + 2);
-    const size_t lds_syn = gmax_syn * (size_t)rt * syn_td(rt) * 4;
+    const size_t lds_syn = (KFEC_SYN_WAVE_CT ? (size_t)(kMacBlock / 64) * syn_wave_groups(cols) : gmax_syn) *
+                           (size_t)rt * syn_td(rt) * 4;
     // (syndrome form: whole-dword granules, and each workgroup's groups must fit one buffer resource)
     const bool syn = R > 0 && R <= KFEC_SYN_MAX_R && lds_syn <= kSynLdsMax && vec != 1 &&
                      gmax_syn * (size_t)K * pitch < (size_t(1) << 31) && gmax_syn * (size_t)R * pitch < (size_t(1) << 31) &&
