@@ -699,3 +699,40 @@ def test_seal_in_place_respects_slots_and_buffer_end(dev):
     assert set(changed) <= allowed  # only trailers of the packets that fit
     with pytest.raises(KfecError):
         seal(0, flat, off, d_len, None, ol, slot=0)
+
+
+@pytest.mark.parametrize("mode", [fo.SEAL_CHECKSUM, fo.SEAL_PLAIN_XOR])
+def test_seal_open_packet_at_buffer_end(dev, mode):
+    """A packet that ends exactly at the end of src (whose 16-byte windows would run past the buffer) takes the
+    streaming rows; its neighbours take the register rows: all byte-exact vs the oracle, at every alignment."""
+    from kcptube_amd.frame import open_, seal
+    rng = random.Random(700 + mode)
+    for L in (1, 3, 4, 5, 17, 100, 511, 513, 1449, 2046, 2047):
+        for lead in range(4):
+            pk = [rng.randbytes(rng.randint(1, 1500)) for _ in range(5)] + [rng.randbytes(L)]
+            src, off, lens = _arena(pk, dev)
+            end = int(off[-1].item()) + L + lead  # the buffer ends `lead` bytes after the last packet
+            src = src[:end]
+            pitch = 2056
+            d_len = torch.tensor(lens, dtype=torch.int32, device=dev)
+            dst = torch.full((len(pk), pitch), SENT, dtype=torch.uint8, device=dev)
+            olen = torch.full((len(pk),), -1, dtype=torch.int32, device=dev)
+            seal(mode, src, off, d_len, dst, olen)
+            torch.cuda.synchronize()
+            sealed = []
+            for p, d in enumerate(pk):
+                exp = fo.seal(d, mode)
+                assert int(olen[p]) == len(exp), (L, lead, p)
+                assert dst[p, :len(exp)].cpu().numpy().tobytes() == exp, (L, lead, p)
+                sealed.append(exp)
+            # open, with the last sealed packet ending at the end of its buffer
+            src2, off2, lens2 = _arena(sealed, dev)
+            src2 = src2[:int(off2[-1].item()) + len(sealed[-1]) + lead]
+            dst2 = torch.full((len(pk), pitch), SENT, dtype=torch.uint8, device=dev)
+            olen2 = torch.full((len(pk),), -1, dtype=torch.int32, device=dev)
+            ok = torch.full((len(pk),), 7, dtype=torch.uint8, device=dev)
+            open_(mode, src2, off2, torch.tensor(lens2, dtype=torch.int32, device=dev), dst2, olen2, ok)
+            torch.cuda.synchronize()
+            for p, d in enumerate(pk):
+                assert int(ok[p]) == 1 and int(olen2[p]) == len(d), (L, lead, p)
+                assert dst2[p, :len(d)].cpu().numpy().tobytes() == d, (L, lead, p)
