@@ -1164,7 +1164,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
     constexpr int PD = PDX ? PDX : (VEC >= 32 ? KFEC_PD : 2 * KFEC_PD);
     constexpr int TD = SynLayout<RT>::TD;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ct[];  // [wave][group slot][RT][TD] or [group slot][RT][TD]
-    if (syn_listed(a, *a.list_count)) return;  // the listed kernel has it (whole workgroup)
+    if (a.list_count && syn_listed(a, *a.list_count)) return;  // the listed kernel has it (whole workgroup)
     const uint32_t base = blockIdx.x * kMacBlock;
     const uint32_t cols = a.cols, K = a.K;
     const uint32_t gfirst = base / cols;
@@ -1409,6 +1409,7 @@ static int run_syn(SynArgs a, size_t lds, int cus, hipStream_t s)
 {
     const uint32_t nb = (a.total + kMacBlock - 1) / kMacBlock;
     hipLaunchKernelGGL((syn_kernel<VEC, RT, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), lds, s, a);
+    if (!a.list_count) return hipGetLastError() == hipSuccess ? 0 : -3;  // dense only
     // the listed shape: persistent, ~8 workgroups per CU, at most one wave per (group, 64 columns) task
     const uint64_t tasks = (uint64_t)a.G * (a.cols_pad / 64);
     const uint32_t nl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((tasks + 3) / 4, (uint64_t)std::max(cus, 1) * 8));
@@ -1558,13 +1559,18 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         const size_t lds = lds_syn;
         return for_group_ranges(G, cols, 1, [&](size_t g0, size_t gn) {
             // the ordered list of this launch's groups with data to recover, and its length, on the device
+            // (not for the latency shape's few groups: there the dense kernel alone runs, two launches fewer
+            // per decode call plus the listed kernel's)
+            const bool small = gn <= kLatencyGroups;
             const uint32_t nch = (uint32_t)((gn + kActChunk - 1) / kActChunk);
             const uint8_t *oi = d_out_idx + g0 * R;
-            hipLaunchKernelGGL(active_count_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)gn, (uint32_t)R, oi, chunk_cnt);
-            hipLaunchKernelGGL(active_scan_kernel, dim3(1), dim3(kBlock), 0, s, nch, chunk_cnt, count);
-            hipLaunchKernelGGL(active_scatter_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)gn, (uint32_t)R, oi,
-                               (const uint32_t *)chunk_cnt, list);
-            if (hipGetLastError() != hipSuccess) return -3;
+            if (!small) {
+                hipLaunchKernelGGL(active_count_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)gn, (uint32_t)R, oi, chunk_cnt);
+                hipLaunchKernelGGL(active_scan_kernel, dim3(1), dim3(kBlock), 0, s, nch, chunk_cnt, count);
+                hipLaunchKernelGGL(active_scatter_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)gn, (uint32_t)R, oi,
+                                   (const uint32_t *)chunk_cnt, list);
+                if (hipGetLastError() != hipSuccess) return -3;
+            }
             SynArgs a{};
             a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
             a.parity = static_cast<const uint8_t *>(d_parity) + g0 * R * pitch;
@@ -1572,7 +1578,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
             a.rec = rec + g0 * rs;
             a.etab = reinterpret_cast<const uint32_t *>(d_enc + enc_tab_offset(K, N));
             a.list = list;
-            a.list_count = count;
+            a.list_count = small ? nullptr : count;  // nullptr: dense only (syn_kernel runs, no listed launch)
             a.etab_rows = (uint32_t)enc_tab_rows(R);
             a.pitch = pitch;
             a.total = (uint32_t)(gn * cols);
