@@ -197,7 +197,7 @@ struct OcbArgs {
 // and the 32 lanes of a read hit 32 different banks whatever their bytes: no conflicts.  Te2 / Te3 are Te0 /
 // Te1 rotated by 16 bits (Td likewise), so a column is T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d]) ^ k: two
 // replicated tables and one rotate per column.
-//   seal: te[j][v][c] = Te_j[v], j = 0, 1 (64 KiB).  open: td[j][v][c] = Td_j[v] (64 KiB), isb[w][c] = the
+//   seal: te[v][j][c] = Te_j[v], j = 0, 1 (64 KiB).  open: td[v][j][c] = Td_j[v] (64 KiB), isb[w][c] = the
 //   inverse S-box bytes 4w .. 4w + 3 (8 KiB), and Te0 once (the pad of a partial block and the tag: at most
 //   two blocks per packet).
 constexpr int kRep = 32;
@@ -208,14 +208,14 @@ struct OcbLds<false> {
     uint4 rk[15];
     uint4 dk[15];
     uint4 l[32];
-    uint32_t te[2][256][kRep];
+    uint32_t te[256][2][kRep];  // row v: the 32 copies of Te0[v], then of Te1[v] (256 B)
 };
 template <>
 struct OcbLds<true> {
     uint4 rk[15];
     uint4 dk[15];
     uint4 l[32];
-    uint32_t td[2][256][kRep];
+    uint32_t td[256][2][kRep];
     uint32_t isb[64][kRep];
     uint32_t te0[256];
 };
@@ -226,20 +226,22 @@ __device__ __forceinline__ uint32_t b2(uint32_t x) { return (x >> 16) & 0xFFu; }
 __device__ __forceinline__ uint32_t b3(uint32_t x) { return x >> 24; }
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int k) { return __builtin_amdgcn_alignbit(x, x, 32 - k); }
 
-// T[byte k of x][c] of a replicated table: the byte offset v * 128 + 4 c built as one shift and one and-or
-template <int K>
-__device__ __forceinline__ uint32_t rep_at(const uint32_t (*T)[kRep], uint32_t x, uint32_t c4)
+// Table J's copy c of entry (byte K of x): a row is 256 bytes, so the byte offset is byte K of x in bits 8..15
+// and 4 c (< 128) in bits 0..7 -- one v_perm_b32 (the shift-and-or form was two VALU ops per read) -- plus
+// 128 J, the read's immediate offset
+template <int J, int K>
+__device__ __forceinline__ uint32_t rep_at(const uint32_t (*T)[2][kRep], uint32_t x, uint32_t c4)
 {
-    const uint32_t sh = K == 0 ? x << 7 : x >> (8 * K - 7);
-    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(T) + ((sh & 0x7F80u) | c4));
+    const uint32_t o = __builtin_amdgcn_perm(x, c4, 0x0C0C0000u | ((4u + K) << 8));
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(T) + o + 128 * J);
 }
 
 // one column of a round: T0[b0(a)] ^ T1[b1(b)] ^ rotl16(T0[b2(cc)] ^ T1[b3(d)]) ^ k
-__device__ __forceinline__ uint32_t tcol(const uint32_t (*T)[256][kRep], uint32_t c4, uint32_t a, uint32_t b, uint32_t cc,
+__device__ __forceinline__ uint32_t tcol(const uint32_t (*T)[2][kRep], uint32_t c4, uint32_t a, uint32_t b, uint32_t cc,
                                          uint32_t d, uint32_t k)
 {
-    const uint32_t hi = rep_at<2>(T[0], cc, c4) ^ rep_at<3>(T[1], d, c4);
-    return xor3(rep_at<0>(T[0], a, c4), rep_at<1>(T[1], b, c4), rotl(hi, 16)) ^ k;
+    const uint32_t hi = rep_at<0, 2>(T, cc, c4) ^ rep_at<1, 3>(T, d, c4);
+    return xor3(rep_at<0, 0>(T, a, c4), rep_at<1, 1>(T, b, c4), rotl(hi, 16)) ^ k;
 }
 
 // Te0 holds S(x) in byte 1 (Te0[x] = {2S, S, S, 3S})
@@ -262,11 +264,11 @@ __device__ __forceinline__ uint4 aes_enc(const OcbLds<false> &t, uint32_t c4, ui
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     const uint4 k = t.rk[14];
-    const uint32_t (*T)[kRep] = t.te[0];
-    const uint32_t o0 = sbox_col(rep_at<0>(T, s0, c4), rep_at<1>(T, s1, c4), rep_at<2>(T, s2, c4), rep_at<3>(T, s3, c4));
-    const uint32_t o1 = sbox_col(rep_at<0>(T, s1, c4), rep_at<1>(T, s2, c4), rep_at<2>(T, s3, c4), rep_at<3>(T, s0, c4));
-    const uint32_t o2 = sbox_col(rep_at<0>(T, s2, c4), rep_at<1>(T, s3, c4), rep_at<2>(T, s0, c4), rep_at<3>(T, s1, c4));
-    const uint32_t o3 = sbox_col(rep_at<0>(T, s3, c4), rep_at<1>(T, s0, c4), rep_at<2>(T, s1, c4), rep_at<3>(T, s2, c4));
+    const uint32_t (*T)[2][kRep] = t.te;
+    const uint32_t o0 = sbox_col(rep_at<0, 0>(T, s0, c4), rep_at<0, 1>(T, s1, c4), rep_at<0, 2>(T, s2, c4), rep_at<0, 3>(T, s3, c4));
+    const uint32_t o1 = sbox_col(rep_at<0, 0>(T, s1, c4), rep_at<0, 1>(T, s2, c4), rep_at<0, 2>(T, s3, c4), rep_at<0, 3>(T, s0, c4));
+    const uint32_t o2 = sbox_col(rep_at<0, 0>(T, s2, c4), rep_at<0, 1>(T, s3, c4), rep_at<0, 2>(T, s0, c4), rep_at<0, 3>(T, s1, c4));
+    const uint32_t o3 = sbox_col(rep_at<0, 0>(T, s3, c4), rep_at<0, 1>(T, s0, c4), rep_at<0, 2>(T, s1, c4), rep_at<0, 3>(T, s2, c4));
     return make_uint4(o0 ^ k.x, o1 ^ k.y, o2 ^ k.z, o3 ^ k.w);
 }
 
@@ -349,7 +351,7 @@ __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
         }
         if constexpr (OPEN) {
             for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
-                s.td[i / (256 * kRep)][i / kRep % 256][i % kRep] = a.key->td[i / (256 * kRep)][i / kRep % 256];
+                s.td[i / (2 * kRep)][i / kRep % 2][i % kRep] = a.key->td[i / kRep % 2][i / (2 * kRep)];
             for (int i = threadIdx.x; i < 64 * kRep; i += kOcbBlock) {
                 const int w = i / kRep;
                 s.isb[w][i % kRep] = a.key->isb[4 * w] | a.key->isb[4 * w + 1] << 8 | a.key->isb[4 * w + 2] << 16 |
@@ -358,7 +360,7 @@ __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
             for (int i = threadIdx.x; i < 256; i += kOcbBlock) s.te0[i] = a.key->te[0][i];
         } else {
             for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
-                s.te[i / (256 * kRep)][i / kRep % 256][i % kRep] = a.key->te[i / (256 * kRep)][i / kRep % 256];
+                s.te[i / (2 * kRep)][i / kRep % 2][i % kRep] = a.key->te[i / kRep % 2][i / (2 * kRep)];
         }
         __syncthreads();
     }
