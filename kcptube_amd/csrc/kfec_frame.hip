@@ -117,10 +117,62 @@ __device__ __forceinline__ uint32_t row_in_block() { return threadIdx.x / kRowLa
 // Write dwords [0, nd) of one row: an H-byte header followed by payload bytes [0, len) of base[start..],
 // zero after the payload.  Lane l of the row's 32 writes 16-byte chunks l, l + 32, ...; a row's last chunk, when it is
 // partial, is written dword by dword so that nothing past dword nd is touched.
+#ifndef KFEC_FRAME_REG
+#define KFEC_FRAME_REG 1  // 0: every row streams round by round (A/B knob)
+#endif
+constexpr uint32_t kQuadRounds = 4;  // rows of up to 2 KiB are loaded whole (every kcptube slot and packet)
+
+__device__ uint4 g_zero16;  // never written: the target of the loads a lane does not need
+
+// payload_quad without a branch: both loads are always issued (a chunk without payload reads g_zero16), so
+// the loads of all the rounds of a row are in flight together.  A load under a branch is waited for at the
+// join (its value is a phi there), which kept one round per row in flight.  The caller checks that every
+// window lies inside the buffer.
+__device__ __forceinline__ void payload_quad_nb(const uint32_t *base32, uint64_t start, uint32_t len, int32_t q0,
+                                                uint32_t (&o)[4])
+{
+    const int lo = max(0, -q0), hi = min(16, (int32_t)len - q0);  // payload bytes [lo, hi) of the chunk
+    const bool any = hi > lo;
+    const uint64_t a4 = start + (uint64_t)(int64_t)(q0 + 16);
+    const uint64_t w4 = a4 >> 2;
+    const uint32_t sh = (uint32_t)(a4 & 3u);
+    const uint4 x = *(any ? reinterpret_cast<const uint4 *>(base32 + (w4 - 4)) : &g_zero16);
+    const uint32_t x4 = *(any && sh ? base32 + w4 : &g_zero16.x);
+    const uint32_t d[5] = {x.x, x.y, x.z, x.w, x4};
+    const uint32_t M = any ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t nib = (M >> (4 * i)) & 0xFu;
+        o[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) & (((nib * 0x00204081u) & 0x01010101u) * 0xFFu);
+    }
+}
+
 __device__ __forceinline__ void store_quads(uint32_t *__restrict__ dst, uint32_t nd, const uint32_t (&h)[4], uint32_t H,
                                             const uint32_t *__restrict__ base, uint64_t lim32, uint64_t start,
                                             uint32_t len, uint32_t lane)
 {
+    if (KFEC_FRAME_REG && nd <= 4 * kRowLanes * kQuadRounds && start >= H && ((start + len + 15) >> 2) + 1 <= lim32) {
+        uint32_t o[kQuadRounds][4];
+#pragma unroll
+        for (uint32_t r = 0; r < kQuadRounds; ++r)
+            payload_quad_nb(base, start, len, (int32_t)(16 * (r * kRowLanes + lane)) - (int32_t)H, o[r]);
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[0][i] |= header_dword(h, H, i);
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kQuadRounds; ++r) {
+            const uint32_t j = r * kRowLanes + lane;
+            if (4 * j + 4 <= nd) {
+                *reinterpret_cast<uint4 *>(dst + 4 * j) = make_uint4(o[r][0], o[r][1], o[r][2], o[r][3]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (4 * j + i < nd) dst[4 * j + i] = o[r][i];
+            }
+        }
+        return;
+    }
     for (uint32_t j = lane; 4 * j < nd; j += kRowLanes) {
         uint32_t o[4];
         payload_quad(base, lim32, start, len, (int64_t)(16 * j) - H, o);
