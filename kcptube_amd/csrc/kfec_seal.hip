@@ -80,42 +80,35 @@ constexpr int kRowsPerBlock = kSealBlock / kRowLanes;
 #ifndef KFEC_SEAL_OPEN_PF
 #define KFEC_SEAL_OPEN_PF 1  // 0: open loads each packet when it reaches it (A/B knob)
 #endif
-#ifndef KFEC_SEAL_INPLACE_PF
-#define KFEC_SEAL_INPLACE_PF 0  // 1: the in-place kernel prefetches too (A/B knob)
-#endif
 #ifndef KFEC_SEAL_AB
 #define KFEC_SEAL_AB 0  // ablation (timing only, wrong results): 1 = the register rows skip the CRC
 #endif
 
 // The CRC tables each workgroup stages into LDS (60 KiB; all maps GF(2)-linear, so table lookups of the
 // input's bytes XORed together):
-//   diag[v][s]:  slot s holds s16(s & 15, v), the raw CRC (zero init) of a 16-byte chunk with byte v at position
-//                s & 15 and zeros elsewhere (slicing-by-16: a chunk's CRC is 16 independent lookups).  At step k
-//                row lane l looks up its byte at position (l + k) & 15 in slot l + k: a row of 64 dwords puts
-//                slot s in bank s mod 32, so the 32 lanes of a read hit 32 different banks whatever their
-//                bytes -- no conflicts (one table per position shared by all lanes gave 2.3 LDS cycles per read
-//                on random bytes) -- and the step is the read's immediate offset (4 k)
-//   sh[j][v]:    byte j = v of a CRC register advanced through 512 zero bytes (Horner over rounds)
+//   s16[k][v]:   raw CRC (zero init) of a 16-byte chunk with byte v at position k and zeros elsewhere
+//                (slicing-by-16: a chunk's CRC is 16 independent lookups; s16[12..15] are slicing-by-4's tables)
+//   sh[m][j][v]: byte j = v of a CRC register advanced through 16 << m zero bytes (m = 5: Horner over rounds;
+//                m < 5: the in-place kernel's butterfly)
 //   col[i][l]:   register bit i of row lane l advanced past the 31 - l chunks of its round after it, so the
 //                row's 32 lane sums combine as XOR_l XOR_i bit_i(R_l) col[i][l]: one conflict-free lookup
 //                per bit (lane l reads bank l) and no dependent chain, instead of a 5-level tree of shifts
-// Measured and dropped: slicing-by-4 (4 dependent steps per chunk), per-lane copies of the
-// bytewise table (conflict-free, 16 dependent steps per chunk: slower), nibble tables (conflict-free, twice
+// Measured and dropped: per-lane copies of the bytewise table and a diagonal layout of s16 (both
+// conflict-free, both slower: dependent chains / a per-lane byte rotation), nibble tables (conflict-free, twice
 // the lookups and a third more VALU: slower).
-#ifndef KFEC_SEAL_DIAG
-#define KFEC_SEAL_DIAG 0  // 1: the diagonal, conflict-free layout below (+20% VALU for the rotation: slower)
-#endif
-constexpr int kDiagPitch = 2 * kRowLanes;
 struct CrcLds {
-#if KFEC_SEAL_DIAG
-    uint32_t diag[256][kDiagPitch];
-#else
     uint32_t s16[16][256];
-#endif
-    uint32_t sh[4][256];
+    uint32_t sh[6][4][256];
     uint32_t col[32][kRowLanes];
 };
 constexpr int kCrcWords = (int)(sizeof(CrcLds) / 4);
+// what the in-place kernel stages (28 KiB, for its occupancy): slicing-by-4's tables (s16[12..15]) and sh
+struct CrcLdsIP {
+    uint32_t s4[4][256];
+    uint32_t sh[6][4][256];
+};
+__device__ __forceinline__ const uint32_t (*s4_of(const CrcLds &t))[256] { return t.s16 + 12; }
+__device__ __forceinline__ const uint32_t (*s4_of(const CrcLdsIP &t))[256] { return t.s4; }
 // after the LDS tables, in global memory only (one row of 32 dwords read per packet): unshift[d][i] = the CRC
 // register 1 << i taken back through d zero bytes (d < 512) -- the inverse of advancing it, which exists
 // because the reflected CRC-32 table's top bytes T[v] >> 24 are a permutation of v
@@ -143,17 +136,13 @@ __device__ uint32_t advance(uint32_t r, int d)  // r through d zero bytes
 __global__ void crc_tables_kernel(uint32_t *tab)
 {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    constexpr int kS16 = KFEC_SEAL_DIAG ? 256 * kDiagPitch : 16 * 256, kSh = kS16 + 4 * 256;
+    constexpr int kS16 = 16 * 256, kSh = kS16 + 6 * 4 * 256;
     uint32_t r;
-    if (e < kS16) {
-#if KFEC_SEAL_DIAG  // diag[v][s]
-        r = advance(c_crc.t[0][e / kDiagPitch], 15 - (e % kDiagPitch & 15));
-#else  // s16[k][v]
+    if (e < kS16) {  // s16[k][v]
         r = advance(c_crc.t[0][e & 255], 15 - e / 256);
-#endif
-    } else if (e < kSh) {
-        const int f = e - kS16, j = f / 256, v = f & 255;
-        r = advance((uint32_t)v << (8 * j), kCrcRound);
+    } else if (e < kSh) {  // sh[m][j][v]
+        const int f = e - kS16, m = f / 1024, j = (f / 256) & 3, v = f & 255;
+        r = advance((uint32_t)v << (8 * j), kCrcLane << m);
     } else if (e < kCrcWords) {
         const int f = e - kSh, i = f / kRowLanes, l = f % kRowLanes;
         r = advance(1u << i, kCrcLane * (kRowLanes - 1 - l));
@@ -170,38 +159,40 @@ __global__ void crc_tables_kernel(uint32_t *tab)
     tab[e] = r;
 }
 
-// raw CRC (zero init) of the 16-byte chunk o on row lane l: 16 independent, conflict-free lookups (diag)
-__device__ __forceinline__ uint32_t crc_chunk(const CrcLds &t, const uint32_t (&o)[4], uint32_t lane)
+// raw CRC (zero init) of the 16-byte chunk o: 16 independent lookups (slicing-by-16)
+__device__ __forceinline__ uint32_t crc_chunk(const CrcLds &t, const uint32_t (&o)[4], uint32_t)
 {
-#if KFEC_SEAL_DIAG
-    // rotate the chunk right by q = l & 15 bytes, so that step k finds byte (k + q) & 15 at byte k
-    const uint32_t q = lane & 15u;
-    uint32_t e[4], d[4], x[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) e[i] = q & 8u ? o[(i + 2) & 3] : o[i];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) d[i] = q & 4u ? e[(i + 1) & 3] : e[i];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_alignbyte(d[(i + 1) & 3], d[i], q & 3u);
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c ^= t.diag[(x[k >> 2] >> (8 * (k & 3))) & 0xFFu][lane + k];
-    return c;
-#else
     uint32_t c[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
         c[i] = t.s16[4 * i][o[i] & 0xFFu] ^ t.s16[4 * i + 1][(o[i] >> 8) & 0xFFu] ^
                t.s16[4 * i + 2][(o[i] >> 16) & 0xFFu] ^ t.s16[4 * i + 3][o[i] >> 24];
     return c[0] ^ c[1] ^ c[2] ^ c[3];
-#endif
 }
 
-// the register r advanced through 512 zero bytes
-__device__ __forceinline__ uint32_t crc_shift512(const CrcLds &t, uint32_t r)
+// the same by slicing-by-4 (a chain of 4 steps, s16[12..15] as its tables): fewer VALU, for the in-place kernel
+template <class T>
+__device__ __forceinline__ uint32_t crc_chunk4(const T &t, const uint32_t (&o)[4])
 {
-    return t.sh[0][r & 0xFFu] ^ t.sh[1][(r >> 8) & 0xFFu] ^ t.sh[2][(r >> 16) & 0xFFu] ^ t.sh[3][r >> 24];
+    const uint32_t (*s)[256] = s4_of(t);
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t x = c ^ o[i];
+        c = s[0][x & 0xFFu] ^ s[1][(x >> 8) & 0xFFu] ^ s[2][(x >> 16) & 0xFFu] ^ s[3][x >> 24];
+    }
+    return c;
 }
+
+// the register r advanced through 16 << m zero bytes
+template <class T>
+__device__ __forceinline__ uint32_t crc_shift(const T &t, int m, uint32_t r)
+{
+    const uint32_t (*s)[256] = t.sh[m];
+    return s[0][r & 0xFFu] ^ s[1][(r >> 8) & 0xFFu] ^ s[2][(r >> 16) & 0xFFu] ^ s[3][r >> 24];
+}
+
+__device__ __forceinline__ uint32_t crc_shift512(const CrcLds &t, uint32_t r) { return crc_shift(t, 5, r); }
 
 // the 32 lane sums of a row, each advanced past the chunks after it in the round (col), XORed over the row
 __device__ __forceinline__ uint32_t row_combine(const CrcLds &t, uint32_t R, uint32_t lane)
@@ -214,13 +205,10 @@ __device__ __forceinline__ uint32_t row_combine(const CrcLds &t, uint32_t R, uin
     return Z;
 }
 
-__device__ __forceinline__ uint32_t crc_byte(const CrcLds &t, uint32_t c, uint32_t byte)
+template <class T>
+__device__ __forceinline__ uint32_t crc_byte(const T &t, uint32_t c, uint32_t byte)
 {
-#if KFEC_SEAL_DIAG
-    return (c >> 8) ^ t.diag[(c ^ byte) & 0xFFu][15];
-#else
-    return (c >> 8) ^ t.s16[15][(c ^ byte) & 0xFFu];
-#endif
+    return (c >> 8) ^ s4_of(t)[3][(c ^ byte) & 0xFFu];
 }
 
 // 16 bytes [q0, q0 + 16) of base[start, start + len), zero outside (dword-aligned base, dwords < lim32):
@@ -298,6 +286,48 @@ __device__ __forceinline__ uint32_t row_crc32(const CrcLds &tab, const uint32_t 
     }
     // by linearity the 32 lanes' Horner sums combine exactly as one round's chunk CRCs do
     R = row_combine(tab, R, lane);
+    return ~R;
+}
+
+// row_crc32 in the round-1 form the in-place kernel measures fastest with (`tools/gpu_seal_ab.sh`, same call:
+// 1.97-2.00 ms against 2.06-2.16 for the register rows, where nothing else hides the CRC): slicing-by-4
+// chains and a butterfly of shift maps, fewer VALU than slicing-by-16 and the column combine
+template <class T>
+__device__ __forceinline__ uint32_t row_crc32_bf(const T &tab, const uint32_t *base32, uint64_t lim32, uint64_t start,
+                                                 uint32_t len, uint32_t lane)
+{
+    if (len < 4) {  // the init cannot be folded into message bytes: one lane, byte by byte
+        uint32_t c = 0xFFFFFFFFu;
+        if (lane == 0) {
+            uint32_t o[4];
+            chunk16(base32, lim32, start, len, 0, o);
+            for (uint32_t i = 0; i < len; ++i) c = crc_byte(tab, c, o[0] >> (8 * i));
+        }
+        return ~__shfl(c, 0, kRowLanes);
+    }
+    const uint32_t rounds = (len + kCrcRound - 1) / kCrcRound, pad = rounds * kCrcRound - len;
+    uint32_t R = 0;
+    for (uint32_t r = 0; r < rounds; ++r) {
+        uint32_t o[4];
+        const int32_t q0 = (int32_t)(r * kCrcRound + kCrcLane * lane) - (int32_t)pad;
+        chunk16(base32, lim32, start, len, q0, o);
+        if (q0 <= 3 && q0 > -16) {  // complement message bytes 0..3 (the 0xFFFFFFFF init)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int32_t q = q0 + 4 * i + b;
+                    if (q >= 0 && q < 4) o[i] ^= 0xFFu << (8 * b);
+                }
+        }
+        R = crc_shift(tab, 5, R) ^ crc_chunk4(tab, o);  // Horner over this lane's chunks
+    }
+    // butterfly: level k, the lane holding the earlier block A shifts it past the later block B (16 << k bytes)
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t other = __shfl_xor(R, 1 << k, kRowLanes);
+        const bool later = lane & (1u << k);
+        R = crc_shift(tab, k, later ? other : R) ^ (later ? R : other);
+    }
     return ~R;
 }
 
@@ -797,58 +827,46 @@ __global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu
 // its out-of-place path 24%).  Seal writes a trailer only where it fits the packet's slot (a.dst_pitch =
 // the slot size from d_off, e.g. pkt_pitch) and the buffer: a packet filling its slot would otherwise get
 // its trailer written over the next packet while another row is still reading that packet for its CRC.
-__global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu(4))) seal_in_place_kernel(SealArgs a, bool open)
+__global__ void __launch_bounds__(kSealBlock) seal_in_place_kernel(SealArgs a, bool open)
 {
-    __shared__ CrcLds s_tab;
-    stage_tables(a.tab, s_tab);
+    __shared__ CrcLdsIP s_tab;
+    {
+        uint32_t *flat = reinterpret_cast<uint32_t *>(&s_tab);
+        const uint32_t *src = a.tab + offsetof(CrcLds, s16) / 4 + 12 * 256;  // s16[12..15], then sh: contiguous
+        for (int i = threadIdx.x; i < (int)(sizeof(CrcLdsIP) / 4); i += kSealBlock) flat[i] = src[i];
+        __syncthreads();
+    }
     const uint32_t lane = threadIdx.x % kRowLanes;
     uint8_t *base = const_cast<uint8_t *>(reinterpret_cast<const uint8_t *>(a.src));
-    // decrypt_data: bad length / encrypt_data: empty data, or no room for the trailer
-    auto valid = [&](uint32_t L, uint64_t off) {
-        return open ? L > KFEC_SEAL_TRAILER
-                    : L != 0 && (uint64_t)L + KFEC_SEAL_TRAILER <= a.dst_pitch && off + L + KFEC_SEAL_TRAILER <= a.src_bytes;
-    };
-    // the bytes under the checksum go to the registers; open reads the trailer with one more load
-    auto load_len = [&](uint32_t L, uint64_t off) {
-        const uint32_t n = open ? L - KFEC_SEAL_TRAILER : L;
-        return KFEC_SEAL_REG && L > (open ? KFEC_SEAL_TRAILER : 0u) && n <= kRegBytes && row_fits(off, n, a.src_dw) ? n
-                                                                                                                 : 0u;
-    };
-    auto crc_len = [&](uint32_t L) { return open ? L - KFEC_SEAL_TRAILER : L; };
-    for_each_row<KFEC_SEAL_INPLACE_PF != 0>(a, lane, load_len, crc_len, [&](uint64_t p, uint32_t L, uint64_t off, uint32_t (&o)[kRegRounds][4], uint32_t u) {
-        if (!valid(L, off)) {
+    for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRowLanes; p < a.P;
+         p += (uint64_t)gridDim.x * kRowsPerBlock) {
+        const uint32_t L = a.len[p];
+        const uint64_t off = a.off[p];
+        if (open ? L <= KFEC_SEAL_TRAILER : L == 0) {  // decrypt_data: bad length / encrypt_data: empty data
             if (lane == 0) {
                 a.out_len[p] = 0;
                 if (open) a.ok[p] = 0;
             }
-            return;
+            continue;
         }
-        const uint32_t n = crc_len(L);  // bytes under the checksum
-        uint32_t cs, trailer = 0;
-        if (load_len(L, off)) {
-            if (open) {  // bytes n, n + 1: the dwords holding them lie inside the packet, so inside the buffer
-                const uint32_t *b32 = a.src;
-                const uint32_t w0 = b32[(off + n) >> 2], w1 = b32[(off + n + 1) >> 2];
-                trailer = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)((off + n) & 3u)) & 0xFFFFu;
-            }
-            mask_tail(o, n, lane);
-            cs = checksum16(crc_regs(s_tab, u, o, n, lane));
-        } else {
-            cs = checksum16(row_crc32(s_tab, a.src, a.src_dw, off, n, lane));
-            if (open && lane == 0) trailer = (uint32_t)base[off + n] | ((uint32_t)base[off + n + 1] << 8);
+        if (!open && ((uint64_t)L + KFEC_SEAL_TRAILER > a.dst_pitch || off + L + KFEC_SEAL_TRAILER > a.src_bytes)) {
+            if (lane == 0) a.out_len[p] = 0;  // no room for the trailer: "does not fit", nothing written
+            continue;
         }
+        const uint32_t n = open ? L - KFEC_SEAL_TRAILER : L;  // bytes under the checksum
+        const uint32_t cs = checksum16(row_crc32_bf(s_tab, a.src, a.src_dw, off, n, lane));
         if (lane == 0) {
+            uint8_t *t = base + off + n;
             if (open) {
-                a.ok[p] = cs == trailer;
+                a.ok[p] = cs == ((uint32_t)t[0] | ((uint32_t)t[1] << 8));
                 a.out_len[p] = n;
             } else {
-                uint8_t *t = base + off + n;
                 t[0] = (uint8_t)cs;
                 t[1] = (uint8_t)(cs >> 8);
                 a.out_len[p] = L + KFEC_SEAL_TRAILER;
             }
         }
-    });
+    }
 }
 
 uint32_t *crc_tables(hipStream_t s)
