@@ -768,30 +768,33 @@ __global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu
         const uint32_t n = L - KFEC_SEAL_TRAILER, nd = (n + 3) / 4;
         if (px) {  // xor_backward: plain[i] = T ^ (XOR of cipher[0..i)), T = XOR of every cipher byte
             mask_tail(o, L, lane);
-            uint32_t x = 0;
-#pragma unroll
-            for (int r = 0; r < kRegRounds; ++r) x ^= o[r][0] ^ o[r][1] ^ o[r][2] ^ o[r][3];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) x ^= __shfl_xor(x, 1 << k, kRowLanes);
-            x ^= x >> 16;
-            x ^= x >> 8;
-            const uint32_t T = (x & 0xFFu) * 0x01010101u;
-            uint32_t carry = 0;  // XOR of the cipher bytes of the rounds before (broadcast byte)
+            // one scan for all rounds: byte r of cx is the XOR of this lane's chunk of round r, so the exclusive
+            // prefix over the row's lanes of every round comes out of one 5-level scan (XOR is bytewise)
+            uint32_t cx = 0;
 #pragma unroll
             for (int r = 0; r < kRegRounds; ++r) {
-                // exclusive prefix XOR of the round's chunks across lanes, then bytewise inside the chunk
-                uint32_t cx = o[r][0] ^ o[r][1] ^ o[r][2] ^ o[r][3];
-                cx ^= cx >> 16;
-                cx ^= cx >> 8;
-                cx = (cx & 0xFFu) * 0x01010101u;
-                uint32_t incl = cx;
+                uint32_t c = o[r][0] ^ o[r][1] ^ o[r][2] ^ o[r][3];
+                c ^= c >> 16;
+                c ^= c >> 8;
+                cx |= (c & 0xFFu) << (8 * r);
+            }
+            uint32_t incl = cx;
 #pragma unroll
-                for (int k = 0; k < 5; ++k) {
-                    const uint32_t v = __shfl_up(incl, 1 << k, kRowLanes);
-                    if (lane >= (1u << k)) incl ^= v;
-                }
-                uint32_t run = carry ^ incl ^ cx;
-                carry ^= __shfl(incl, kRowLanes - 1, kRowLanes);
+            for (int k = 0; k < 5; ++k) {
+                const uint32_t v = __shfl_up(incl, 1 << k, kRowLanes);
+                if (lane >= (1u << k)) incl ^= v;
+            }
+            const uint32_t tot = __shfl(incl, kRowLanes - 1, kRowLanes);  // byte r: XOR of round r's bytes
+            uint32_t before = tot << 8;                                    // byte r: XOR of the rounds before r
+            before ^= before << 8;
+            before ^= before << 16;
+            uint32_t T = tot ^ (tot >> 16);  // XOR of every cipher byte, broadcast
+            T ^= T >> 8;
+            T = (T & 0xFFu) * 0x01010101u;
+            const uint32_t ex = before ^ incl ^ cx;  // byte r: cipher bytes before this lane's chunk of round r
+#pragma unroll
+            for (int r = 0; r < kRegRounds; ++r) {
+                uint32_t run = ((ex >> (8 * r)) & 0xFFu) * 0x01010101u;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     uint32_t in = o[r][i] ^ (o[r][i] << 8);
