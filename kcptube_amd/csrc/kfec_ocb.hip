@@ -513,15 +513,16 @@ int launch_ocb(const kfec_aead *k, bool open, size_t P, const void *src, size_t 
         return std::max(n, 1);
     }();
     // one workgroup per resident slot (LDS tables and VGPRs decide how many fit on a CU)
-    static int fit[2] = {0, 0};
-    if (!fit[open]) {
+    auto occupancy = [](const void *f) {
         int b = 0;
-        const void *fn = open ? reinterpret_cast<const void *>(&ocb_kernel<true>) : reinterpret_cast<const void *>(&ocb_kernel<false>);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kOcbBlock, 0) != hipSuccess || b < 1) b = 1;
-        fit[open] = b;
-    }
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, kOcbBlock, 0) != hipSuccess || b < 1) b = 1;
+        return b;
+    };
+    static const int fit_open = occupancy(reinterpret_cast<const void *>(&ocb_kernel<true>));  // thread-safe init
+    static const int fit_seal = occupancy(reinterpret_cast<const void *>(&ocb_kernel<false>));
+    const int fit = open ? fit_open : fit_seal;
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
-    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * fit[open]));
+    const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * fit));
     if (open) hipLaunchKernelGGL(ocb_kernel<true>, grid, dim3(kOcbBlock), 0, s, a);
     else hipLaunchKernelGGL(ocb_kernel<false>, grid, dim3(kOcbBlock), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;

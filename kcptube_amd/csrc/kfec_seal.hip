@@ -919,15 +919,16 @@ int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes
     }();
     // one workgroup per resident slot (the LDS tables and the VGPRs decide how many fit on a CU); each loops
     // over rows of 16 packets
-    const void *fn = !dst ? reinterpret_cast<const void *>(&seal_in_place_kernel)
-                          : open ? reinterpret_cast<const void *>(&open_kernel) : reinterpret_cast<const void *>(&seal_kernel);
-    static int per_cu[3] = {0, 0, 0};
-    int &fit = per_cu[!dst ? 0 : open ? 1 : 2];
-    if (fit == 0) {
+    // resident workgroups per CU, once per kernel (thread-safe static initialisation)
+    auto occupancy = [](const void *f) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kSealBlock, 0) != hipSuccess || b < 1) b = 1;
-        fit = b;
-    }
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, kSealBlock, 0) != hipSuccess || b < 1) b = 1;
+        return b;
+    };
+    static const int fit_in_place = occupancy(reinterpret_cast<const void *>(&seal_in_place_kernel));
+    static const int fit_open = occupancy(reinterpret_cast<const void *>(&open_kernel));
+    static const int fit_seal = occupancy(reinterpret_cast<const void *>(&seal_kernel));
+    const int fit = !dst ? fit_in_place : open ? fit_open : fit_seal;
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
     const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * fit));
     if (!dst) hipLaunchKernelGGL(seal_in_place_kernel, grid, dim3(kSealBlock), 0, s, a, open);  // checksum mode
