@@ -349,8 +349,6 @@ constexpr uint32_t kRegBytes = kRegRounds * kCrcRound;
 
 __device__ uint4 g_zero16;  // never written: the target of the loads a register row does not need
 
-  // never written: the target of the loads a register row does not need
-
 // The register rows load without a branch: both loads of a chunk are always issued, a chunk past the packet
 // (or a dword it does not need) reading g_zero16 instead.  A load under a branch makes the compiler wait for
 // it at the join (the loaded value is a phi there), which serialised every chunk of a row behind the one
