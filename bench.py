@@ -4,6 +4,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 20:3|10:3dec|200:55|20:3loss1]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+Both forms run one process per GPU: without a launcher's WORLD_SIZE, `--gpus N > 1` spawns the N rank
+processes itself (spawn_ranks) before any GPU call; a world that differs from --gpus is an error (exit 2).
+
 Metric (BASELINE.json): "FEC encode+decode GiB/s (device-resident), fec=20:3 kcp_mtu=1440".
 One step = encode every group of the batch (K data -> R parity shards) and decode every group with R
 data shards erased (selection, per-group m x m inverse, recovery MAC), all on the device with inputs
@@ -202,15 +205,65 @@ def rank_groups(groups_per_gpu: int, world: int, rank: int) -> tuple[int, int, i
     return g0, g1, total
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(cmd: list[str], n: int, poll_s: float = 0.2) -> int:
+    """`bench.py --gpus N` started without a launcher: run `cmd` as N rank processes of one node (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT set as torch.distributed.run sets them) and
+    return the first non-zero exit code, else 0.  The parent never imports torch or touches a GPU (the
+    ranks are fresh processes, not forks of an initialised one); the children inherit stdout, so rank 0's
+    JSON line is the parent's output.  When one rank fails the others are terminated (by handle) instead of
+    waiting in a barrier for a peer that is gone."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(poll_s)
+    for p in procs:
+        p.wait()
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: spawn the ranks before anything touches a device in this process
+        sys.exit(spawn_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher formed a world of {world} ranks", file=sys.stderr)
+        sys.exit(2)
+
     import torch
     import torch.distributed as dist
 
     from kcptube_amd import FecCode
     from kcptube_amd.partition import combine_digests, group_range
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -391,7 +444,9 @@ def main():
         "data": "synthetic: splitmix64 counter bytes generated on device (SURVEY 8d); erasure patterns per-group PRNG",
         "config": {"workload": workload, "fec": f"{K}:{R}", "kcp_mtu": B, "groups_per_gpu": G,
                    "global_groups": total_groups,
-                   "parallelism": f"{world} independent group ranges (no collective)"},
+                   "parallelism": f"{world} independent group ranges (no collective)",
+                   # ranks map to devices as LOCAL_RANK % device_count: fewer devices than ranks is a rehearsal
+                   "devices": min(world, torch.cuda.device_count())},
         "roofline": roof,
         "encode_ms": round(enc_ms, 4) if do_enc else None,
         "decode_ms": round(dec_ms, 4),

@@ -57,3 +57,17 @@ def test_bench_two_ranks_match_single_rank(config):
     assert two["recovered_shards_per_step"] == one["recovered_shards_per_step"] > 0
     assert two["combined_digest"] == one["combined_digest"]
     assert two["value"] > 0
+
+
+def test_bench_gpus_flag_spawns_the_ranks_itself():
+    """`python bench.py --gpus 2` (the driver's plain form, no launcher) forms a world of 2 ranks by itself
+    and its result equals the single-rank run over the same global groups."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    common = ["--config", "20:3", "--no-cpu", "--steps", "2", "--warmup", "1"]
+    two = _run([sys.executable, "bench.py", "--gpus", "2", "--groups", "4096"] + common, parts=2)
+    one = _run([sys.executable, "bench.py", "--gpus", "1", "--groups", "8192"] + common, parts=2)
+    assert two["n_gpus"] == 2 and two["verified_bit_exact"]
+    assert two["config"]["global_groups"] == 8192
+    assert two["combined_digest"] == one["combined_digest"]

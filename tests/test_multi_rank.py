@@ -89,6 +89,44 @@ def test_two_rank_gloo_partition_matches_single_rank(tmp_path, oracle):
     np.testing.assert_array_equal(par_all[g0:g1], par_1)
 
 
+def test_bench_gpus_must_match_the_world(tmp_path):
+    """`--gpus 3` inside a launcher-formed world of 1 is refused before any device work."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--no-cpu"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "world of 1" in r.stderr
+
+
+def test_bench_spawns_one_process_per_rank(tmp_path):
+    """bench.spawn_ranks (what `bench.py --gpus N` does without a launcher) starts N processes with the
+    torch.distributed.run environment, one shared 127.0.0.1 rendezvous, and distinct ranks."""
+    import sys
+    import bench
+    script = ("import os, sys; e = os.environ; "
+              "open(os.path.join(sys.argv[1], e['RANK']), 'w').write("
+              "' '.join(e[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')))")
+    env_before = dict(os.environ)
+    rc = bench.spawn_ranks([sys.executable, "-c", script, str(tmp_path)], 4, poll_s=0.05)
+    assert rc == 0 and dict(os.environ) == env_before
+    rows = [open(tmp_path / str(r)).read().split() for r in range(4)]
+    assert [row[:3] for row in rows] == [[str(r), str(r), "4"] for r in range(4)]
+    assert {row[3] for row in rows} == {"127.0.0.1"} and len({row[4] for row in rows}) == 1
+
+
+def test_bench_spawn_fails_when_a_rank_fails():
+    """One failing rank fails the job, and a peer left waiting (it would block in a barrier) is ended."""
+    import sys
+    import time
+    import bench
+    script = "import os, sys, time; r = int(os.environ['RANK']); time.sleep(60) if r == 0 else sys.exit(5)"
+    t0 = time.time()
+    rc = bench.spawn_ranks([sys.executable, "-c", script], 2, poll_s=0.05)
+    assert rc == 5 and time.time() - t0 < 30
+
+
 def test_bench_rank_groups_partition_the_global_space():
     """bench.py's own rank slicing (weak scaling: groups_per_gpu x world, split by group_range) tiles the
     global group space exactly, for every world size the driver runs."""
