@@ -7,7 +7,8 @@
  *   key    = SHA-3(256)(password)                                          (aead.hpp:405-437, 488-515)
  *   nonce  = the 16-bit iv_raw repeated: 16 bytes (aes_gcm), 12 (aes_ocb), 8 (chacha20), 24 (xchacha20)
  *            (aead.hpp:291-311, 379-400, 464-483, 542-562)
- *   packet = ciphertext || 16-byte Poly1305 tag || iv_raw (2 bytes, little-endian)    (data_operations.cpp:214-219)
+ *   packet = ciphertext || 16-byte tag || iv_raw (2 bytes, little-endian)    (data_operations.cpp:214-219);
+ *            the tag is Poly1305 (chacha20, xchacha20), GHASH (aes_gcm) or the OCB tag (aes_ocb)
  *   associated data "KCP PortHopping"                                      (aead.hpp:16)
  * Botan's AES-256/GCM takes the 16-byte nonce through GHASH into J0 (SP 800-38D); AES-256/OCB is RFC 7253
  * with a 128-bit tag.
@@ -49,7 +50,14 @@ typedef struct kfec_aead kfec_aead;
 /* The per-connection cipher object (encrypt_decrypt<chacha20 / xchacha20>(password), aead.hpp): derives the
  * key on the current HIP device and builds the per-iv tables there.  KFEC_EINVAL for another mode or an
  * empty password (the reference leaves its Botan objects unset then, aead.hpp:408-413, and the first packet
- * dereferences them); KFEC_ENODEV without a GPU; KFEC_ENOMEM. */
+ * dereferences them); KFEC_ENODEV without a GPU; KFEC_ENOMEM.
+ *
+ * Device memory: EVERY object holds its own tables on its device -- about 130 MiB (chacha20, aes_gcm: 128 MiB
+ * of per-iv keystream), 132 MiB (xchacha20) or 1 MiB (aes_ocb).  Objects are not shared between connections
+ * with the same password and mode, so create one per password and device (kcptube derives everything from
+ * the password) and hand it to every connection that uses it; the object is read-only after creation and
+ * may be used from several threads and streams at once.  Creation runs on a private stream and blocks the
+ * calling thread for ~2 ms; the seal / open calls switch to the object's device before launching. */
 int kfec_aead_create(int mode, const void *password, size_t password_len, kfec_aead **out);
 void kfec_aead_destroy(kfec_aead *a);
 int kfec_aead_mode(const kfec_aead *a);
@@ -67,10 +75,10 @@ int kfec_aead_seal_batch(const kfec_aead *a, size_t P, const void *d_src, size_t
 
 /* decrypt_data for P sealed packets: iv_raw from each packet's last two bytes, the tag verified over the
  * ciphertext.  d_ok[p] = 1 and d_out_len[p] = len - 18 with the plaintext at d_dst + p * dst_pitch (zero
- * padded to a multiple of 4) when the tag verifies; otherwise d_ok[p] = 0, d_out_len[p] = 0 and the
- * packet's dst bytes are zero.  Packets shorter than 18 bytes fail (decrypt_data: "incorrect data length"
- * for <= 2 bytes, Botan's too-short-for-the-tag exception for the rest), as do packets whose plaintext
- * exceeds dst_pitch. */
+ * padded to a multiple of 4) when the tag verifies; otherwise d_ok[p] = 0 and d_out_len[p] = 0.  A packet
+ * whose tag fails has its dst bytes zeroed; packets rejected on length -- shorter than 18 bytes (decrypt_data:
+ * "incorrect data length" for <= 2 bytes, Botan's too-short-for-the-tag exception for the rest) or with a
+ * plaintext longer than dst_pitch -- leave their dst bytes untouched. */
 int kfec_aead_open_batch(const kfec_aead *a, size_t P, const void *d_src, size_t src_bytes, const uint64_t *d_off,
                          const uint32_t *d_len, void *d_dst, size_t dst_pitch, uint32_t *d_out_len, uint8_t *d_ok,
                          void *stream);

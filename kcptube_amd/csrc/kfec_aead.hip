@@ -847,17 +847,7 @@ __global__ void __launch_bounds__(kAeadBlock) aead16_kernel(AeadArgs a)
     }
 }
 
-int aead_cus()
-{
-    static int cus = [] {
-        int d = 0, n = 0;
-        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) !=
-                                                  hipSuccess)
-            n = 256;
-        return std::max(n, 1);
-    }();
-    return cus;
-}
+int aead_cus() { return current_device_cus(); }
 
 }  // namespace
 
@@ -903,8 +893,20 @@ int launch_aead(const kfec_aead *k, bool open, size_t P, const void *src, size_t
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// key derivation and per-iv tables on the current device (synchronous: once per connection)
+int aead_setup_on(kfec_aead *k, const void *password, size_t len, hipStream_t s);
+
+// key derivation and per-iv tables on the current device (synchronous: once per connection).  It runs on a
+// private non-blocking stream and waits for that stream only, so in-flight work of other streams is not stalled.
 int aead_setup(kfec_aead *k, const void *password, size_t len)
+{
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return KFEC_EHIP;
+    const int rc = aead_setup_on(k, password, len, s);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
+int aead_setup_on(kfec_aead *k, const void *password, size_t len, hipStream_t s)
 {
     uint8_t *d_pw = nullptr;
     uint32_t *d_key = nullptr;
@@ -920,15 +922,15 @@ int aead_setup(kfec_aead *k, const void *password, size_t len)
         k->d_tab = nullptr;
         rc = KFEC_ENOMEM;
     }
-    if (rc == KFEC_OK && hipMemcpy(d_pw, password, len, hipMemcpyHostToDevice) != hipSuccess) rc = KFEC_EHIP;
+    if (rc == KFEC_OK && hipMemcpyAsync(d_pw, password, len, hipMemcpyHostToDevice, s) != hipSuccess) rc = KFEC_EHIP;
     if (rc == KFEC_OK) {
-        hipLaunchKernelGGL(sha3_256_kernel, dim3(1), dim3(64), 0, nullptr, d_pw, (uint64_t)len, d_key);
+        hipLaunchKernelGGL(sha3_256_kernel, dim3(1), dim3(64), 0, s, d_pw, (uint64_t)len, d_key);
         if (gcm) {
-            rc = gcm_setup(k, d_key);
+            rc = gcm_setup(k, d_key, s);
         } else if (ocb) {
-            rc = ocb_setup(k, d_key);
+            rc = ocb_setup(k, d_key, s);
         } else {
-            hipLaunchKernelGGL(iv_table_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, k->mode, d_key, k->d_tab);
+            hipLaunchKernelGGL(iv_table_kernel, dim3(65536 / 256), dim3(256), 0, s, k->mode, d_key, k->d_tab);
             if (KFEC_AEAD_ROW16 && KFEC_AEAD_KS) {
                 if (hipMalloc(&k->d_ks, (size_t)65536 * kChaKsBytes) != hipSuccess) {
                     k->d_ks = nullptr;
@@ -936,15 +938,17 @@ int aead_setup(kfec_aead *k, const void *password, size_t len)
                 } else {
                     k->ks_bytes = kChaKsBytes;
                     const uint64_t th = 65536ull * (kChaKsBytes / 64);
-                    hipLaunchKernelGGL(chacha_ks_kernel, dim3((uint32_t)((th + 255) / 256)), dim3(256), 0, nullptr,
+                    hipLaunchKernelGGL(chacha_ks_kernel, dim3((uint32_t)((th + 255) / 256)), dim3(256), 0, s,
                                        k->mode, d_key, k->d_tab, reinterpret_cast<uint32_t *>(k->d_ks));
                 }
             }
         }
-        if (rc == KFEC_OK && (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-                              hipMemcpy(k->key, d_key, 32, hipMemcpyDeviceToHost) != hipSuccess))
+        if (rc == KFEC_OK && (hipGetLastError() != hipSuccess ||
+                              hipMemcpyAsync(k->key, d_key, 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                              hipStreamSynchronize(s) != hipSuccess))
             rc = KFEC_EHIP;
     }
+    (void)hipStreamSynchronize(s);  // (a failed launch sequence: nothing may still read d_pw / d_key)
     (void)hipFree(d_pw);
     (void)hipFree(d_key);
     if (rc != KFEC_OK) {
@@ -988,6 +992,7 @@ int kfec_aead_create(int mode, const void *password, size_t password_len, kfec_a
 void kfec_aead_destroy(kfec_aead *a)
 {
     if (!a) return;
+    (void)hipSetDevice(a->device);  // the tables live on the cipher's device
     if (a->d_tab) (void)hipFree(a->d_tab);
     kfec::gcm_free(a);
     delete a;
@@ -1011,6 +1016,7 @@ int kfec_aead_seal_batch(const kfec_aead *a, size_t P, const void *d_src, size_t
     if (!a || dst_pitch % 4) return KFEC_EINVAL;
     if (P && (!d_src || !aead_al4(d_src) || !d_off || !d_len || !d_iv || !d_dst || !aead_al4(d_dst) || !d_out_len))
         return KFEC_EINVAL;
+    if (hipSetDevice(a->device) != hipSuccess) return KFEC_EHIP;  // launch where the cipher's tables live
     return kfec::launch_aead(a, false, P, d_src, src_bytes, d_off, d_len, d_iv, d_dst, dst_pitch, d_out_len, nullptr,
                              static_cast<hipStream_t>(stream))
                ? KFEC_EHIP
@@ -1024,6 +1030,7 @@ int kfec_aead_open_batch(const kfec_aead *a, size_t P, const void *d_src, size_t
     if (!a || dst_pitch % 4) return KFEC_EINVAL;
     if (P && (!d_src || !aead_al4(d_src) || !d_off || !d_len || !d_dst || !aead_al4(d_dst) || !d_out_len || !d_ok))
         return KFEC_EINVAL;
+    if (hipSetDevice(a->device) != hipSuccess) return KFEC_EHIP;  // launch where the cipher's tables live
     return kfec::launch_aead(a, true, P, d_src, src_bytes, d_off, d_len, nullptr, d_dst, dst_pitch, d_out_len, d_ok,
                              static_cast<hipStream_t>(stream))
                ? KFEC_EHIP

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -28,6 +29,21 @@ struct kfec_ctx {
     uint8_t *h_stage = nullptr;  // fine-grained pinned host staging the kernels read and write in place
     size_t h_stage_cap = 0;
 };
+
+int kfec::current_device_cus()
+{
+    static std::atomic<int> cache[64];
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (dev < 0 || dev >= 64) {
+        return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+    }
+    n = cache[dev].load(std::memory_order_relaxed);
+    if (n > 0) return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
+    cache[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
 
 namespace {
 

@@ -343,18 +343,18 @@ __global__ void __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(
 
 }  // namespace
 
-int gcm_setup(kfec_aead *k, const uint32_t *d_key)
+int gcm_setup(kfec_aead *k, const uint32_t *d_key, hipStream_t s)
 {
     if (hipMalloc(&k->d_rk, 240) != hipSuccess || hipMalloc(&k->d_h, 16) != hipSuccess ||
         hipMalloc(&k->d_gh, kGhTables * 32 * 16 * 16) != hipSuccess || hipMalloc(&k->d_ivt, 65536 * 32) != hipSuccess ||
         hipMalloc(&k->d_ks, (size_t)65536 * kKsBytes) != hipSuccess)
         return KFEC_ENOMEM;
     k->ks_bytes = kKsBytes;
-    hipLaunchKernelGGL(gcm_key_kernel, dim3(1), dim3(64), 0, nullptr, d_key, k->d_rk, k->d_h);
-    hipLaunchKernelGGL(gcm_tables_kernel, dim3(kGhTables * 32 * 16 / 256), dim3(256), 0, nullptr, k->d_h, k->d_gh);
-    hipLaunchKernelGGL(gcm_iv_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, k->d_rk, k->d_h, k->d_ivt);
+    hipLaunchKernelGGL(gcm_key_kernel, dim3(1), dim3(64), 0, s, d_key, k->d_rk, k->d_h);
+    hipLaunchKernelGGL(gcm_tables_kernel, dim3(kGhTables * 32 * 16 / 256), dim3(256), 0, s, k->d_h, k->d_gh);
+    hipLaunchKernelGGL(gcm_iv_kernel, dim3(65536 / 256), dim3(256), 0, s, k->d_rk, k->d_h, k->d_ivt);
     const uint64_t ks_threads = 65536ull * (kKsBytes / 16);
-    hipLaunchKernelGGL(gcm_ks_kernel, dim3((uint32_t)((ks_threads + 255) / 256)), dim3(256), 0, nullptr, k->d_rk,
+    hipLaunchKernelGGL(gcm_ks_kernel, dim3((uint32_t)((ks_threads + 255) / 256)), dim3(256), 0, s, k->d_rk,
                        k->d_ivt, k->d_ks);
     return hipGetLastError() == hipSuccess ? KFEC_OK : KFEC_EHIP;
 }
@@ -387,13 +387,7 @@ int launch_gcm(const kfec_aead *k, bool open, size_t P, const void *src, size_t 
     a.ks = k->d_ks;
     a.rk = k->d_rk;
     a.P = P;
-    static int cus = [] {
-        int d = 0, n = 0;
-        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) !=
-                                                  hipSuccess)
-            n = 256;
-        return std::max(n, 1);
-    }();
+    const int cus = current_device_cus();
     // 40 KiB of GHASH tables per workgroup: 3 resident per CU at 512 lanes (6 waves per SIMD), 4 at 256;
     // grid-stride over packets
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;

@@ -44,6 +44,9 @@ struct DeviceInfo {
     int cus = 0;
 };
 
+// multiprocessor count of the current device, cached per device id (grids of the persistent kernels)
+int current_device_cus();
+
 // every launcher returns 0 or a negative KFEC_E* code
 int launch_build_matrix(uint8_t *d_enc, int K, int N, hipStream_t s);
 int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, size_t B, size_t pitch,
@@ -112,9 +115,9 @@ struct kfec_aead {
 };
 
 namespace kfec {
-int gcm_setup(kfec_aead *k, const uint32_t *d_key);
+int gcm_setup(kfec_aead *k, const uint32_t *d_key, hipStream_t s);
 void gcm_free(kfec_aead *k);  // every AES-mode table (gcm and ocb)
-int ocb_setup(kfec_aead *k, const uint32_t *d_key);
+int ocb_setup(kfec_aead *k, const uint32_t *d_key, hipStream_t s);
 int launch_ocb(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
                const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
                hipStream_t s);

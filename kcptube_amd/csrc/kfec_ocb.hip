@@ -475,14 +475,14 @@ __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
 
 }  // namespace
 
-int ocb_setup(kfec_aead *k, const uint32_t *d_key)
+int ocb_setup(kfec_aead *k, const uint32_t *d_key, hipStream_t s)
 {
     if (hipMalloc(&k->d_ocb, sizeof(OcbKey)) != hipSuccess || hipMalloc(&k->d_ivt, 65536 * 16) != hipSuccess)
         return KFEC_ENOMEM;
     OcbKey *ok = reinterpret_cast<OcbKey *>(k->d_ocb);
-    hipLaunchKernelGGL(ocb_key_kernel, dim3(1), dim3(64), 0, nullptr, d_key, ok);
-    hipLaunchKernelGGL(ocb_tables_kernel, dim3(1), dim3(256), 0, nullptr, ok);
-    hipLaunchKernelGGL(ocb_iv_kernel, dim3(65536 / 256), dim3(256), 0, nullptr, d_key,
+    hipLaunchKernelGGL(ocb_key_kernel, dim3(1), dim3(64), 0, s, d_key, ok);
+    hipLaunchKernelGGL(ocb_tables_kernel, dim3(1), dim3(256), 0, s, ok);
+    hipLaunchKernelGGL(ocb_iv_kernel, dim3(65536 / 256), dim3(256), 0, s, d_key,
                        reinterpret_cast<uint4 *>(k->d_ivt));
     return hipGetLastError() == hipSuccess ? KFEC_OK : KFEC_EHIP;
 }
@@ -505,13 +505,7 @@ int launch_ocb(const kfec_aead *k, bool open, size_t P, const void *src, size_t 
     a.key = reinterpret_cast<const OcbKey *>(k->d_ocb);
     a.off0 = reinterpret_cast<const uint4 *>(k->d_ivt);
     a.P = P;
-    static int cus = [] {
-        int d = 0, n = 0;
-        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) !=
-                                                  hipSuccess)
-            n = 256;
-        return std::max(n, 1);
-    }();
+    const int cus = current_device_cus();
     // one workgroup per resident slot (LDS tables and VGPRs decide how many fit on a CU)
     auto occupancy = [](const void *f) {
         int b = 0;

@@ -854,6 +854,13 @@ __global__ void __launch_bounds__(kSealBlock) seal_in_place_kernel(SealArgs a, b
             if (lane == 0) a.out_len[p] = 0;  // no room for the trailer: "does not fit", nothing written
             continue;
         }
+        if (open && off + L > a.src_bytes) {  // the packet runs past the buffer: a bad length, nothing read
+            if (lane == 0) {
+                a.out_len[p] = 0;
+                a.ok[p] = 0;
+            }
+            continue;
+        }
         const uint32_t n = open ? L - KFEC_SEAL_TRAILER : L;  // bytes under the checksum
         const uint32_t cs = checksum16(row_crc32_bf(s_tab, a.src, a.src_dw, off, n, lane));
         if (lane == 0) {
@@ -908,13 +915,7 @@ int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes
     a.tab = crc_tables(s);
     if (!a.tab) return -3;
     a.unshift = a.tab + kCrcWords;
-    static int cus = [] {
-        int d = 0, n = 0;
-        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) !=
-                                                  hipSuccess)
-            n = 256;
-        return std::max(n, 1);
-    }();
+    const int cus = current_device_cus();
     // one workgroup per resident slot (the LDS tables and the VGPRs decide how many fit on a CU); each loops
     // over rows of 16 packets
     // resident workgroups per CU, once per kernel (thread-safe static initialisation)

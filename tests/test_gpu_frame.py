@@ -699,6 +699,17 @@ def test_seal_in_place_respects_slots_and_buffer_end(dev):
     assert set(changed) <= allowed  # only trailers of the packets that fit
     with pytest.raises(KfecError):
         seal(0, flat, off, d_len, None, ol, slot=0)
+    # open in place: the sealed packets verify; a length that runs past the buffer end is a bad length (out_len 0,
+    # ok 0) and its trailer is not read
+    from kcptube_amd.frame import open_
+    o_len = torch.tensor([64, 12, 63, 64, pitch + 2], dtype=torch.int32, device=dev)
+    o_off = torch.tensor([0, 3 * pitch, 4 * pitch, 5 * pitch, 5 * pitch - 2], dtype=torch.int64, device=dev)
+    ol2 = torch.full((5,), -1, dtype=torch.int32, device=dev)
+    ok2 = torch.full((5,), 7, dtype=torch.uint8, device=dev)
+    open_(0, flat, o_off, o_len, None, ol2, ok2)
+    torch.cuda.synchronize()
+    assert ol2.cpu().tolist()[:3] == [62, 10, 61] and ok2.cpu().tolist()[:3] == [1, 1, 1]
+    assert ol2.cpu().tolist()[3:] == [0, 0] and ok2.cpu().tolist()[3:] == [0, 0]
 
 
 @pytest.mark.parametrize("mode", [fo.SEAL_CHECKSUM, fo.SEAL_PLAIN_XOR])
