@@ -46,7 +46,10 @@ typedef struct kfec_ctx kfec_ctx;
 int kfec_create(size_t K, size_t N, kfec_ctx **out);
 /* reset_martix(K, N) (fecpp.cpp:437-451): re-targets an existing coder.  On any error (KFEC_EINVAL, or a
  * failed allocation / launch) the coder is unchanged: the new matrix is committed only once built.
- * Batch queues (kfec_pipeline.h) created on the coder must be recreated after a reset. */
+ * Batch queues (kfec_pipeline.h) created on the coder must be recreated after a reset.
+ * A reset must not run concurrently with any other call that uses the same coder (its queues included):
+ * it frees the old matrix, which a concurrent launch may still be reading.  fecpp::fec_code has no locking
+ * either; kcptube re-targets a coder from the thread that uses it (client.cpp:1755, relay.cpp:947). */
 int kfec_reset(kfec_ctx *ctx, size_t K, size_t N);
 void kfec_destroy(kfec_ctx *ctx);
 size_t kfec_get_K(const kfec_ctx *ctx);

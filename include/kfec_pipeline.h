@@ -25,7 +25,8 @@
  * Threading: a kfec_tx / kfec_rx and its queue are used from one thread at a time (the reference serialises
  * with mutex_fec_snd / mutex_fec_rcv, connections.hpp:609-611).  Destroy the kfec_tx / kfec_rx of a queue
  * before the queue.  A queue is sized for its coder's K / N: after kfec_reset (reset_martix) of that coder
- * every push / send / flush of the queue returns KFEC_EINVAL -- recreate the queues.
+ * every push / send / flush of the queue returns KFEC_EINVAL -- recreate the queues.  That check is for resets
+ * sequenced before the call; a reset concurrent with a queue call is not allowed (kfec.h, kfec_reset).
  * Staging: datagrams and shards are copied once, into the queue's pinned arena, when they arrive; finished
  * 8 MiB stretches of it go H2D on the queue's own copy stream while the host keeps filling it, so a flush
  * waits only for the tail, the kernels and the D2H of its results.
