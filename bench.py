@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="20:3", choices=sorted(CONFIGS))
     p.add_argument("--groups", type=int, default=0, help="override groups per GPU")
+    p.add_argument("--pitch", type=int, default=0,
+                   help="bytes per shard slot in HBM (default: kcp_mtu, rows back to back; a larger pitch only "
+                        "aligns the rows -- same shard bytes, same algorithmic traffic -- and is never the headline)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=16.0, help="target CPU-seconds of the baseline sample")
     p.add_argument("--cpu-groups", type=int, default=1 << 16, help="distinct groups of the CPU baseline sample")
@@ -281,16 +284,19 @@ def main():
     g0, g1, total_groups = rank_groups(G, world, rank)  # this rank's contiguous range of the global groups
     G = g1 - g0
     c = FecCode(K, N)
-    data = torch.empty((G, K, B), dtype=torch.uint8, device=dev)
-    par = torch.empty((G, R, B), dtype=torch.uint8, device=dev)
+    pitch = max(args.pitch, B) if args.pitch else B
+    if pitch != B:
+        workload += f" (shard slots padded to a {pitch}-byte pitch)"
+    data = torch.empty((G, K, pitch), dtype=torch.uint8, device=dev)
+    par = torch.empty((G, R, pitch), dtype=torch.uint8, device=dev)
     masks = torch.empty((G, 4), dtype=torch.int64, device=dev)
-    out = torch.empty((G, R, B), dtype=torch.uint8, device=dev)
+    out = torch.empty((G, R, pitch), dtype=torch.uint8, device=dev)
     idx = torch.empty((G, R), dtype=torch.uint8, device=dev)
     st = torch.empty((G,), dtype=torch.uint8, device=dev)
     ws = c.decode_workspace(G, device=dev)
-    c.synth(data, SEED, g0=g0)
+    c.synth(data, SEED, g0=g0, B=B)
     c.erasure_masks(masks, SEED, pool, erase, mode, g0=g0)
-    c.encode_batch(data, par)  # parity exists before a decode-only step
+    c.encode_batch(data, par, B=B)  # parity exists before a decode-only step
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
@@ -301,10 +307,10 @@ def main():
         if i is not None:
             ev[i][0].record(stream)
         if do_enc:
-            c.encode_batch(data, par)
+            c.encode_batch(data, par, B=B)
         if i is not None:
             ev[i][1].record(stream)
-        c.decode_batch(data, par, masks, out, idx, st, ws)
+        c.decode_batch(data, par, masks, out, idx, st, ws, B=B)
         if i is not None:
             ev[i][2].record(stream)
 
@@ -332,7 +338,7 @@ def main():
 
     # correctness of what was timed (untimed): every erased data shard recovered bit-exact
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
-    c.verify_recovered(data, out, idx, mism)
+    c.verify_recovered(data, out, idx, mism, B=B)
     torch.cuda.synchronize()
     n_rec = int((idx != 0xFF).sum().item())
     n_dec = int((idx[:, 0] != 0xFF).sum().item()) if R > 0 else 0  # groups with m > 0 (m = 0 reads nothing)
@@ -348,10 +354,10 @@ def main():
         import hashlib
         if parts % world:
             raise SystemExit("KFEC_BENCH_DIGEST must be a multiple of the world size")
-        o = out.cpu().numpy()
+        o = out[..., :B].cpu().numpy()
         ix = idx.cpu().numpy()
         o[ix == 0xFF] = 0
-        pn = par.cpu().numpy()
+        pn = par[..., :B].cpu().numpy()
         for p in range(rank * parts // world, (rank + 1) * parts // world):
             a, b = group_range(total_groups, parts, p)
             a, b = a - g0, b - g0
@@ -394,8 +400,8 @@ def main():
     if os.path.exists(pmc):
         try:
             with open(pmc) as f:
-                tr = json.load(f).get(args.config)
-            if tr and tr.get("groups") == G:
+                tr = json.load(f).get(args.config if pitch == B else f"{args.config}@p{pitch}")
+            if tr and tr.get("groups") == G and tr.get("pitch", B) == pitch:
                 traffic = tr.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -442,7 +448,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: splitmix64 counter bytes generated on device (SURVEY 8d); erasure patterns per-group PRNG",
-        "config": {"workload": workload, "fec": f"{K}:{R}", "kcp_mtu": B, "groups_per_gpu": G,
+        "config": {"workload": workload, "fec": f"{K}:{R}", "kcp_mtu": B, "pitch": pitch, "groups_per_gpu": G,
                    "global_groups": total_groups,
                    "parallelism": f"{world} independent group ranges (no collective)",
                    # ranks map to devices as LOCAL_RANK % device_count: fewer devices than ranks is a rehearsal

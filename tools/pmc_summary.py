@@ -14,6 +14,7 @@ import argparse, collections, csv, glob, json, os, re, shutil
 ap = argparse.ArgumentParser()
 ap.add_argument("prof_dir"); ap.add_argument("tag")
 ap.add_argument("--config", default="20:3"); ap.add_argument("--groups", type=int, default=1 << 20)
+ap.add_argument("--pitch", type=int, default=0, help="shard pitch of a padded-layout run (key <config>@p<pitch>)")
 args = ap.parse_args()
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = os.path.join(root, "profiles"); os.makedirs(out, exist_ok=True)
@@ -48,8 +49,11 @@ dominant = re.compile(r"syn_kernel<\d+, \d+(, \d+)?>" if args.config.endswith("d
                       else r"mac_kernel<\d+, \d+, false(, \d+)?>")
 for k, d in summary.items():
     if dominant.search(k) and "hbm_bytes_per_launch" in d:
-        trf[args.config] = {"groups": args.groups, "kernel": k, "hbm_bytes_per_launch": int(d["hbm_bytes_per_launch"]),
-                            "source": f"profiles/{args.tag}_pmc.json"}
+        key = f"{args.config}@p{args.pitch}" if args.pitch else args.config
+        trf[key] = {"groups": args.groups, "kernel": k, "hbm_bytes_per_launch": int(d["hbm_bytes_per_launch"]),
+                    "source": f"profiles/{args.tag}_pmc.json"}
+        if args.pitch:
+            trf[key]["pitch"] = args.pitch
 json.dump(trf, open(trf_path, "w"), indent=1)
 for k, d in summary.items():
     print(k[:60], {c: round(x, 4) if isinstance(x, float) else x for c, x in d.items()
