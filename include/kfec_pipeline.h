@@ -37,6 +37,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "kfec_aead.h"
 #include "kfec_frame.h"
 
 #ifdef __cplusplus
@@ -47,6 +48,7 @@ typedef struct kfec_txq kfec_txq;
 typedef struct kfec_tx kfec_tx;
 typedef struct kfec_rxq kfec_rxq;
 typedef struct kfec_rx kfec_rx;
+typedef struct kfec_opener kfec_opener;
 
 /* ---- send -------------------------------------------------------------------------------------------- */
 
@@ -77,8 +79,31 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
 typedef void (*kfec_packet_cb)(void *user, uint64_t tag, uint32_t sn, uint8_t sub_sn, const uint8_t *pkt,
                                size_t len);
 
-/* Encode every queued group on the GPU and emit its N-K redundant packets (queue order).  Synchronous. */
+/* Encode every queued group on the GPU and emit its N-K redundant packets (queue order).  Synchronous.
+ * With KFEC_TXQ_DEFER_DATA (kfec_txq_seal) the staged data packets come out here too, in send order, each
+ * group's redundant packets right after the data packet that completed it -- the order in which the
+ * reference's fec_maker hands its packets to data_sender (client.cpp:797-840). */
 int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *user, void *stream);
+
+/* Packet protection on the device, encrypt_data (data_operations.cpp:171-234) as data_sender applies it to
+ * every packet it sends (client.cpp:780-795):
+ *   mode KFEC_SEAL_CHECKSUM / KFEC_SEAL_PLAIN_XOR (kfec_frame.h; encryption none / plain_xor, aead NULL) or
+ *   KFEC_AEAD_AES_GCM / _AES_OCB / _CHACHA20 / _XCHACHA20 with the matching cipher (kfec_aead.h, created on the
+ *   coder's device); KFEC_TXQ_SEAL_OFF (the default) emits plain FEC packets.
+ * Sealed, every packet the flush emits is ciphertext || tag || iv_raw (AEAD) or data || checksum16 (checksum
+ * modes), computed after the pack on the device and copied back once.  The AEAD iv_raw of the i-th sealed
+ * packet (emission order, counted over the queue's life) is the top 16 bits of splitmix64(iv_seed + i): the
+ * reference draws it uniformly from a thread-local mt19937 (change_iv, aead.hpp:464-475); a counter-based
+ * draw gives the same distribution and lets a test replay the sequence.
+ * flags KFEC_TXQ_DEFER_DATA: kfec_tx_send no longer writes the data packet (pkt may be NULL, *pkt_len = 0): the
+ * packet is staged in the queue's arena and emitted -- sealed, if a mode is set -- by the next flush, so no
+ * packet is sealed on the host.  KFEC_EINVAL for an unknown mode, a missing / mismatched cipher, or a change
+ * while packets are staged or groups queued. */
+#define KFEC_TXQ_SEAL_OFF (-1)
+#define KFEC_TXQ_DEFER_DATA 1u
+int kfec_txq_seal(kfec_txq *q, int mode, const kfec_aead *aead, uint64_t iv_seed, unsigned flags);
+/* Data packets staged by KFEC_TXQ_DEFER_DATA senders since the last flush. */
+size_t kfec_txq_staged(const kfec_txq *q);
 
 /* ---- receive ----------------------------------------------------------------------------------------- */
 
@@ -115,6 +140,25 @@ typedef void (*kfec_datagram_cb)(void *user, uint64_t tag, uint32_t sn, uint8_t 
 /* Decode every queued group on the GPU and emit the recovered datagrams (queue order, ascending index within
  * a group), as fec_find_missings' extract_from_container + KCP::Input loop.  Synchronous. */
 int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream);
+
+/* ---- receive-side packet opening ---------------------------------------------------------------------- */
+
+/* decrypt_data (data_operations.cpp:373-435) for batches of received packets on the device, ahead of
+ * kfec_rx_push: the packets of many connections are staged (one host copy into pinned memory), opened by one
+ * kernel launch per flush and handed back in staging order.  mode / aead as kfec_txq_seal (KFEC_TXQ_SEAL_OFF is
+ * refused); the cipher, if any, must live on the current device.  Up to max_packets packets of at most
+ * max_packet bytes between flushes. */
+int kfec_opener_create(int mode, const kfec_aead *aead, size_t max_packets, size_t max_packet, kfec_opener **out);
+void kfec_opener_destroy(kfec_opener *o);
+size_t kfec_opener_pending(const kfec_opener *o);
+/* Stage one received packet: KFEC_EINVAL for a packet longer than max_packet, KFEC_ENOMEM when max_packets
+ * are staged (flush, then retry). */
+int kfec_opener_add(kfec_opener *o, const uint8_t *pkt, size_t len, uint64_t tag);
+/* Opened packet callback: tag given to kfec_opener_add, the plaintext (what decrypt_data returns), ok = 0
+ * when the tag / checksum did not verify or the length was invalid (the reference drops such a packet). */
+typedef void (*kfec_opened_cb)(void *user, uint64_t tag, const uint8_t *plain, size_t len, int ok);
+/* Open every staged packet on the device (synchronous) and call cb for each, in staging order. */
+int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *stream);
 
 #ifdef __cplusplus
 }

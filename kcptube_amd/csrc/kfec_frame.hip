@@ -703,7 +703,25 @@ uint32_t grid_rows(uint64_t rows)
 
 int launched() { return hipGetLastError() == hipSuccess ? 0 : -3; }
 
+// packet descriptors of a row-major packet array (the pack kernel's output) for the seal / open kernels
+__global__ void __launch_bounds__(kFrameBlock) pkt_desc_kernel(uint64_t P, uint64_t pitch, const uint16_t *len16,
+                                                               uint64_t *off, uint32_t *len32)
+{
+    const uint64_t i = blockIdx.x * (uint64_t)kFrameBlock + threadIdx.x;
+    if (i >= P) return;
+    off[i] = i * pitch;
+    len32[i] = len16[i];
+}
+
 }  // namespace
+
+int launch_pkt_desc(size_t P, size_t pitch, const uint16_t *len16, uint64_t *off, uint32_t *len32, hipStream_t s)
+{
+    if (P == 0) return 0;
+    hipLaunchKernelGGL(pkt_desc_kernel, dim3((uint32_t)((P + kFrameBlock - 1) / kFrameBlock)), dim3(kFrameBlock), 0, s,
+                       (uint64_t)P, (uint64_t)pitch, len16, off, len32);
+    return launched();
+}
 
 // 0 on success, 1 when the fused kernel does not apply (the caller frames, then encodes), -3 on a HIP error
 int launch_framed_encode(const uint8_t *d_enc, int K, int N, size_t G, const void *src, size_t src_bytes,

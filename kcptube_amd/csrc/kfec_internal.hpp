@@ -93,6 +93,8 @@ struct DataPackets {
 int launch_framed_encode(const uint8_t *d_enc, int K, int N, size_t G, const void *src, size_t src_bytes,
                          const uint64_t *off, const uint16_t *len, size_t B, size_t pitch, void *parity,
                          uint16_t *align, hipStream_t s, const DataPackets *dp = nullptr);
+// off[i] = i * pitch, len32[i] = len16[i] for i < P: descriptors of a packet array for the seal / open calls
+int launch_pkt_desc(size_t P, size_t pitch, const uint16_t *len16, uint64_t *off, uint32_t *len32, hipStream_t s);
 // packet integrity (kfec_seal.hip)
 int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
                 const uint32_t *len, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok, hipStream_t s);

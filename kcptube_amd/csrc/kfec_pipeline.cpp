@@ -6,6 +6,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "kfec_internal.hpp"
+
 #include <algorithm>
 #include <cstring>
 #include <memory>
@@ -134,6 +136,34 @@ inline uint32_t get_be32(const uint8_t *p)
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
 }
 
+// the AEAD iv_raw draw of sealed packet number i (kfec_txq_seal)
+inline uint16_t iv_draw(uint64_t seed, uint64_t i)
+{
+    uint64_t x = seed + i + 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return (uint16_t)((x ^ (x >> 31)) >> 48);
+}
+
+bool seal_mode_ok(int mode, const kfec_aead *aead)
+{
+    if (mode == KFEC_SEAL_CHECKSUM || mode == KFEC_SEAL_PLAIN_XOR) return aead == nullptr;
+    if (mode == KFEC_AEAD_AES_GCM || mode == KFEC_AEAD_AES_OCB || mode == KFEC_AEAD_CHACHA20 || mode == KFEC_AEAD_XCHACHA20)
+        return aead != nullptr && kfec_aead_mode(aead) == mode;
+    return false;
+}
+
+size_t seal_overhead(int mode) { return mode == KFEC_SEAL_CHECKSUM || mode == KFEC_SEAL_PLAIN_XOR ? KFEC_SEAL_TRAILER : KFEC_AEAD_OVERHEAD; }
+
+// encrypt_data / decrypt_data of P packets [off, +len) of a device arena into [P][pitch] rows
+int seal_rows(int mode, const kfec_aead *aead, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
+              const uint32_t *len, const uint16_t *iv, void *dst, size_t pitch, uint32_t *out_len, void *stream)
+{
+    if (P == 0) return KFEC_OK;
+    if (aead) return kfec_aead_seal_batch(aead, P, src, src_bytes, off, len, iv, dst, pitch, out_len, stream);
+    return kfec_seal_batch(mode, P, src, src_bytes, off, len, dst, pitch, out_len, stream);
+}
+
 }  // namespace
 
 // ---- send ------------------------------------------------------------------------------------------------
@@ -152,6 +182,22 @@ struct kfec_txq {
     size_t m_len = 0, m_sn = 0, m_conv = 0;
     std::vector<uint64_t> tags;
     Device d_dg, d_meta, d_par, d_align, d_res;
+    // packet protection and deferred data packets (kfec_txq_seal)
+    int seal_mode = KFEC_TXQ_SEAL_OFF;
+    const kfec_aead *aead = nullptr;
+    uint64_t iv_seed = 0, iv_ctr = 0;
+    bool defer = false;
+    struct DataPkt {
+        uint64_t off;   // the whole data packet (9-byte header + datagram) in the staging arena
+        uint32_t len;
+        uint32_t sn;
+        uint8_t sub;
+        int32_t group;  // the queue slot of the group this packet completed, or -1
+        uint64_t tag;
+    };
+    std::vector<DataPkt> dpk;  // staged since the last flush, in send order
+    Pinned h_sdesc, h_sealed;  // seal descriptors (+ iv draws) up; sealed rows + lengths down
+    Device d_sdesc, d_sealed;
     uint64_t *h_off() const { return h_meta.as<uint64_t>(); }
     uint16_t *h_len() const { return reinterpret_cast<uint16_t *>(h_meta.as<uint8_t>() + m_len); }
     uint32_t *h_sn() const { return reinterpret_cast<uint32_t *>(h_meta.as<uint8_t>() + m_sn); }
@@ -287,30 +333,53 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
 {
     if (!tx || !pkt || !pkt_len || (len && !datagram)) return KFEC_EINVAL;
     kfec_txq *q = tx->q;
-    if (len > q->mtu || kn_changed(q->ctx, q->K, q->N)) return KFEC_EINVAL;
+    const bool defer = q->defer;
+    if (len > q->mtu || kn_changed(q->ctx, q->K, q->N) || (!defer && (!pkt || !pkt_len))) return KFEC_EINVAL;
     const bool completes = tx->conv != 0 && tx->cached + 1 == q->K;
     if (completes && q->n == q->G) return KFEC_ENOMEM;
-    if (tx->conv != 0 && q->used + round4(len) > q->cap) {
-        if (q->n) return KFEC_ENOMEM;  // a flush frees the queued groups' bytes
-        int rc = tx_compact(q);        // first reclaim what no partial group holds any more
-        if (!rc && q->used + round4(len) > q->cap) rc = grow_arena(q->h_dg, q->d_dg, q->up, q->used, round4(len), q->cap);
+    // staged bytes: the datagram (group cache) and, deferred, the data packet around it
+    const size_t need = round4(len + (defer ? KFEC_PKT_DATA_HEADER : 0));
+    if ((tx->conv != 0 || defer) && q->used + need > q->cap) {
+        if (q->n || !q->dpk.empty()) return KFEC_ENOMEM;  // a flush frees the queued bytes
+        int rc = tx_compact(q);                            // first reclaim what no partial group holds any more
+        if (!rc && q->used + need > q->cap) rc = grow_arena(q->h_dg, q->d_dg, q->up, q->used, need, q->cap);
         if (rc) return rc;
     }
+    if (defer) {
+        try {
+            q->dpk.reserve(q->dpk.size() + 1);
+        } catch (...) {
+            return KFEC_ENOMEM;
+        }
+    }
     // create_fec_data_packet (connections.cpp:395-411), sub_sn = fec_snd_sub_sn++ (client.cpp:805-806)
-    put_le32(pkt, timestamp);
-    put_be32(pkt + 4, tx->sn);
-    pkt[8] = tx->sub_sn++;
-    if (len) std::memcpy(pkt + KFEC_PKT_DATA_HEADER, datagram, len);
-    *pkt_len = KFEC_PKT_DATA_HEADER + len;
+    const uint8_t sub = tx->sub_sn++;
+    uint8_t *dst = defer ? q->h_dg.as<uint8_t>() + q->used : pkt;  // deferred: staged for the flush
+    put_le32(dst, timestamp);
+    put_be32(dst + 4, tx->sn);
+    dst[8] = sub;
+    if (len) std::memcpy(dst + KFEC_PKT_DATA_HEADER, datagram, len);
+    if (pkt_len) *pkt_len = defer ? 0 : KFEC_PKT_DATA_HEADER + len;
+    const int32_t slot = completes ? (int32_t)q->n : -1;
+    if (defer) {
+        q->dpk.push_back({q->used, (uint32_t)(KFEC_PKT_DATA_HEADER + len), tx->sn, sub, slot, tx->tag});
+        if (tx->conv == 0) {
+            q->used += need;
+            q->up.grow(q->h_dg, q->d_dg, q->used);
+        }
+    }
     if (tx->conv == 0) {  // client.cpp:811-815
         tx->sub_sn = 0;
         return KFEC_OK;
     }
-    if (len) std::memcpy(q->h_dg.as<uint8_t>() + q->used, datagram, len);
-    tx->cache_off[tx->cached] = q->used;
+    if (!defer && len) std::memcpy(q->h_dg.as<uint8_t>() + q->used, datagram, len);
+    tx->cache_off[tx->cached] = q->used + (defer ? KFEC_PKT_DATA_HEADER : 0);
     tx->cache_len[tx->cached++] = (uint16_t)len;
-    q->used += round4(len);
-    if (!completes) return KFEC_OK;
+    q->used += need;
+    if (!completes) {
+        if (defer) q->up.grow(q->h_dg, q->d_dg, q->used);
+        return KFEC_OK;
+    }
     // the group is complete: it takes queue slot n (compact_into_container + encode run at the flush)
     const size_t g = q->n;
     for (size_t i = 0; i < q->K; ++i) {
@@ -331,14 +400,15 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
 int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *user, void *stream)
 {
     if (!q) return KFEC_EINVAL;
-    const size_t n = q->n;
-    if (n == 0) return KFEC_OK;
+    const size_t n = q->n, nd = q->dpk.size();
+    if (n == 0 && nd == 0) return KFEC_OK;
     if (kn_changed(q->ctx, q->K, q->N)) return KFEC_EINVAL;  // the coder was reset: recreate the queue
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t K = q->K, R = q->R;
     const size_t B = q->mtu + KFEC_FEC_CONTAINER_HEADER, pitch = round4(B);
     const size_t pkt_pitch = round4(KFEC_PKT_REDUNDANT_HEADER + B);
-    const size_t nk = n * K;
+    const size_t nk = n * K, nr = n * R;
+    const bool seal = q->seal_mode != KFEC_TXQ_SEAL_OFF;
     // pack the used tables back to back (each destination lies below its source, and below the sources still
     // to be moved): [off nk*8][len nk*2][pad][sn n*4][conv n*4]
     uint8_t *hm = q->h_meta.as<uint8_t>();
@@ -349,34 +419,133 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
     uint8_t *dm = q->d_meta.as<uint8_t>();
     const uint64_t *d_off = reinterpret_cast<const uint64_t *>(dm);
     const uint16_t *d_len = reinterpret_cast<const uint16_t *>(dm + L);
+    // sealed rows: the nd data packets, then the n x R redundant packets; descriptors up in one copy:
+    // [data off nd*8][data len nd*4][pad][iv rows*2]; down: [rows][spitch] sealed, then out_len rows*4
+    const size_t rows = seal ? nd + nr : 0;
+    const size_t spitch = round4(KFEC_PKT_REDUNDANT_HEADER + B + seal_overhead(q->seal_mode));
+    const size_t dL = nd * 8, dI = round8(dL + nd * 4), dT = dI + rows * 2;
+    const size_t sO = rows * spitch, sT = sO + rows * 4;
+    if (seal) {
+        if (q->h_sdesc.ensure(dT) || q->d_sdesc.ensure(dT + nr * 12 + 8) || q->h_sealed.ensure(sT) || q->d_sealed.ensure(sT))
+            return KFEC_ENOMEM;
+        uint8_t *hd = q->h_sdesc.as<uint8_t>();
+        uint16_t *iv = reinterpret_cast<uint16_t *>(hd + dI);
+        for (size_t i = 0; i < nd; ++i) {
+            reinterpret_cast<uint64_t *>(hd)[i] = q->dpk[i].off;
+            reinterpret_cast<uint32_t *>(hd + dL)[i] = q->dpk[i].len;
+        }
+        // iv draws in emission order (see kfec_txq_flush): data packet i, then its group's redundant packets
+        auto red_ivs = [&](size_t g) {
+            for (size_t r = 0; r < R; ++r) iv[nd + g * R + r] = iv_draw(q->iv_seed, q->iv_ctr++);
+        };
+        if (q->defer) {
+            for (size_t i = 0; i < nd; ++i) {
+                iv[i] = iv_draw(q->iv_seed, q->iv_ctr++);
+                if (q->dpk[i].group >= 0) red_ivs((size_t)q->dpk[i].group);
+            }
+        } else {
+            for (size_t g = 0; g < n; ++g) red_ivs(g);
+        }
+        if (hipMemcpyAsync(q->d_sdesc.p, hd, dT, hipMemcpyHostToDevice, s) != hipSuccess) return KFEC_EHIP;
+    }
     if (q->up.finish(q->h_dg, q->d_dg, q->used, s) ||
-        hipMemcpyAsync(dm, hm, T, hipMemcpyHostToDevice, s) != hipSuccess)
+        (n && hipMemcpyAsync(dm, hm, T, hipMemcpyHostToDevice, s) != hipSuccess))
         return KFEC_EHIP;
     const size_t arena = std::max<size_t>(q->used, 4);
-    int rc = kfec_encode_framed_batch(q->ctx, n, q->d_dg.p, arena, d_off, d_len, B, pitch, q->d_par.p,
+    const size_t P = nr * pkt_pitch;  // [n][R] compact redundant packets, then their lengths
+    uint8_t *dr = q->d_res.as<uint8_t>();
+    int rc = KFEC_OK;
+    if (n) {
+        rc = kfec_encode_framed_batch(q->ctx, n, q->d_dg.p, arena, d_off, d_len, B, pitch, q->d_par.p,
                                       q->d_align.as<uint16_t>(), stream);
-    if (rc) return rc;
-    const size_t P = n * R * pkt_pitch;  // [n][R] compact redundant packets, then their lengths
-    if (R) {
-        uint8_t *dr = q->d_res.as<uint8_t>();
-        rc = kfec_pack_batch(q->ctx, n, KFEC_PACK_REDUNDANT | KFEC_PACK_COMPACT, q->d_dg.p, arena, d_off, d_len, pitch,
-                             q->d_par.p, q->d_align.as<uint16_t>(), reinterpret_cast<const uint32_t *>(dm + S),
-                             reinterpret_cast<const uint32_t *>(dm + C), timestamp, dr, pkt_pitch,
-                             reinterpret_cast<uint16_t *>(dr + P), stream);
         if (rc) return rc;
-        if (hipMemcpyAsync(q->h_res.p, dr, P + n * R * 2, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
+        if (R) {
+            rc = kfec_pack_batch(q->ctx, n, KFEC_PACK_REDUNDANT | KFEC_PACK_COMPACT, q->d_dg.p, arena, d_off, d_len,
+                                 pitch, q->d_par.p, q->d_align.as<uint16_t>(), reinterpret_cast<const uint32_t *>(dm + S),
+                                 reinterpret_cast<const uint32_t *>(dm + C), timestamp, dr, pkt_pitch,
+                                 reinterpret_cast<uint16_t *>(dr + P), stream);
+            if (rc) return rc;
+        }
+    }
+    if (seal) {
+        uint8_t *ds = q->d_sdesc.as<uint8_t>();
+        const uint16_t *d_iv = reinterpret_cast<const uint16_t *>(ds + dI);
+        uint8_t *sealed = q->d_sealed.as<uint8_t>();
+        uint32_t *out_len = reinterpret_cast<uint32_t *>(sealed + sO);
+        const kfec_aead *a = q->aead;
+        // the staged data packets, straight from the arena
+        rc = seal_rows(q->seal_mode, a, nd, q->d_dg.p, arena, reinterpret_cast<const uint64_t *>(ds),
+                       reinterpret_cast<const uint32_t *>(ds + dL), d_iv, sealed, spitch, out_len, stream);
+        if (rc) return rc;
+        if (nr) {  // the redundant packets the pack just wrote
+            uint64_t *r_off = reinterpret_cast<uint64_t *>(ds + round8(dT));
+            uint32_t *r_len = reinterpret_cast<uint32_t *>(r_off + nr);
+            if (kfec::launch_pkt_desc(nr, pkt_pitch, reinterpret_cast<const uint16_t *>(dr + P), r_off, r_len, s))
+                return KFEC_EHIP;
+            rc = seal_rows(q->seal_mode, a, nr, dr, std::max<size_t>(P, 4), r_off, r_len, d_iv + nd,
+                           sealed + nd * spitch, spitch, out_len + nd, stream);
+            if (rc) return rc;
+        }
+        if (hipMemcpyAsync(q->h_sealed.p, sealed, sT, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
+    } else if (nr) {
+        if (hipMemcpyAsync(q->h_res.p, dr, P + nr * 2, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
     }
     if (hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
     const uint32_t *sn = reinterpret_cast<const uint32_t *>(hm + S);
     const uint8_t *pk = q->h_res.as<uint8_t>();
     const uint16_t *pk_len = reinterpret_cast<const uint16_t *>(pk + P);
-    for (size_t g = 0; g < n && cb; ++g)
+    const uint8_t *hs = q->h_sealed.as<uint8_t>();
+    const uint32_t *s_len = reinterpret_cast<const uint32_t *>(hs + sO);
+    auto emit_red = [&](size_t g) {
         for (size_t r = 0; r < R; ++r) {
-            const uint16_t len = pk_len[g * R + r];
-            if (len) cb(user, q->tags[g], sn[g], (uint8_t)(K + r), pk + (g * R + r) * pkt_pitch, len);
+            const size_t i = g * R + r;
+            const uint8_t *p = seal ? hs + (nd + i) * spitch : pk + i * pkt_pitch;
+            const size_t len = seal ? s_len[nd + i] : pk_len[i];
+            if (len) cb(user, q->tags[g], sn[g], (uint8_t)(K + r), p, len);
         }
+    };
+    if (cb) {
+        if (q->defer) {  // send order; a group's redundant packets right after the data packet completing it
+            for (size_t i = 0; i < nd; ++i) {
+                const kfec_txq::DataPkt &d = q->dpk[i];
+                const uint8_t *p = seal ? hs + i * spitch : q->h_dg.as<uint8_t>() + d.off;
+                const size_t len = seal ? s_len[i] : d.len;
+                if (len) cb(user, d.tag, d.sn, d.sub, p, len);
+                if (d.group >= 0) emit_red((size_t)d.group);
+            }
+        } else {
+            for (size_t g = 0; g < n; ++g) emit_red(g);
+        }
+    }
     q->n = 0;
+    q->dpk.clear();
     return tx_compact(q);  // keep the partial groups, at the front of the arena
+}
+
+size_t kfec_txq_staged(const kfec_txq *q) { return q ? q->dpk.size() : 0; }
+
+int kfec_txq_seal(kfec_txq *q, int mode, const kfec_aead *aead, uint64_t iv_seed, unsigned flags)
+{
+    if (!q || (flags & ~KFEC_TXQ_DEFER_DATA) || q->n || !q->dpk.empty()) return KFEC_EINVAL;
+    if (mode != KFEC_TXQ_SEAL_OFF) {
+        if (!seal_mode_ok(mode, aead) || (aead && aead->device != kfec_device(q->ctx))) return KFEC_EINVAL;
+    } else if (aead) {
+        return KFEC_EINVAL;
+    }
+    const bool defer = (flags & KFEC_TXQ_DEFER_DATA) != 0;
+    if (defer && !q->defer) {  // every data packet now takes its 9-byte header in the arena too
+        const size_t slot = std::max<size_t>(round4(q->mtu + KFEC_PKT_DATA_HEADER), 4);
+        if (slot * q->G * q->K > q->cap) {
+            if (q->up.cs && hipStreamSynchronize(q->up.cs) != hipSuccess) return KFEC_EHIP;
+            if (grow_arena(q->h_dg, q->d_dg, q->up, q->used, slot * q->G * q->K - q->used, q->cap)) return KFEC_ENOMEM;
+        }
+    }
+    q->seal_mode = mode;
+    q->aead = mode == KFEC_TXQ_SEAL_OFF ? nullptr : aead;
+    q->iv_seed = iv_seed;
+    q->iv_ctr = 0;
+    q->defer = defer;
+    return KFEC_OK;
 }
 
 }  // extern "C"
@@ -695,6 +864,117 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
         }
     q->n = 0;
     return rx_compact(q);  // keep the shards of the groups still waiting for K shares
+}
+
+}  // extern "C"
+
+// ---- receive-side packet opening (decrypt_data on the device, ahead of kfec_rx_push) --------------------
+struct kfec_opener {
+    int mode = KFEC_SEAL_CHECKSUM;
+    const kfec_aead *aead = nullptr;
+    int device = 0;
+    size_t max_packets = 0, max_packet = 0, pitch = 0;
+    size_t n = 0, used = 0;
+    // h_arena: the staged packets (4-byte offsets); h_desc: off u64 [n], len u32 [n] (one copy up);
+    // h_out: [n][pitch] plaintext, then out_len u32 [n], then ok u8 [n] (one copy down)
+    Pinned h_arena, h_desc, h_out;
+    Device d_arena, d_desc, d_out;
+    std::vector<uint64_t> tags;
+};
+
+extern "C" {
+
+int kfec_opener_create(int mode, const kfec_aead *aead, size_t max_packets, size_t max_packet, kfec_opener **out)
+{
+    if (!out) return KFEC_EINVAL;
+    *out = nullptr;
+    if (!max_packets || !max_packet || max_packet > 0xFFFFFF || !seal_mode_ok(mode, aead)) return KFEC_EINVAL;
+    int dev = 0, count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || hipGetDevice(&dev) != hipSuccess) return KFEC_ENODEV;
+    if (aead && aead->device != dev) return KFEC_EINVAL;
+    kfec_opener *o = new (std::nothrow) kfec_opener;
+    if (!o) return KFEC_ENOMEM;
+    o->mode = mode;
+    o->aead = aead;
+    o->device = dev;
+    o->max_packets = max_packets;
+    o->max_packet = max_packet;
+    o->pitch = round4(max_packet);
+    const size_t arena = max_packets * round4(max_packet), desc = max_packets * 12,
+                 res = max_packets * (o->pitch + 5);
+    try {
+        o->tags.resize(max_packets);
+    } catch (...) {
+        delete o;
+        return KFEC_ENOMEM;
+    }
+    if (o->h_arena.ensure(arena) || o->h_desc.ensure(desc) || o->h_out.ensure(res) || o->d_arena.ensure(arena) ||
+        o->d_desc.ensure(desc) || o->d_out.ensure(res)) {
+        delete o;
+        return KFEC_ENOMEM;
+    }
+    *out = o;
+    return KFEC_OK;
+}
+
+void kfec_opener_destroy(kfec_opener *o)
+{
+    if (!o) return;
+    (void)hipSetDevice(o->device);
+    delete o;
+}
+
+size_t kfec_opener_pending(const kfec_opener *o) { return o ? o->n : 0; }
+
+int kfec_opener_add(kfec_opener *o, const uint8_t *pkt, size_t len, uint64_t tag)
+{
+    if (!o || (len && !pkt) || len > o->max_packet) return KFEC_EINVAL;
+    if (o->n == o->max_packets) return KFEC_ENOMEM;
+    const size_t i = o->n++;
+    if (len) std::memcpy(o->h_arena.as<uint8_t>() + o->used, pkt, len);
+    reinterpret_cast<uint64_t *>(o->h_desc.p)[i] = o->used;
+    o->tags[i] = tag;
+    // lengths follow the offsets once the batch size is known (kfec_opener_flush packs them)
+    reinterpret_cast<uint32_t *>(o->h_desc.as<uint8_t>() + o->max_packets * 8)[i] = (uint32_t)len;
+    o->used += round4(len);
+    return KFEC_OK;
+}
+
+int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *stream)
+{
+    if (!o) return KFEC_EINVAL;
+    const size_t n = o->n;
+    if (n == 0) return KFEC_OK;
+    if (hipSetDevice(o->device) != hipSuccess) return KFEC_EHIP;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    uint8_t *hd = o->h_desc.as<uint8_t>();
+    std::memmove(hd + n * 8, hd + o->max_packets * 8, n * 4);  // [off n*8][len n*4]: one copy
+    uint8_t *dd = o->d_desc.as<uint8_t>();
+    uint8_t *dr = o->d_out.as<uint8_t>();
+    const size_t L = n * o->pitch;
+    uint32_t *out_len = reinterpret_cast<uint32_t *>(dr + L);
+    uint8_t *ok = dr + L + n * 4;
+    const size_t arena = std::max<size_t>(o->used, 4);
+    if (hipMemcpyAsync(o->d_arena.p, o->h_arena.p, arena, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(dd, hd, n * 12, hipMemcpyHostToDevice, s) != hipSuccess)
+        return KFEC_EHIP;
+    const uint64_t *d_off = reinterpret_cast<const uint64_t *>(dd);
+    const uint32_t *d_len = reinterpret_cast<const uint32_t *>(dd + n * 8);
+    const int rc = o->aead ? kfec_aead_open_batch(o->aead, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok,
+                                                 stream)
+                           : kfec_open_batch(o->mode, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok,
+                                             stream);
+    if (rc) return rc;
+    if (hipMemcpyAsync(o->h_out.p, dr, L + n * 5, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return KFEC_EHIP;
+    const uint8_t *ho = o->h_out.as<uint8_t>();
+    const uint32_t *h_len = reinterpret_cast<const uint32_t *>(ho + L);
+    const uint8_t *h_ok = ho + L + n * 4;
+    for (size_t i = 0; i < n && cb; ++i) cb(user, o->tags[i], ho + i * o->pitch, h_ok[i] ? h_len[i] : 0, h_ok[i] ? 1 : 0);
+    o->n = 0;
+    o->used = 0;
+    return KFEC_OK;
 }
 
 }  // extern "C"

@@ -109,6 +109,13 @@ def load_library():
         "kfec_rx_cached": (sz, [_vp]),
         "kfec_rx_push": (C.c_int, [_vp, _u8p, sz, C.POINTER(_u8p), _szp]),
         "kfec_rxq_flush": (C.c_int, [_vp, _vp, _vp, _vp]),
+        "kfec_txq_seal": (C.c_int, [_vp, C.c_int, _vp, C.c_uint64, C.c_uint]),
+        "kfec_txq_staged": (sz, [_vp]),
+        "kfec_opener_create": (C.c_int, [C.c_int, _vp, sz, sz, C.POINTER(_vp)]),
+        "kfec_opener_destroy": (None, [_vp]),
+        "kfec_opener_pending": (sz, [_vp]),
+        "kfec_opener_add": (C.c_int, [_vp, _u8p, sz, C.c_uint64]),
+        "kfec_opener_flush": (C.c_int, [_vp, _vp, _vp, _vp]),
         "kfec_seal_batch": (C.c_int, [C.c_int, sz, _vp, sz, _vp, _vp, _vp, sz, _vp, _vp]),
         "kfec_open_batch": (C.c_int, [C.c_int, sz, _vp, sz, _vp, _vp, _vp, sz, _vp, _vp, _vp]),
         # include/kfec_aead.h

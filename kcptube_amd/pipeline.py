@@ -20,6 +20,27 @@ from .fec import FecCode, KfecError, _check
 _u8p = C.POINTER(C.c_uint8)
 PACKET_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint8, _u8p, C.c_size_t)
 DATAGRAM_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint8, _u8p, C.c_size_t)
+OPENED_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64, _u8p, C.c_size_t, C.c_int)
+
+SEAL_OFF = -1        # KFEC_TXQ_SEAL_OFF
+SEAL_CHECKSUM = 0    # KFEC_SEAL_CHECKSUM: encryption none (checksum16 trailer)
+SEAL_PLAIN_XOR = 1   # KFEC_SEAL_PLAIN_XOR
+DEFER_DATA = 1       # KFEC_TXQ_DEFER_DATA
+
+
+def iv_draw(seed: int, i: int) -> int:
+    """iv_raw of the i-th sealed packet of a queue (kfec_txq_seal): top 16 bits of splitmix64(seed + i)."""
+    m = (1 << 64) - 1
+    x = (seed + i + 0x9E3779B97F4A7C15) & m
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & m
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & m
+    return (x ^ (x >> 31)) >> 48
+
+
+def _mode_and_handle(mode, aead):
+    if aead is not None:
+        return aead.mode, aead._h
+    return int(mode), None
 
 
 class TxQueue:
@@ -38,8 +59,20 @@ class TxQueue:
     def capacity(self) -> int:
         return int(self._lib.kfec_txq_capacity(self._q))
 
+    def seal(self, mode: int = SEAL_CHECKSUM, aead=None, iv_seed: int = 0, defer_data: bool = True) -> None:
+        """kfec_txq_seal: protect every emitted packet on the device (mode SEAL_CHECKSUM / SEAL_PLAIN_XOR, or an
+        AeadCipher whose mode is used); defer_data stages the data packets for the flush as well."""
+        m, h = _mode_and_handle(mode, aead)
+        self._aead = aead  # the cipher must outlive the queue's use of it
+        _check(self._lib.kfec_txq_seal(self._q, m, h, iv_seed & ((1 << 64) - 1), DEFER_DATA if defer_data else 0),
+               "kfec_txq_seal")
+
+    def staged(self) -> int:
+        return int(self._lib.kfec_txq_staged(self._q))
+
     def flush(self, timestamp: int = 0) -> list[tuple[int, int, int, bytes]]:
-        """Encode every queued group; returns [(tag, sn, sub_sn, redundant packet bytes)] in queue order."""
+        """Encode every queued group; returns [(tag, sn, sub_sn, packet bytes)] in emission order: the redundant
+        packets in queue order or, with deferred data packets, every packet in the order fec_maker sends it."""
         out = []
 
         def cb(_user, tag, sn, sub, ptr, n):
@@ -68,7 +101,8 @@ class FecSender:
         _check(self._lib.kfec_tx_create(q._q, conv & 0xFFFFFFFF, tag, C.byref(self._tx)), "kfec_tx_create")
 
     def send(self, datagram: bytes, timestamp: int = 0) -> bytes:
-        """fec_maker(datagram): the data packet (the group, once complete, is queued for the flush)."""
+        """fec_maker(datagram): the data packet (the group, once complete, is queued for the flush); b"" when
+        the queue defers data packets to its flush."""
         d = (C.c_uint8 * max(len(datagram), 1)).from_buffer_copy(bytes(datagram) or b"\0")
         pkt = (C.c_uint8 * (len(datagram) + 16))()
         n = C.c_size_t(0)
@@ -148,5 +182,45 @@ class FecReceiver:
         try:
             if self._rx.value:
                 self._lib.kfec_rx_destroy(self._rx)
+        except Exception:
+            pass
+
+
+class Opener:
+    """kfec_opener: decrypt_data for batches of received packets on the device, ahead of FecReceiver.push."""
+
+    def __init__(self, mode: int = SEAL_CHECKSUM, aead=None, max_packets: int = 1024, max_packet: int = 1500):
+        from .fec import load_library
+        self._lib = load_library()
+        self._aead = aead
+        m, h = _mode_and_handle(mode, aead)
+        self._o = C.c_void_p()
+        _check(self._lib.kfec_opener_create(m, h, max_packets, max_packet, C.byref(self._o)), "kfec_opener_create")
+
+    def pending(self) -> int:
+        return int(self._lib.kfec_opener_pending(self._o))
+
+    def add(self, pkt: bytes, tag: int = 0) -> None:
+        buf = (C.c_uint8 * max(len(pkt), 1)).from_buffer_copy(bytes(pkt) or b"\0")
+        rc = self._lib.kfec_opener_add(self._o, buf, len(pkt), tag)
+        if rc == -4:
+            raise KfecError("kfec_opener_add: batch full, flush first")
+        _check(rc, "kfec_opener_add")
+
+    def flush(self) -> list[tuple[int, bytes, bool]]:
+        """Open every staged packet; returns [(tag, plaintext, ok)] in staging order (plaintext b"" if not ok)."""
+        out = []
+
+        def cb(_user, tag, ptr, n, ok):
+            out.append((int(tag), C.string_at(ptr, n) if n else b"", bool(ok)))
+
+        fn = OPENED_CB(cb)
+        _check(self._lib.kfec_opener_flush(self._o, C.cast(fn, C.c_void_p), None, None), "kfec_opener_flush")
+        return out
+
+    def __del__(self):
+        try:
+            if self._o.value:
+                self._lib.kfec_opener_destroy(self._o)
         except Exception:
             pass

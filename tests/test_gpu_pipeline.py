@@ -308,3 +308,121 @@ def test_cpp_program_over_the_pipeline_header(dev):
     assert p.returncode == 0, p.stdout + p.stderr
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["bad"] == 0 and r["recovered"] == r["recovered_expected"] == 2 * 512 * 3 * 3
+
+
+_SEAL_MODES = {"none": 0, "plain_xor": 1}
+
+
+def _ref_seal(enc: str, password: bytes, pkt: bytes, iv: int) -> bytes:
+    from oracle import aead_oracle as ao
+    if enc in _SEAL_MODES:
+        return fo.seal(pkt, _SEAL_MODES[enc])
+    return ao.aead_seal(enc, password, pkt, iv)
+
+
+def _ref_open(enc: str, password: bytes, pkt: bytes):
+    from oracle import aead_oracle as ao
+    if enc in _SEAL_MODES:
+        r = fo.open_(pkt, _SEAL_MODES[enc])
+        return (b"", False) if r is None else r
+    return ao.aead_open(enc, password, pkt)
+
+
+@pytest.mark.parametrize("enc", ["none", "plain_xor", "chacha20", "aes_gcm"])
+def test_sealed_pipeline_through_lossy_channel(dev, oracle, enc):
+    """data_sender's encrypt_data on every packet fec_maker emits (client.cpp:780-840), on the device: the
+    queue stages the data packets (KFEC_TXQ_DEFER_DATA), and each flush emits every packet sealed, in the order
+    the reference sends them -- byte-exact against FecTx + encrypt_data with the queue's iv draws replayed.  The
+    receiver opens the sealed packets in device batches (kfec_opener, decrypt_data) and feeds kfec_rx_push: same
+    recovered datagrams as the oracle's fec_unpack / fec_find_missings over the oracle-opened packets; a
+    tampered packet fails to open and is dropped, as the reference drops it."""
+    from kcptube_amd.aead import AeadCipher
+    from kcptube_amd.pipeline import FecReceiver, FecSender, Opener, RxQueue, TxQueue, iv_draw
+    K, N, mtu = 6, 9, 300
+    password, seed = b"kcptube-test-password", 0x1234_5678_9ABC_DEF0
+    c = _coder(K, N)
+    q = TxQueue(c, max_groups=16, max_datagram=mtu)
+    cipher = None if enc in _SEAL_MODES else AeadCipher(enc, password)
+    q.seal(_SEAL_MODES.get(enc, 0), aead=cipher, iv_seed=seed)
+    rng = random.Random(sum(enc.encode()))
+    conns = 3
+    txs = [FecSender(q, conv=0x300 + i, tag=i) for i in range(conns)]
+    refs = [fo.FecTx(K, N, lambda d, t, a: oracle.encode(K, N, d, a, t), conv=0x300 + i) for i in range(conns)]
+    got, exp_plain = [], []
+    for step in range(K * 8 * conns + 5):
+        i = rng.randrange(conns)
+        d = rng.randbytes(rng.choice([0, 1, mtu, rng.randint(0, mtu)]))
+        assert txs[i].send(d, timestamp=99) == b""  # deferred: nothing leaves before the flush
+        exp_plain += [(i, p) for p in refs[i].send(d, timestamp=99)]
+        if q.pending() == 16 or rng.random() < 0.04:
+            got += q.flush(timestamp=99)
+    got += q.flush(timestamp=99)
+    assert q.staged() == 0 and q.pending() == 0
+    # the sealed stream equals the reference's plain stream sealed with the replayed iv draws
+    exp = [(t, _ref_seal(enc, password, p, iv_draw(seed, k))) for k, (t, p) in enumerate(exp_plain)]
+    assert len(got) == len(exp) > 100
+    assert [(t, p) for t, _, _, p in got] == exp
+    # receive: lossy, reordered channel; one tampered packet
+    kept = [(t, p) for t, p in exp if rng.random() >= 0.08]
+    for j in range(0, len(kept) - 1, 7):
+        kept[j], kept[j + 1] = kept[j + 1], kept[j]
+    bad = len(kept) // 2
+    t_bad, p_bad = kept[bad]
+    kept[bad] = (t_bad, p_bad[:3] + bytes([p_bad[3] ^ 0x40]) + p_bad[4:])
+    op = Opener(_SEAL_MODES.get(enc, 0), aead=cipher, max_packets=64, max_packet=mtu + 64)
+    rq = RxQueue(c, max_groups=64, max_shard=mtu + 2)
+    rx = [FecReceiver(rq, tag=i) for i in range(conns)]
+    ref_rx = [fo.FecRx(K, N, lambda s, a: oracle.decode(K, N, s, a)) for _ in range(conns)]
+    out, exp_out = [[] for _ in range(conns)], [[] for _ in range(conns)]
+    n_bad = 0
+
+    def drain():
+        nonlocal n_bad
+        for tag, plain, ok in op.flush():
+            if not ok:
+                n_bad += 1
+                continue
+            own, _ = rx[tag].push(plain)
+            if own is not None:
+                out[tag].append(own)
+        for tag, sn, idx, d in rq.flush():
+            out[tag].append(d)
+
+    for t, p in kept:
+        plain, ok = _ref_open(enc, password, p)
+        if ok:
+            exp_out[t] += ref_rx[t].push(plain)
+        op.add(p, tag=t)
+        if op.pending() == 64:
+            drain()
+    drain()
+    assert n_bad == 1
+    for i in range(conns):
+        assert sorted(out[i]) == sorted(exp_out[i]), i
+    assert sum(r.recovered for r in ref_rx) > 3
+
+
+def test_txq_seal_arguments(dev):
+    """kfec_txq_seal refuses an unknown mode, an AEAD mode without its cipher, a cipher with a checksum mode,
+    and a change while packets are staged."""
+    from kcptube_amd.aead import AeadCipher
+    from kcptube_amd.fec import KfecError
+    from kcptube_amd.pipeline import FecSender, TxQueue
+    c = _coder(4, 6)
+    q = TxQueue(c, 4, 64)
+    with pytest.raises(KfecError):
+        q.seal(9)
+    with pytest.raises(KfecError):
+        q.seal(6)  # chacha20 without a cipher
+    cipher = AeadCipher("chacha20", b"pw")
+    assert c._lib.kfec_txq_seal(q._q, 0, cipher._h, 0, 1) == -1  # a cipher with a checksum mode
+    assert c._lib.kfec_txq_seal(q._q, 4, cipher._h, 0, 1) == -1  # a cipher of another mode
+    q.seal(0, defer_data=True)
+    tx = FecSender(q, conv=1)
+    assert tx.send(b"abc") == b""
+    with pytest.raises(KfecError):
+        q.seal(1)  # a packet is staged
+    pk = q.flush()
+    assert [p for _, _, _, p in pk] == [fo.seal(fo.data_packet(b"abc", 0, 0, 0), 0)]
+    q.seal(-1, defer_data=False)  # back to plain, immediate data packets
+    assert tx.send(b"d") == fo.data_packet(b"d", 0, 1, 0)
