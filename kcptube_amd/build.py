@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libkfec.so")
 COMPAT_TEST = os.path.join(PKG, "compat_test")
 
-SOURCES = ["kfec_kernels.hip", "kfec_frame.hip", "kfec_seal.hip", "kfec_aead.hip", "kfec_gcm.hip", "kfec_ocb.hip", "kfec_api.cpp", "kfec_pipeline.cpp"]
+SOURCES = ["kfec_kernels.hip", "kfec_frame.hip", "kfec_seal.hip", "kfec_aead.hip", "kfec_gcm.hip", "kfec_ocb.hip", "kfec_worker.hip", "kfec_api.cpp", "kfec_pipeline.cpp"]
 HEADERS = ["kfec_gf.hpp", "kfec_internal.hpp", "kfec_aes.hpp", "kfec_pkt.hpp"]
 
 

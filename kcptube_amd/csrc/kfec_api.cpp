@@ -28,6 +28,7 @@ struct kfec_ctx {
     size_t stage_cap = 0;
     uint8_t *h_stage = nullptr;  // fine-grained pinned host staging the kernels read and write in place
     size_t h_stage_cap = 0;
+    uint64_t mat_id = 0;         // unique id of the current matrix (the resident worker's table cache key)
 };
 
 int kfec::current_device_cus()
@@ -48,6 +49,10 @@ int kfec::current_device_cus()
 namespace {
 
 bool kn_valid(size_t K, size_t N) { return !(K == 0 || N == 0 || K > 256 || N > 256 || K > N); }
+
+std::atomic<uint64_t> g_mat_ids{0};
+std::mutex g_live_mu;
+int g_live[64];  // coders per device: the resident workers of a device stop with its last coder
 
 int probe_device(kfec::DeviceInfo &di)
 {
@@ -83,6 +88,7 @@ int build_matrix(kfec_ctx *c, size_t K, size_t N)
     c->h_enc.swap(h);
     c->K = K;
     c->N = N;
+    c->mat_id = g_mat_ids.fetch_add(1) + 1;
     return KFEC_OK;
 }
 
@@ -139,6 +145,8 @@ const char *kfec_version(void) { return "kfec 0.3 (gfx950 perm-MAC, flattened co
 
 int kfec_device(const kfec_ctx *ctx) { return ctx ? ctx->di.device : -1; }
 
+uint64_t kfec_worker_requests(void) { return kfec::worker_served(); }
+
 int kfec_create(size_t K, size_t N, kfec_ctx **out)
 {
     if (!out) return KFEC_EINVAL;
@@ -158,6 +166,10 @@ int kfec_create(size_t K, size_t N, kfec_ctx **out)
     if (rc) {
         kfec_destroy(c);
         return rc;
+    }
+    if (di.device >= 0 && di.device < 64) {
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        ++g_live[di.device];
     }
     *out = c;
     return KFEC_OK;
@@ -180,7 +192,13 @@ void kfec_destroy(kfec_ctx *ctx)
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    const int dev = ctx->di.device;
+    const bool counted = ctx->mat_id != 0;  // kfec_create returned it
     delete ctx;
+    if (counted && dev >= 0 && dev < 64) {
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        if (--g_live[dev] == 0) kfec::worker_stop(dev);
+    }
 }
 
 size_t kfec_get_K(const kfec_ctx *ctx) { return ctx ? ctx->K : 0; }
@@ -203,6 +221,12 @@ int kfec_encode(const kfec_ctx *cctx, const uint8_t *input, size_t data_length, 
     if (input == nullptr || B == 0 || (data_length / B) % K != 0 || data_length < K * B) return KFEC_EMPTY;
     if (R == 0) return KFEC_OK;
     if (!parity_out) return KFEC_EINVAL;
+    if (kfec::worker_enabled()) {
+        // resident worker: no launch and no stream synchronisation per call (kfec_worker.hip)
+        if (set_dev(ctx)) return KFEC_EHIP;
+        const int wr = kfec::worker_encode(ctx->di.device, ctx->d_enc, ctx->mat_id, (int)K, (int)N, B, input, parity_out);
+        if (wr <= 0) return wr;  // 1: shape the worker does not take
+    }
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (set_dev(ctx)) return KFEC_EHIP;
     const size_t off_par = al256(K * B);
@@ -254,6 +278,35 @@ int kfec_decode(const kfec_ctx *cctx, const size_t *share_ids, const uint8_t *co
         }
         *n_out = m;
         return KFEC_OK;
+    }
+    if (kfec::worker_enabled()) {
+        // The reference's share selection (fecpp.cpp:528-548) as bookkeeping on the ids: row i takes data
+        // share i when present, otherwise the highest id not used yet; the worker does all the arithmetic.
+        const uint8_t *row_ptr[256];
+        uint8_t M[256], P[256];
+        size_t m = 0, lo = 0, hi = n_shares;
+        for (size_t i = 0; i < K; ++i) {
+            if (lo < n_shares && share_ids[lo] == i) {
+                row_ptr[i] = share_ptrs[lo++];
+            } else {
+                --hi;
+                row_ptr[i] = share_ptrs[hi];
+                M[m] = (uint8_t)i;
+                P[m] = (uint8_t)share_ids[hi];
+                ++m;
+            }
+        }
+        if (m == 0) return KFEC_OK;  // every data share present: the reference's empty map
+        if (!out || !out_ids) return KFEC_EINVAL;
+        if (set_dev(ctx)) return KFEC_EHIP;
+        const int wr = kfec::worker_decode(ctx->di.device, ctx->d_enc, ctx->mat_id, (int)K, (int)N, B, row_ptr, (int)m,
+                                           M, P, out);
+        if (wr == 0) {
+            for (size_t t = 0; t < m; ++t) out_ids[t] = M[t];
+            *n_out = m;
+            return KFEC_OK;
+        }
+        if (wr < 0) return wr;
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (set_dev(ctx)) return KFEC_EHIP;

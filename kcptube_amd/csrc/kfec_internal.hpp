@@ -63,6 +63,15 @@ int launch_erasure_masks(uint64_t seed, int N, size_t g0, size_t G, size_t pool,
 int launch_verify(int K, int N, size_t G, size_t B, size_t pitch, const void *d_data, const void *d_out,
                   const uint8_t *d_out_idx, uint64_t *d_mismatch, hipStream_t s);
 
+// resident per-call worker (kfec_worker.hip): 0 done, 1 shape not taken (use the launch path), < 0 KFEC_E*
+bool worker_enabled();
+uint64_t worker_served();  // requests the workers completed (process-wide)
+int worker_encode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int N, size_t B, const uint8_t *input,
+                  uint8_t *parity_out);
+int worker_decode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int N, size_t B,
+                  const uint8_t *const *row_ptr, int m, const uint8_t *M, const uint8_t *P, uint8_t *out);
+void worker_stop(int device);
+
 // framing and wire layer (kfec_frame.hip)
 int launch_frame(int K, int N, bool recv, size_t G, const void *src, size_t src_bytes, const uint64_t *off,
                  const uint16_t *len, const uint64_t *present, size_t B, size_t pitch, void *data, void *parity,

@@ -78,6 +78,7 @@ def load_library():
         "kfec_verify_recovered": (C.c_int, [_vp, sz, sz, sz, _vp, _vp, _vp, _vp, _vp]),
         "kfec_version": (C.c_char_p, []),
         "kfec_device": (C.c_int, [_vp]),
+        "kfec_worker_requests": (C.c_uint64, []),
         # include/kfec_frame.h
         "kfec_frame_data_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, sz, sz, _vp, _vp, _vp]),
         "kfec_encode_framed_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, sz, sz, _vp, _vp, _vp]),
@@ -309,6 +310,11 @@ class FecCode:
         B = pitch if B is None else B
         _check(self._lib.kfec_verify_recovered(self._ctx, G, B, pitch, _dptr(data), _dptr(out), _dptr(out_idx),
                                                _dptr(mismatch), _stream_handle(stream)), "kfec_verify_recovered")
+
+
+def worker_requests() -> int:
+    """Single-group calls served so far by the resident per-call workers (kfec_worker_requests)."""
+    return int(load_library().kfec_worker_requests())
 
 
 def version() -> str:

@@ -31,7 +31,8 @@ int main()
     std::string js = "{\"metric\": \"latency path, fec=20:3 B=1440, one host thread (us per call)\"";
     // single group, host memory in and out
     const int reps = 2000;
-    for (int i = 0; i < 50; ++i) kfec_encode(ctx, data.data(), K * B, B, par.data());
+    for (int i = 0; i < 50; ++i)
+        if (int rc = kfec_encode(ctx, data.data(), K * B, B, par.data())) { printf("kfec_encode rc %d\n", rc); return 2; }
     auto t0 = clk::now();
     for (int i = 0; i < reps; ++i) kfec_encode(ctx, data.data(), K * B, B, par.data());
     js += ", \"kfec_encode_1_group_us\": " + std::to_string(us_since(t0) / reps);
@@ -40,10 +41,15 @@ int main()
     for (size_t s = 3; s < K; ++s) { ids.push_back(s); ptrs.push_back(data.data() + s * B); }
     for (size_t r = 0; r < R; ++r) { ids.push_back(K + r); ptrs.push_back(par.data() + r * B); }
     size_t out_ids[3], n_out = 0;
-    for (int i = 0; i < 50; ++i) kfec_decode(ctx, ids.data(), ptrs.data(), ids.size(), B, out_ids, out.data(), &n_out);
+    for (int i = 0; i < 50; ++i)
+        if (int rc = kfec_decode(ctx, ids.data(), ptrs.data(), ids.size(), B, out_ids, out.data(), &n_out)) {
+            printf("kfec_decode rc %d\n", rc);
+            return 2;
+        }
     t0 = clk::now();
     for (int i = 0; i < reps; ++i) kfec_decode(ctx, ids.data(), ptrs.data(), ids.size(), B, out_ids, out.data(), &n_out);
     js += ", \"kfec_decode_1_group_3_lost_us\": " + std::to_string(us_since(t0) / reps);
+    js += ", \"worker_requests\": " + std::to_string(kfec_worker_requests());
     bool ok = n_out == 3 && !std::memcmp(out.data(), data.data(), 3 * B);
     // small flushes of the batched queues
     for (size_t G : {1, 16, 256, 1024}) {
