@@ -127,13 +127,16 @@ int kfec_verify_recovered(const kfec_ctx *ctx, size_t G, size_t B, size_t pitch,
 const char *kfec_version(void);
 int kfec_device(const kfec_ctx *ctx);
 /* Single-group calls served so far by the resident per-call workers (process-wide; diagnostics).
- * kfec_encode / kfec_decode run on a resident worker workgroup per slot (no launch or stream synchronisation
- * per call) for groups with N - K <= 16 missing / parity rows, (N - K + K) * round16(B) <= 38 KiB and
- * (N - K) * K <= 819; other shapes take a kernel launch.  A worker leaves the GPU after KFEC_WORKER_IDLE_US
+ * kfec_encode / kfec_decode run on a resident worker (KFEC_WORKER_WGS workgroups, default 8, per slot: no
+ * launch or stream synchronisation per call) for groups with N - K <= 16, N * round16(B) <= 36 KiB and
+ * (N - K) * K <= 512; other shapes take a kernel launch.  A worker leaves the GPU after KFEC_WORKER_IDLE_US
  * (default 20000) without a request and when the last coder of its device is destroyed, and is relaunched on
  * demand.  KFEC_WORKER=0 turns the workers off; KFEC_WORKER=1 makes a worker failure an error instead of a
  * switch to the launch path; KFEC_WORKER_SLOTS (1-8, default 2) sets the workers per device. */
 uint64_t kfec_worker_requests(void);
+/* One empty request through a resident worker of the coder's device (diagnostics: the communication floor of
+ * the per-call path).  KFEC_OK, or KFEC_ENODEV when the workers are off. */
+int kfec_worker_ping(const kfec_ctx *ctx);
 
 #ifdef __cplusplus
 }

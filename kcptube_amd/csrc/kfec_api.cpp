@@ -147,6 +147,14 @@ int kfec_device(const kfec_ctx *ctx) { return ctx ? ctx->di.device : -1; }
 
 uint64_t kfec_worker_requests(void) { return kfec::worker_served(); }
 
+int kfec_worker_ping(const kfec_ctx *ctx)
+{
+    if (!ctx) return KFEC_EINVAL;
+    if (set_dev(ctx)) return KFEC_EHIP;
+    const int rc = kfec::worker_ping(ctx->di.device);
+    return rc == 1 ? KFEC_ENODEV : rc;
+}
+
 int kfec_create(size_t K, size_t N, kfec_ctx **out)
 {
     if (!out) return KFEC_EINVAL;

@@ -71,6 +71,7 @@ int worker_encode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int 
 int worker_decode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int N, size_t B,
                   const uint8_t *const *row_ptr, int m, const uint8_t *M, const uint8_t *P, uint8_t *out);
 void worker_stop(int device);
+int worker_ping(int device);  // 0, 1 workers off, < 0 KFEC_E*
 
 // framing and wire layer (kfec_frame.hip)
 int launch_frame(int K, int N, bool recv, size_t G, const void *src, size_t src_bytes, const uint64_t *off,

@@ -6,12 +6,14 @@
 // (kcp.cpp:144, client.cpp:775 -> fec_maker :797).  A launch + hipStreamSynchronize alone costs more than
 // that, so the per-call path cannot pay one per group.
 //
-// How: each worker is a single 512-thread workgroup that stays resident on one CU and polls a doorbell word
-// in fine-grained (coherent) pinned host memory.  The caller copies the group's shares into the slot's
-// pinned stage, writes the doorbell (sequence number + op + K, N, B in ONE 64-bit store), and spins on the
-// slot's completion word.  The worker sees the doorbell over PCIe, pulls the request body and the shares
-// into LDS in one burst of 16-byte loads, computes, writes the parity / recovered shards straight back into
-// the pinned stage, publishes them with a system-scope release, and stores the completion word.
+// How: a worker is W resident workgroups (default 8, one per CU) that poll a doorbell word in fine-grained
+// (coherent) pinned host memory.  The caller copies the group's shares into the slot's pinned stage, writes
+// the doorbell (sequence number + op + K, N, B in ONE 64-bit store) and spins on the slot's completion words.
+// Workgroup w owns the 16-byte column granules [w*G/W, (w+1)*G/W) of every shard (G = pitch / 16): it pulls its
+// slice of the request body's shares into LDS in one burst of 16-byte loads over PCIe, computes its slice of
+// the output rows, writes them straight back into the pinned stage, publishes them with a system-scope
+// release and stores its completion word.  Splitting the columns over CUs splits the PCIe reads, the GF work
+// and the write-back acknowledgements of one small group W ways.
 //
 //   encode  parity_r = XOR_j enc[K+r][j] * D_j                       (fecpp.cpp:504-510)
 //   decode  rows in the reference's selection order (fecpp.cpp:528-548, done by the caller: bookkeeping only),
@@ -21,52 +23,57 @@
 //
 // All GF products use the perm MAC of kfec_gf.hpp with tables in LDS; the parity-row tables of the coder's
 // matrix are copied from its device allocation (enc_tab_offset) once per matrix and kept in LDS while the
-// same matrix is used.  Lifetime: a worker exits when asked (op STOP), or after KFEC_WORKER_IDLE_US without a
-// request (default 20 ms), and always writes its generation to the slot's exit word; the host relaunches it on
-// the next request.  Every wave reaches the exit: the loop's only waits are the bounded doorbell poll and
-// workgroup barriers.
+// same matrix is used.  Lifetime: workgroup 0 leaves after KFEC_WORKER_IDLE_US without a request (default
+// 20 ms) and relays a quit value through the device-memory word the other workgroups poll; all leave on op STOP.  Each
+// writes its generation to its exit word; the host relaunches the worker on the next request.  Every wave
+// reaches the exit: the loop's only waits are the bounded doorbell / quit poll and workgroup barriers.
 #include "kfec_gf.hpp"
 #include "kfec_internal.hpp"
 
 #include <atomic>
-#include <cstdio>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 
 namespace kfec {
 namespace {
 
-constexpr int kWThreads = 512;
+constexpr int kWThreads = 256;             // threads per worker workgroup
+constexpr int kMaxW = 8;                   // workgroups per worker
 constexpr int kMaxR = 16;                  // parity rows (encode) / missing rows (decode) a worker takes
-constexpr size_t kStageMax = 38 * 1024;    // (K + R) * pitch: LDS rows of the shares (20:3 at 1440 B: 33 KB)
-constexpr size_t kTabMax = 16 * 1024;      // R * K * 20 bytes: parity-row perm tables in LDS
-// LDS carve (bytes, all 16-aligned)
+constexpr size_t kStageMax = 36 * 1024;    // (K + R) * pitch of a request
+constexpr size_t kTabMax = 16 * 1024;      // R * K * 32 bytes: parity-row perm tables (8-dword entries) in LDS
+constexpr size_t kSliceMax = 16 * 1024;    // K * ceil(G / W) * 16 bytes: one workgroup's slice of the shares
+// LDS carve of one workgroup (bytes, all 16-aligned)
 constexpr size_t kLdsData = 0;
-constexpr size_t kLdsTab = kLdsData + kStageMax;
-constexpr size_t kLdsCinv = kLdsTab + kTabMax;                    // m x m perm tables of Sinv
-constexpr size_t kLdsGj = kLdsCinv + kMaxR * kMaxR * 20;          // m x 2m Gauss-Jordan matrix (u32 entries)
-constexpr size_t kLdsGf = kLdsGj + kMaxR * 2 * kMaxR * 4;         // exp[512] + log[256]
+constexpr size_t kLdsTab = kLdsData + kSliceMax;
+constexpr size_t kLdsCinv = kLdsTab + kTabMax;                    // m x m perm tables of Sinv (8-dword entries)
+constexpr size_t kLdsGj = kLdsCinv + kMaxR * kMaxR * 32;          // m x 2m Gauss-Jordan matrix (u32 entries)
+constexpr size_t kLdsPart = kLdsGj + kMaxR * 2 * kMaxR * 4;       // partial sums of the share groups [JS][4][ncw]
+constexpr size_t kLdsGf = kLdsPart + 4 * 1024;                    // exp[512] + log[256]
 constexpr size_t kLdsBody = kLdsGf + 768;                         // the request body (128 bytes)
 constexpr size_t kLdsBytes = kLdsBody + 128;
-static_assert(kLdsBytes <= 64 * 1024, "the worker fits the default 64 KiB workgroup LDS");
+static_assert(kLdsBytes <= 64 * 1024, "a worker workgroup fits the default 64 KiB of LDS");
 
-// Slot layout in pinned host memory (offsets in bytes).  The host writes [0, 8) and the body; the device
-// writes the completion / exit words (their own 128-byte line) and the output rows.
+// Slot layout in pinned host memory (offsets in bytes).  The host writes the doorbell, the body and the shares;
+// the device writes the completion / exit words (lines of their own), the output rows and the debug times.
 constexpr size_t kOffDoorbell = 0;
-constexpr size_t kOffDone = 128;    // u64: seq | status << 32
-constexpr size_t kOffExited = 136;  // u64: generation of a worker that has left its loop
-constexpr size_t kOffTrace = 144;   // u64: progress marker (KFEC_WORKER_DEBUG only): phase | seq << 8
 constexpr size_t kOffBody = 256;    // WorkerBody
-constexpr size_t kOffShares = 1024; // K rows x pitch: the shares, in row order
-constexpr size_t kSlotBytes = kOffShares + 2 * kStageMax;  // shares + output rows
+constexpr size_t kOffTrace = 512;   // u64: device-side phase times (KFEC_WORKER_DEBUG=2)
+constexpr size_t kOffDone = 1024;   // u64 per workgroup, 128 bytes apart: seq | status << 32
+constexpr size_t kOffExited = 2048; // u64 per workgroup, 128 bytes apart: generation of a workgroup that has left
+constexpr size_t kLineW = 128;      // (one line per workgroup: no two CUs write into one host cache line)
+constexpr size_t kOffShares = 4096; // K rows x pitch: the shares, in row order; then the output rows
+constexpr size_t kSlotBytes = kOffShares + 2 * kStageMax;
 
-enum : uint32_t { kOpEncode = 1, kOpDecode = 2, kOpStop = 3 };
-constexpr int kWorkerDead = -1000;  // post_and_wait: the worker did not answer (the device's workers are disabled)
+enum : uint32_t { kOpPing = 0, kOpEncode = 1, kOpDecode = 2, kOpStop = 3 };  // ping: answered at once
 constexpr uint32_t kSeqMask = (1u << 30) - 1;
+constexpr int kWorkerDead = -1000;  // post_and_wait: the worker did not answer (the device's workers are disabled)
 
 // doorbell: seq (30 bits) | op (2) | K - 1 (8) | N - 1 (8) | B (16)
 __host__ __device__ inline uint64_t db_pack(uint32_t seq, uint32_t op, uint32_t K, uint32_t N, uint32_t B)
@@ -82,7 +89,7 @@ struct WorkerBody {          // 128 bytes
     uint64_t mat_id;         // unique per built matrix: the LDS table cache key
     uint64_t miss[4];        // decode: bit j set <=> row j holds a parity share (data share j is missing)
     uint32_t m;              // decode: number of missing data shares (<= kMaxR)
-    uint32_t out_pitch;      // unused by the device; keeps the layout explicit
+    uint32_t reserved;
     uint8_t M[kMaxR];        // missing data ids, ascending (row t of the output)
     uint8_t P[kMaxR];        // the parity share id used for M[t] (fecpp.cpp:538-544)
     uint8_t pad[128 - 88];
@@ -96,192 +103,348 @@ __device__ __forceinline__ uint32_t wk_gmul(const uint8_t *e, const uint8_t *l, 
     return (a && b) ? e[l[a] + l[b]] : 0u;
 }
 
-__device__ __forceinline__ uint32_t wk_apply(uint32_t acc, const uint32_t *t, uint32_t x)
+// acc ^ c * x with c's perm tables at an 8-dword (32-byte aligned) LDS entry: two 16-byte LDS reads
+__device__ __forceinline__ uint32_t tab_mac(uint32_t acc, const uint32_t *ent, uint32_t s0, uint32_t s1, uint32_t s2)
 {
-    return perm_mac(acc, t, x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u);
+    const uint4 a = *reinterpret_cast<const uint4 *>(ent);
+    const uint32_t t[5] = {a.x, a.y, a.z, a.w, ent[4]};
+    return perm_mac(acc, t, s0, s1, s2);
+}
+
+// acc[q] ^= XOR_{j0 <= j < K} tab(j, rows[q]) * X[j][c] for q < RT (RT a compile-time row count: no per-row branches),
+// shares j with skip bit set contribute nothing (their dword is replaced by 0: c * 0 = 0, no branch).  Shares
+// are taken 4 at a time so their LDS reads (and the broadcast table reads) are issued together.
+template <int RT>
+__device__ __forceinline__ void rows_mac(uint32_t (&acc)[4], const uint32_t *X, int nc, int c, int j0, int K,
+                                         const uint32_t *tab, int R, const int (&rows)[4], const uint64_t (&skip)[4])
+{
+    auto skipped = [&](int j) -> bool { return (skip[j >> 6] >> (j & 63)) & 1ull; };
+    int j = j0;
+    for (; j + 4 <= K; j += 4) {
+        uint32_t x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = skipped(j + u) ? 0u : X[(j + u) * nc + c];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t s0 = x[u] & 0x07070707u, s1 = (x[u] >> 3) & 0x07070707u, s2 = (x[u] >> 6) & 0x03030303u;
+#pragma unroll
+            for (int q = 0; q < RT; ++q) acc[q] = tab_mac(acc[q], tab + ((j + u) * R + rows[q]) * 8, s0, s1, s2);
+        }
+    }
+    for (; j < K; ++j) {
+        const uint32_t x = skipped(j) ? 0u : X[j * nc + c];
+        const uint32_t s0 = x & 0x07070707u, s1 = (x >> 3) & 0x07070707u, s2 = (x >> 6) & 0x03030303u;
+#pragma unroll
+        for (int q = 0; q < RT; ++q) acc[q] = tab_mac(acc[q], tab + (j * R + rows[q]) * 8, s0, s1, s2);
+    }
+}
+
+template <typename F>
+__device__ __forceinline__ void by_rows(int n, F &&f)  // f(std::integral_constant-like RT) for the uniform row count n
+{
+    if (n >= 4) f(std::integral_constant<int, 4>());
+    else if (n == 3) f(std::integral_constant<int, 3>());
+    else if (n == 2) f(std::integral_constant<int, 2>());
+    else f(std::integral_constant<int, 1>());
+}
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t x)
+{
+    // (readfirstlane returns int: widen through uint32_t, or bit 31 -- op 2 -- sign-extends)
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
 }  // namespace
 
-__global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, uint32_t gen, uint32_t last_seq,
-                                                                uint64_t idle_ticks, int debug)
+__global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, uint64_t *relay, uint32_t gen,
+                                                                uint32_t last_seq, uint64_t idle_ticks, int debug)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint64_t s_db;
     __shared__ uint64_t s_mat;
     __shared__ int s_singular;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, w = blockIdx.x, W = gridDim.x;
     uint8_t *s_exp = smem + kLdsGf, *s_log = smem + kLdsGf + 512;
     for (int i = tid; i < 512; i += kWThreads) s_exp[i] = w_gf.exp[i];
     for (int i = tid; i < 256; i += kWThreads) s_log[i] = w_gf.log[i];
     if (tid == 0) s_mat = 0;  // matrix ids start at 1
     uint64_t *doorbell = reinterpret_cast<uint64_t *>(slot + kOffDoorbell);
-    uint64_t *done = reinterpret_cast<uint64_t *>(slot + kOffDone);
-    uint64_t *exited = reinterpret_cast<uint64_t *>(slot + kOffExited);
+    uint64_t *done = reinterpret_cast<uint64_t *>(slot + kOffDone + kLineW * w);
+    uint64_t *exited = reinterpret_cast<uint64_t *>(slot + kOffExited + kLineW * w);
+    uint64_t *trace = reinterpret_cast<uint64_t *>(slot + kOffTrace);
     const uint4 *h_body = reinterpret_cast<const uint4 *>(slot + kOffBody);
     const uint4 *h_rows = reinterpret_cast<const uint4 *>(slot + kOffShares);
     uint32_t last = last_seq;
-    uint64_t *trace = reinterpret_cast<uint64_t *>(slot + kOffTrace);
-    auto mark = [&](uint64_t phase) {  // (waits for the marker's own store: a later fault cannot drop it)
-        if (debug && (tid & 63) == 0) {  // one marker per wave: trace[2 + wave]
-            __hip_atomic_store(trace + (tid == 0 ? 0 : 2 + (tid >> 6)), phase | ((uint64_t)last << 8), __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            if (tid == 0)
-                __hip_atomic_store(trace + 2, phase | ((uint64_t)last << 8), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        }
-    };
-    mark(1);
 
     for (;;) {
-        // The whole of wave 0 polls (all lanes load the same word; the value is made wave-uniform), never one
-        // lane: a loop under `tid == 0` leaves lanes 1-63 of wave 0 free to run on to the next barrier while
-        // lane 0 spins, and the compiler's structurized loop then replays the previous request forever.
+        // Wave 0 polls -- the whole wave, the value made wave-uniform: a loop under `tid == 0` leaves lanes 1-63
+        // free to run on to the next barrier while lane 0 spins, and the compiler's structurized loop then
+        // replays the previous request forever.  Workgroup 0 alone polls the doorbell in host memory (several
+        // CUs reading one host line at once serialise in the root complex: ping 3.6 us at 1 poller, 12 us at 8)
+        // and relays each new doorbell through a device-memory word the other workgroups poll.  Rolling: 8 loads
+        // in flight ~0.1 us apart, each checked as it returns and reissued.
         if (tid < 64) {
+            uint64_t *src = w == 0 ? doorbell : relay;
             const uint64_t t0 = wall_clock64();
-            uint64_t v;
+            uint64_t v = 0;
+            constexpr int NP = 8;
+            uint64_t xs[NP];
+            auto poll = [&]() -> uint64_t {
+                return w == 0 ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                              : __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            };
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                xs[k] = poll();
+                __builtin_amdgcn_s_sleep(3);
+            }
+            bool hit = false;
             for (;;) {
-                const uint64_t x = __hip_atomic_load(doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                v = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
-                    (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
-                if (db_seq(v) != last) break;
-                if (wall_clock64() - t0 > idle_ticks) {
-                    v = 0;  // idle: leave (seq 0 is never posted)
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    const uint64_t u = uniform64(xs[k]);
+                    if (!hit && u != 0 && db_seq(u) != last) {  // (0: nothing relayed since the launch's memset)
+                        v = u;  // (the relay's quit value ~0 has seq kSeqMask, never posted, and makes v ~0)
+                        hit = true;
+                    }
+                    if (!hit) {
+                        xs[k] = poll();
+                        __builtin_amdgcn_s_sleep(3);
+                    }
+                }
+                if (hit) break;
+                if (w == 0 && wall_clock64() - t0 > idle_ticks) {  // idle: workgroup 0 decides, the others follow
+                    v = ~0ull;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(4);
             }
-            if (tid == 0) s_db = v;
+            if (w == 0 && W > 1) __hip_atomic_store(relay, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) s_db = v == ~0ull ? 0 : v;
         }
         __syncthreads();
         const uint64_t v = s_db;
         if (v == 0) break;
+        const uint64_t ts_seen = debug == 2 ? wall_clock64() : 0;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the stage and body written before the doorbell
         last = db_seq(v);
-        mark(2);
         const uint32_t op = db_op(v);
         uint32_t status = 0;
-        if (op == kOpStop) {
+        if (op == kOpStop || op == kOpPing) {
             if (tid == 0) __hip_atomic_store(done, (uint64_t)last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
+            if (op == kOpStop) break;
+            continue;
         }
         const int K = (int)((v >> 32) & 0xFF) + 1, N = (int)((v >> 40) & 0xFF) + 1, R = N - K;
         const int B = (int)(v >> 48);
-        const int pitch = (B + 15) & ~15, P4 = pitch >> 2;
-        // 1. one burst of 16-byte loads: the body and the K share rows (clamped indices keep r[] in VGPRs)
+        const int pitch = (B + 15) & ~15, G = pitch >> 4, P4 = pitch >> 2;
+        // a request outside the worker's shapes (the host never posts one) is answered, not executed
+        if (R < 1 || R > kMaxR || B < 1 || (size_t)(K + R) * pitch > kStageMax || (size_t)R * K * 32 > kTabMax) {
+            __syncthreads();
+            if (tid == 0)
+                __hip_atomic_store(done, (uint64_t)last | (3ull << 32), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            continue;
+        }
+        // this workgroup's granules [ga, ga + ng) of every row; nc dword columns
+        const int ga = (int)((int64_t)w * G / W), ng = (int)((int64_t)(w + 1) * G / W) - ga, nc = 4 * ng;
+        if ((size_t)K * ((G + W - 1) / W) * 16 > kSliceMax) {  // (the host checks the same bound)
+            __syncthreads();
+            if (tid == 0)
+                __hip_atomic_store(done, (uint64_t)last | (3ull << 32), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            continue;
+        }
+        // thread roles: JS groups of shares, each over ncw column lanes (so a workgroup slice of <= 64 columns
+        // keeps all 4 waves busy, each on a quarter of the shares; the groups' partial sums meet in LDS)
+        const int ncw = nc <= 64 ? 64 : (nc <= 128 ? 128 : kWThreads), JS = kWThreads / ncw;
+        const int jg = tid / ncw, cl = tid - jg * ncw;
+        uint32_t *s_part = reinterpret_cast<uint32_t *>(smem + kLdsPart);  // [JS][4][ncw]
+        // 1. one burst of 16-byte loads: the body and the K rows' slices (clamped indices keep r[] in VGPRs; the
+        //    clamped duplicates store the same bytes)
         {
-            const int n16 = K * (pitch >> 4);
+            const int n16 = K * ng;
             uint4 *s16 = reinterpret_cast<uint4 *>(smem + kLdsData);
             uint4 *b16 = reinterpret_cast<uint4 *>(smem + kLdsBody);
-            mark(10);
             const uint4 bq = h_body[tid & 7];
-            for (int i0 = 0; i0 < n16; i0 += kWThreads * 8) {
-                uint4 r[8];
+            for (int i0 = 0; i0 < n16; i0 += kWThreads * 4) {
+                uint4 r[4];
+                int dst[4];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) r[u] = h_rows[min(i0 + u * kWThreads + tid, n16 - 1)];
+                for (int u = 0; u < 4; ++u) {
+                    const int i = max(min(i0 + u * kWThreads + tid, n16 - 1), 0);
+                    const int j = i / max(ng, 1), g = i - j * max(ng, 1);
+                    dst[u] = i;
+                    r[u] = h_rows[j * G + ga + g];
+                }
 #pragma unroll
-                for (int u = 0; u < 8; ++u) s16[min(i0 + u * kWThreads + tid, n16 - 1)] = r[u];  // (same bytes)
+                for (int u = 0; u < 4; ++u) s16[dst[u]] = r[u];
             }
             if (tid < 8) b16[tid] = bq;
-            mark(11);
         }
         __syncthreads();
-        mark(3);
+        const uint64_t ts_loaded = debug == 2 ? wall_clock64() : 0;
+        const uint64_t ck_loaded = debug == 2 ? __builtin_amdgcn_s_memtime() : 0;
         const WorkerBody *body = reinterpret_cast<const WorkerBody *>(smem + kLdsBody);
         uint32_t *s_tab = reinterpret_cast<uint32_t *>(smem + kLdsTab);
-        const uint32_t *s_rows = reinterpret_cast<const uint32_t *>(smem + kLdsData);
-        // 2. parity-row perm tables of this matrix: s_tab[(j * R + r) * 5 + i], kept while the matrix is reused
-        if (debug && tid == 0)
-            __hip_atomic_store(trace + 1, (uint64_t)body->m | ((uint64_t)body->M[0] << 8) | ((uint64_t)body->P[0] << 16) |
-                                              ((uint64_t)K << 24) | ((uint64_t)R << 40) | ((uint64_t)(body->mat_id & 0xFF) << 56),
-                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint32_t *s_rows = reinterpret_cast<uint32_t *>(smem + kLdsData);  // [K][nc] dwords
+        // 2. parity-row perm tables of this matrix: s_tab[(j * R + r) * 8 + i], kept while the matrix is reused
         if (body->mat_id != s_mat) {
             const uint32_t *g_tab =
                 reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(body->enc) + enc_tab_offset(K, N));
             const int rows = (int)enc_tab_rows(R), n = K * R * 5;
             for (int i = tid; i < n; i += kWThreads) {
-                const int e = i / 5, w = i - e * 5, j = e / R, r = e - j * R;
-                s_tab[i] = g_tab[(j * rows + r) * 5 + w];
+                const int e = i / 5, q = i - e * 5, j = e / R, r = e - j * R;
+                s_tab[e * 8 + q] = g_tab[(j * rows + r) * 5 + q];
             }
             __syncthreads();
             if (tid == 0) s_mat = body->mat_id;
         }
-        uint32_t *out = reinterpret_cast<uint32_t *>(slot + kOffShares + (size_t)K * pitch);
+        uint32_t *out = reinterpret_cast<uint32_t *>(slot + kOffShares + (size_t)K * pitch) + ga * 4;
         if (op == kOpEncode) {
-            // items (r, c): parity row r, dword column c
-            for (int it = tid; it < R * P4; it += kWThreads) {
-                const int r = it / P4, c = it - r * P4;
-                uint32_t acc = 0;
-                for (int j = 0; j < K; ++j) acc = wk_apply(acc, s_tab + (j * R + r) * 5, s_rows[j * P4 + c]);
-                out[it] = acc;
+            // row tiles of 4 (uniform across the workgroup); thread = (share group, column)
+            const uint64_t none[4] = {0, 0, 0, 0};
+            const int jlo = jg * K / JS, jhi = (jg + 1) * K / JS;
+            for (int r0 = 0; r0 < R; r0 += 4) {
+                const int rows[4] = {r0, r0 + 1, r0 + 2, r0 + 3}, rt_n = min(4, R - r0);
+                by_rows(rt_n, [&](auto rt) {
+                    constexpr int RT = decltype(rt)::value;
+                    for (int c = cl; c < nc; c += ncw) {
+                        uint32_t acc[4] = {0, 0, 0, 0};
+                        rows_mac<RT>(acc, s_rows, nc, c, jlo, jhi, s_tab, R, rows, none);
+#pragma unroll
+                        for (int q = 0; q < RT; ++q) {
+                            if (JS == 1) out[(r0 + q) * P4 + c] = acc[q];
+                            else s_part[(jg * 4 + q) * ncw + c] = acc[q];
+                        }
+                    }
+                });
+                if (JS > 1) {
+                    __syncthreads();
+                    for (int e = tid; e < rt_n * nc; e += kWThreads) {
+                        const int q = e / nc, c = e - q * nc;
+                        uint32_t a = 0;
+                        for (int g = 0; g < JS; ++g) a ^= s_part[(g * 4 + q) * ncw + c];
+                        out[(r0 + q) * P4 + c] = a;
+                    }
+                    __syncthreads();
+                }
             }
         } else {
-            mark(5);
-            const int m = (int)body->m;
+            const int m = min((int)body->m, R);  // (the host sends 1 <= m <= R)
             uint32_t *s_gj = reinterpret_cast<uint32_t *>(smem + kLdsGj);
             uint32_t *s_cinv = reinterpret_cast<uint32_t *>(smem + kLdsCinv);
-            uint32_t *s_y = reinterpret_cast<uint32_t *>(smem + kLdsData);  // y_t overwrites row M_t in place
             // 3. [S | I], S[t][u] = enc[P_t][M_u] (byte 1 of table word 0 is c * 1 = c)
-            const int W = 2 * m;
-            if (tid < m * W) {
-                const int t = tid / W, u = tid - t * W;
-                s_gj[tid] = u < m ? (s_tab[((int)body->M[u] * R + ((int)body->P[t] - K)) * 5] >> 8) & 0xFFu
-                                  : (uint32_t)(u - m == t);
+            const int Wd = 2 * m, ne = m * Wd;  // ne <= 512: at most 2 entries per thread
+            for (int e = tid; e < ne; e += kWThreads) {
+                const int t = e / Wd, u = e - t * Wd;
+                s_gj[e] = u < m ? (s_tab[((int)body->M[u] * R + ((int)body->P[t] - K)) * 8] >> 8) & 0xFFu
+                                : (uint32_t)(u - m == t);
             }
             if (tid == 0) s_singular = 0;
             __syncthreads();
             // Gauss-Jordan without pivot search: every leading minor of a square submatrix of the parity part
             // of this systematic MDS generator is non-singular; a zero pivot is still detected and reported.
             for (int c = 0; c < m; ++c) {
-                uint32_t f = 0, pv = 0;
-                const bool mine = tid < m * W;
-                const int t = mine ? tid / W : 0, u = mine ? tid - t * W : 0;
-                if (mine) {
-                    const uint32_t piv = s_gj[c * W + c];
-                    if (piv == 0 && tid == 0) s_singular = 1;
-                    const uint32_t inv = piv ? s_exp[255 - s_log[piv]] : 0u;
-                    f = s_gj[t * W + c];
-                    pv = wk_gmul(s_exp, s_log, s_gj[c * W + u], inv);
+                uint32_t f[2] = {0, 0}, pv[2] = {0, 0};
+                const uint32_t piv = s_gj[c * Wd + c];
+                if (piv == 0 && tid == 0) s_singular = 1;
+                const uint32_t inv = piv ? s_exp[255 - s_log[piv]] : 0u;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int e = tid + k * kWThreads;
+                    if (e < ne) {
+                        const int t = e / Wd, u = e - t * Wd;
+                        f[k] = s_gj[t * Wd + c];
+                        pv[k] = wk_gmul(s_exp, s_log, s_gj[c * Wd + u], inv);
+                    }
                 }
                 __syncthreads();
-                if (mine) s_gj[tid] = (t == c) ? pv : (s_gj[tid] ^ wk_gmul(s_exp, s_log, f, pv));
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int e = tid + k * kWThreads;
+                    if (e < ne) s_gj[e] = (e / Wd == c) ? pv[k] : (s_gj[e] ^ wk_gmul(s_exp, s_log, f[k], pv[k]));
+                }
                 __syncthreads();
             }
-            mark(6);
             if (tid < m * m) {
                 const int uu = tid / m, t = tid - uu * m;
                 uint32_t tb[5];
-                gf_perm_tables(s_gj[uu * W + m + t], tb);
+                gf_perm_tables(s_gj[uu * Wd + m + t], tb);
 #pragma unroll
-                for (int i = 0; i < 5; ++i) s_cinv[tid * 5 + i] = tb[i];
+                for (int i = 0; i < 5; ++i) s_cinv[tid * 8 + i] = tb[i];
             }
-            // 4. syndromes of the used parity shares over the present data rows
-            const uint64_t miss0 = body->miss[0], miss1 = body->miss[1], miss2 = body->miss[2], miss3 = body->miss[3];
-            for (int it = tid; it < m * P4; it += kWThreads) {
-                const int t = it / P4, c = it - t * P4, pr = (int)body->P[t] - K;
-                uint32_t y = s_rows[(int)body->M[t] * P4 + c];
-                for (int j = 0; j < K; ++j) {
-                    const uint64_t mw = j < 64 ? miss0 : j < 128 ? miss1 : j < 192 ? miss2 : miss3;
-                    if ((mw >> (j & 63)) & 1ull) continue;
-                    y = wk_apply(y, s_tab + (j * R + pr) * 5, s_rows[j * P4 + c]);
+            // 4. syndromes of the used parity shares over the present data rows, 4 at a time (uniform tiles), each
+            //    share group's partial sums meeting in LDS; y_t overwrites row M_t in place
+            const uint64_t miss[4] = {body->miss[0], body->miss[1], body->miss[2], body->miss[3]};
+            const int jlo = jg * K / JS, jhi = (jg + 1) * K / JS;
+            for (int t0 = 0; t0 < m; t0 += 4) {
+                int pr[4], mr[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int t = min(t0 + q, m - 1);
+                    pr[q] = (int)body->P[t] - K;
+                    mr[q] = (int)body->M[t];
                 }
-                s_y[(int)body->M[t] * P4 + c] = y;  // row M_t is read by item (t, c) only
+                const int rt_n = min(4, m - t0);
+                by_rows(rt_n, [&](auto rt) {
+                    constexpr int RT = decltype(rt)::value;
+                    for (int c = cl; c < nc; c += ncw) {
+                        uint32_t y[4] = {0, 0, 0, 0};
+                        if (JS == 1) {
+#pragma unroll
+                            for (int q = 0; q < RT; ++q) y[q] = s_rows[mr[q] * nc + c];
+                        }
+                        rows_mac<RT>(y, s_rows, nc, c, jlo, jhi, s_tab, R, pr, miss);
+#pragma unroll
+                        for (int q = 0; q < RT; ++q) {
+                            if (JS == 1) s_rows[mr[q] * nc + c] = y[q];
+                            else s_part[(jg * 4 + q) * ncw + c] = y[q];
+                        }
+                    }
+                });
+                if (JS > 1) {
+                    __syncthreads();
+                    for (int e = tid; e < rt_n * nc; e += kWThreads) {
+                        const int q = e / nc, c = e - q * nc;
+                        uint32_t a = s_rows[mr[q] * nc + c];
+                        for (int g = 0; g < JS; ++g) a ^= s_part[(g * 4 + q) * ncw + c];
+                        s_rows[mr[q] * nc + c] = a;
+                    }
+                    __syncthreads();
+                }
             }
             __syncthreads();
-            mark(7);
-            // 5. out_u = XOR_t Sinv[u][t] * y_t
-            for (int it = tid; it < m * P4; it += kWThreads) {
-                const int uu = it / P4, c = it - uu * P4;
-                uint32_t o = 0;
-                for (int t = 0; t < m; ++t) o = wk_apply(o, s_cinv + (uu * m + t) * 5, s_y[(int)body->M[t] * P4 + c]);
-                out[it] = o;
+            // 5. out_u = XOR_t Sinv[u][t] * y_t, 4 output rows at a time: the same MAC over the m y rows (gathered
+            //    through a row map) with the m x m tables of Sinv
+            for (int u0 = 0; u0 < m; u0 += 4) {
+                by_rows(m - u0, [&](auto rt) {
+                    constexpr int RT = decltype(rt)::value;
+                    for (int c = tid; c < nc; c += kWThreads) {
+                        uint32_t o[4] = {0, 0, 0, 0};
+                        for (int t = 0; t < m; ++t) {
+                            const uint32_t x = s_rows[(int)body->M[t] * nc + c];
+                            const uint32_t s0 = x & 0x07070707u, s1 = (x >> 3) & 0x07070707u, s2 = (x >> 6) & 0x03030303u;
+#pragma unroll
+                            for (int q = 0; q < RT; ++q) o[q] = tab_mac(o[q], s_cinv + ((u0 + q) * m + t) * 8, s0, s1, s2);
+                        }
+#pragma unroll
+                        for (int q = 0; q < RT; ++q) out[(u0 + q) * P4 + c] = o[q];
+                    }
+                });
             }
             status = (uint32_t)s_singular;
         }
-        mark(4);
+        const uint64_t ts_comp = debug == 2 ? wall_clock64() : 0;
+        const uint64_t ck_comp = debug == 2 ? __builtin_amdgcn_s_memtime() : 0;
         // 6. publish: every thread's output stores complete at system scope before the completion word
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
+        if (debug == 2 && tid == 0 && w == 0) {  // device-side phase times of this request (100 MHz ticks)
+            const uint64_t ts_pub = wall_clock64();
+            __hip_atomic_store(trace + 0, ts_loaded - ts_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 1, ts_comp - ts_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 2, ts_pub - ts_comp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 3, ck_comp - ck_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         if (tid == 0)
             __hip_atomic_store(done, (uint64_t)last | ((uint64_t)status << 32), __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_SYSTEM);
@@ -297,6 +460,7 @@ namespace {
 struct Slot {
     std::mutex mu;
     uint8_t *h = nullptr;        // kSlotBytes of fine-grained pinned host memory
+    uint64_t *d_relay = nullptr; // device-memory doorbell relay from workgroup 0 (zeroed before every launch)
     hipStream_t stream = nullptr;
     uint32_t seq = 0;            // last posted sequence number (0 = none yet)
     uint32_t gen = 0;            // generation of the last launched worker
@@ -328,6 +492,19 @@ int env_mode()
 bool env_enabled() { return env_mode() != 0; }
 std::atomic<uint64_t> g_served{0};
 
+int env_int(const char *name, int def, int lo, int hi)
+{
+    const char *e = getenv(name);
+    int v = e ? atoi(e) : def;
+    return v < lo ? lo : (v > hi ? hi : v);
+}
+
+int n_wgs()
+{
+    static const int n = env_int("KFEC_WORKER_WGS", kMaxW, 1, kMaxW);
+    return n;
+}
+
 // the worker of this device did not answer: required -> error; otherwise warn once and use the launch path
 int worker_dead(DevWorkers &d)
 {
@@ -340,15 +517,17 @@ int worker_dead(DevWorkers &d)
 
 uint64_t idle_ticks()
 {
-    static const uint64_t t = [] {
-        const char *e = getenv("KFEC_WORKER_IDLE_US");
-        long us = e ? atol(e) : 20000;
-        if (us < 100) us = 100;
-        if (us > 10000000) us = 10000000;
-        return (uint64_t)us * 100;  // wall_clock64 runs at 100 MHz on gfx950
-    }();
+    static const uint64_t t = (uint64_t)env_int("KFEC_WORKER_IDLE_US", 20000, 100, 10000000) * 100;  // 100 MHz clock
     return t;
 }
+
+// KFEC_WORKER_DEBUG=2: device-side phase times of workgroup 0, summed and printed when the workers stop
+int debug_level()
+{
+    static const int d = env_int("KFEC_WORKER_DEBUG", 0, 0, 2);
+    return d;
+}
+std::atomic<uint64_t> g_dbg_n{0}, g_dbg_load{0}, g_dbg_comp{0}, g_dbg_pub{0}, g_dbg_clk{0};
 
 inline uint64_t load_acq(const uint8_t *p) { return __atomic_load_n(reinterpret_cast<const uint64_t *>(p), __ATOMIC_ACQUIRE); }
 
@@ -359,19 +538,23 @@ DevWorkers *get_dev(int dev)
     std::lock_guard<std::mutex> lk(d.init_mu);
     if (d.init) return d.failed ? nullptr : &d;
     d.init = true;
-    const char *e = getenv("KFEC_WORKER_SLOTS");
-    int n = e ? atoi(e) : 2;
-    n = n < 1 ? 1 : (n > kMaxSlots ? kMaxSlots : n);
+    const int n = env_int("KFEC_WORKER_SLOTS", 2, 1, kMaxSlots);
     for (int i = 0; i < n; ++i) {
         Slot &s = d.slots[i];
-        void *p = nullptr;
+        void *p = nullptr, *q = nullptr;
         if (hipHostMalloc(&p, kSlotBytes, hipHostMallocCoherent) != hipSuccess) break;
-        std::memset(p, 0, kOffShares);
-        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) {
+        if (hipMalloc(&q, 256) != hipSuccess) {
             (void)hipHostFree(p);
             break;
         }
+        std::memset(p, 0, kOffShares);
+        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipHostFree(p);
+            (void)hipFree(q);
+            break;
+        }
         s.h = static_cast<uint8_t *>(p);
+        s.d_relay = static_cast<uint64_t *>(q);
         d.nslots = i + 1;
     }
     if (d.nslots == 0) d.failed = true;
@@ -393,11 +576,16 @@ Slot &acquire(DevWorkers &d, std::unique_lock<std::mutex> &lk)
     return s;
 }
 
+// workgroup 0 has left (idle) -- the others leave with it
+bool leader_exited(const Slot &s) { return (uint32_t)load_acq(s.h + kOffExited) == s.gen; }
+
 int launch_worker(Slot &s)
 {
     s.gen += 1;
-    hipLaunchKernelGGL(kfec_worker_kernel, dim3(1), dim3(kWThreads), kLdsBytes, s.stream, s.h, s.gen, s.seq - 1,
-                       idle_ticks(), getenv("KFEC_WORKER_DEBUG") ? 1 : 0);
+    // the relay word is cleared in stream order: after the previous worker's last workgroup, before this one
+    if (hipMemsetAsync(s.d_relay, 0, 256, s.stream) != hipSuccess) return KFEC_EHIP;
+    hipLaunchKernelGGL(kfec_worker_kernel, dim3(n_wgs()), dim3(kWThreads), kLdsBytes, s.stream, s.h, s.d_relay, s.gen,
+                       s.seq - 1, idle_ticks(), debug_level());
     if (hipGetLastError() != hipSuccess) {
         s.running = false;
         return KFEC_EHIP;
@@ -406,41 +594,59 @@ int launch_worker(Slot &s)
     return 0;
 }
 
-// post the doorbell and wait for its completion word; returns the status (0 / 1 singular) or a KFEC_E* code
+// the combined completion of `seq`: -1 while some workgroup has not finished it, else the largest status
+int completion(const Slot &s, uint32_t seq, int W)
+{
+    uint32_t st = 0;
+    for (int w = 0; w < W; ++w) {
+        const uint64_t d = load_acq(s.h + kOffDone + kLineW * w);
+        if (db_seq(d) != seq) return -1;
+        st = st > (uint32_t)(d >> 32) ? st : (uint32_t)(d >> 32);
+    }
+    return (int)st;
+}
+
+// post the doorbell and wait for every workgroup's completion word; returns the status (0, 1 singular,
+// 3 refused) or a KFEC_E* code
 int post_and_wait(Slot &s, uint32_t op, int K, int N, int B)
 {
+    const int W = n_wgs();
     uint32_t seq = (s.seq + 1) & kSeqMask;
-    if (seq == 0) seq = 1;
+    if (seq == 0 || seq == kSeqMask) seq = 1;  // (kSeqMask: the seq of the relay's quit value)
     s.seq = seq;
     __atomic_store_n(reinterpret_cast<uint64_t *>(s.h + kOffDoorbell), db_pack(seq, op, (uint32_t)K, (uint32_t)N, (uint32_t)B),
                      __ATOMIC_SEQ_CST);
-    if (!s.running || (uint32_t)load_acq(s.h + kOffExited) == s.gen) {
+    if (!s.running || leader_exited(s)) {
         const int rc = launch_worker(s);
         if (rc) return rc;
     }
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t it = 1;; ++it) {
-        const uint64_t d = load_acq(s.h + kOffDone);
-        if (db_seq(d) == seq) return (int)(d >> 32);
+        const int st = completion(s, seq, W);
+        if (st >= 0) {
+            if (debug_level() == 2) {
+                g_dbg_n += 1;
+                g_dbg_load += load_acq(s.h + kOffTrace);
+                g_dbg_comp += load_acq(s.h + kOffTrace + 8);
+                g_dbg_pub += load_acq(s.h + kOffTrace + 16);
+                g_dbg_clk += load_acq(s.h + kOffTrace + 24);
+            }
+            return st;
+        }
         if ((it & 255) == 0) {
-            if ((uint32_t)load_acq(s.h + kOffExited) == s.gen) {
-                // the worker left its loop (idle timeout) before it saw this doorbell: launch a new one, which
-                // starts behind the old one on the slot's stream and finds the doorbell pending
-                if (db_seq(load_acq(s.h + kOffDone)) == seq) continue;
+            if (leader_exited(s)) {
+                // the worker left its loop (idle timeout) before all of it saw this doorbell: launch a new one,
+                // which starts behind the old one on the slot's stream and finds the doorbell pending (a slice
+                // the old one already wrote is rewritten with the same bytes)
+                if (completion(s, seq, W) >= 0) continue;
                 const int rc = launch_worker(s);
                 if (rc) return rc;
             }
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-                // no answer: report the slot's state and let the caller take the launch path from now on
-                if (getenv("KFEC_WORKER_DEBUG"))
-                {
-                fprintf(stderr, "kfec worker: no answer; doorbell %llx done %llx exited %llx trace %llx %llx gen %u stream %d\n",
+                if (debug_level())
+                    fprintf(stderr, "kfec worker: no answer; doorbell %llx done[0] %llx exited[0] %llx gen %u stream %d\n",
                             (unsigned long long)load_acq(s.h + kOffDoorbell), (unsigned long long)load_acq(s.h + kOffDone),
-                            (unsigned long long)load_acq(s.h + kOffExited), (unsigned long long)load_acq(s.h + kOffTrace),
-                            (unsigned long long)load_acq(s.h + kOffTrace + 8), s.gen, (int)hipStreamQuery(s.stream));
-                for (int w = 0; w < kWThreads / 64; ++w)
-                    fprintf(stderr, "  wave %d: %llx\n", w, (unsigned long long)load_acq(s.h + kOffTrace + 16 + 8 * w));
-            }
+                            (unsigned long long)load_acq(s.h + kOffExited), s.gen, (int)hipStreamQuery(s.stream));
                 s.running = false;
                 return kWorkerDead;
             }
@@ -451,10 +657,10 @@ int post_and_wait(Slot &s, uint32_t op, int K, int N, int B)
 
 bool shape_ok(int K, int N, size_t B, int mrows)
 {
-    const int R = N - K;
-    const size_t pitch = (B + 15) & ~size_t(15);
+    const int R = N - K, W = n_wgs();
+    const size_t pitch = (B + 15) & ~size_t(15), G = pitch / 16;
     return B > 0 && B <= 0xFFFF && R >= 1 && R <= kMaxR && mrows <= kMaxR && (size_t)(K + R) * pitch <= kStageMax &&
-           (size_t)R * K * 20 <= kTabMax;
+           (size_t)R * K * 32 <= kTabMax && (size_t)K * ((G + W - 1) / W) * 16 <= kSliceMax;
 }
 
 }  // namespace
@@ -483,6 +689,7 @@ int worker_encode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int 
     const int st = post_and_wait(s, kOpEncode, K, N, (int)B);
     if (st == kWorkerDead) return worker_dead(*d);
     if (st < 0) return st;
+    if (st) return KFEC_EHIP;  // the worker refused the request's shape
     g_served.fetch_add(1, std::memory_order_relaxed);
     const uint8_t *out = rows + (size_t)K * pitch;
     if (pitch == B) {
@@ -517,6 +724,7 @@ int worker_decode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int 
     const int st = post_and_wait(s, kOpDecode, K, N, (int)B);
     if (st == kWorkerDead) return worker_dead(*d);
     if (st < 0) return st;
+    if (st == 3) return KFEC_EHIP;  // the worker refused the request's shape
     g_served.fetch_add(1, std::memory_order_relaxed);
     if (st) return KFEC_ESINGULAR;
     const uint8_t *o = rows + (size_t)K * pitch;
@@ -528,32 +736,55 @@ int worker_decode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int 
     return 0;
 }
 
+// One empty request (answered by every workgroup at once): the communication floor of the per-call path
+int worker_ping(int device)
+{
+    if (!env_enabled()) return 1;
+    DevWorkers *d = get_dev(device);
+    if (!d) return env_mode() == 2 ? KFEC_EHIP : 1;
+    std::unique_lock<std::mutex> lk;
+    Slot &s = acquire(*d, lk);
+    const int st = post_and_wait(s, kOpPing, 1, 2, 1);
+    if (st == kWorkerDead) return worker_dead(*d);
+    return st < 0 ? st : 0;
+}
+
 // Stop the resident workers of a device (no coder left on it): post STOP to every running slot and wait for
 // the kernel to finish.  Bounded: a worker that does not answer within 2 s is left to its idle timeout.
 void worker_stop(int device)
 {
     if (device < 0 || device >= 64) return;
+    if (debug_level() == 2 && g_dbg_n.load())
+        fprintf(stderr, "kfec worker: %llu requests, device us per request (workgroup 0): loads %.2f compute %.2f publish %.2f; "
+                        "shader clock during compute %.0f MHz\n",
+                (unsigned long long)g_dbg_n.load(), g_dbg_load.load() / 100.0 / g_dbg_n.load(),
+                g_dbg_comp.load() / 100.0 / g_dbg_n.load(), g_dbg_pub.load() / 100.0 / g_dbg_n.load(),
+                g_dbg_comp.load() ? 100.0 * g_dbg_clk.load() / g_dbg_comp.load() : 0.0);
     DevWorkers &d = g_dev[device];
     {
         std::lock_guard<std::mutex> lk(d.init_mu);
         if (!d.init || d.failed) return;
     }
+    const int W = n_wgs();
     for (int i = 0; i < d.nslots; ++i) {
         Slot &s = d.slots[i];
         std::lock_guard<std::mutex> lk(s.mu);
         if (!s.running) continue;
-        if ((uint32_t)load_acq(s.h + kOffExited) != s.gen) {
+        auto all_exited = [&] {
+            for (int w = 0; w < W; ++w)
+                if ((uint32_t)load_acq(s.h + kOffExited + kLineW * w) != s.gen) return false;
+            return true;
+        };
+        if (!all_exited()) {
             uint32_t seq = (s.seq + 1) & kSeqMask;
-            if (seq == 0) seq = 1;
+            if (seq == 0 || seq == kSeqMask) seq = 1;  // (kSeqMask: the seq of the relay's quit value)
             s.seq = seq;
             __atomic_store_n(reinterpret_cast<uint64_t *>(s.h + kOffDoorbell), db_pack(seq, kOpStop, 1, 1, 0),
                              __ATOMIC_SEQ_CST);
             const auto t0 = std::chrono::steady_clock::now();
-            while ((uint32_t)load_acq(s.h + kOffExited) != s.gen &&
-                   std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2))
-                __builtin_ia32_pause();
+            while (!all_exited() && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) __builtin_ia32_pause();
         }
-        if ((uint32_t)load_acq(s.h + kOffExited) == s.gen) (void)hipStreamSynchronize(s.stream);
+        if (all_exited()) (void)hipStreamSynchronize(s.stream);
         s.running = false;
     }
 }

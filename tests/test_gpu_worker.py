@@ -1,8 +1,8 @@
 """The resident per-call worker (kcptube_amd/csrc/kfec_worker.hip): kfec_encode / kfec_decode on one group
 from host memory without a launch per call, against the oracle (fecpp.cpp:495-513, 518-587).
 
-Covers the shapes at the worker's limits (R <= 16 parity / missing rows, (K + R) * pitch <= 38 KiB,
-R * K * 20 <= 16 KiB) and just past them (the launch path takes those), inconsistent shares, block sizes
+Covers the shapes at the worker's limits (R <= 16 parity / missing rows, (K + R) * pitch <= 36 KiB,
+R * K <= 512) and just past them (the launch path takes those), inconsistent shares, block sizes
 that are not multiples of 16, concurrent callers on more coders than slots, the idle exit and relaunch,
 and that the worker and the launch path (KFEC_WORKER=0) give the same bytes.
 """
@@ -56,10 +56,10 @@ def _roundtrip(c, oracle, K, N, B, rng, n_lost=None, corrupt=False):
 @pytest.mark.parametrize("K,N,B", [
     (1, 2, 1), (2, 3, 15), (20, 23, 1440), (10, 13, 1400), (20, 23, 1442), (5, 6, 17),
     (8, 24, 1440),     # R = 16, (K + R) * 1440 = 33.75 KiB: at the row limit
-    (50, 66, 128),     # R * K * 20 = 16 000 bytes of tables, 16 missing
+    (32, 48, 128),     # R * K = 512: at the table limit, 16 missing
     (8, 25, 1440),     # R = 17: past the row limit (launch path)
-    (26, 29, 1440),    # (K + R) * pitch > 38 KiB (launch path)
-    (60, 74, 16),      # R * K * 20 > 16 KiB (launch path)
+    (26, 29, 1440),    # (K + R) * pitch > 36 KiB (launch path)
+    (33, 49, 16),      # R * K > 512 (launch path)
 ])
 def test_worker_shapes_vs_oracle(dev, oracle, K, N, B):
     from kcptube_amd import FecCode
@@ -68,14 +68,15 @@ def test_worker_shapes_vs_oracle(dev, oracle, K, N, B):
     c = FecCode(K, N)
     R = N - K
     n0 = worker_requests()
-    for m in sorted({0, 1, min(R, K)}):
-        _roundtrip(c, oracle, K, N, B, rng, n_lost=m)
-    _roundtrip(c, oracle, K, N, B, rng, n_lost=min(R, K), corrupt=True)
+    losses = sorted({0, 1, min(R, K)}) + [min(R, K)]
+    for i, m in enumerate(losses):
+        _roundtrip(c, oracle, K, N, B, rng, n_lost=m, corrupt=i == len(losses) - 1)
     pitch = (B + 15) // 16 * 16
-    takes = R <= 16 and N * pitch <= 38 * 1024 and R * K * 20 <= 16 * 1024
+    W = int(os.environ.get("KFEC_WORKER_WGS", "8"))
+    takes = R <= 16 and N * pitch <= 36 * 1024 and R * K <= 512 and K * (-(-(pitch // 16) // W)) * 16 <= 16 * 1024
     served = worker_requests() - n0
-    if takes:  # 4 encodes + the decodes that had a data shard missing
-        assert served >= 4 + (2 if min(R, K) > 0 else 0), served
+    if takes:  # every encode, and every decode that had a data shard to recover
+        assert served == len(losses) + sum(1 for m in losses if m > 0), served
     else:
         assert served == 0, served
 

@@ -3,7 +3,8 @@
 # and the small-K persistent syndrome decode A/B (ss0 = syn_kernel + per-item expand loads, ss1 = syn_small_kernel + batched expand) at 10:3 random and 200:55.
 set -o pipefail
 out=gpurun_out/r3a; mkdir -p $out
-KFEC_WORKER_DEBUG=1 timeout -k 10 90 ./tools/latency_bench > $out/latency.json 2>&1 || { cat $out/latency.json; exit 1; }
+for q in d de eed; do timeout -k 5 20 ./tools/worker_check 20 23 1440 3 $q || exit 1; done
+timeout -k 10 90 ./tools/latency_bench > $out/latency.json 2>&1 || { cat $out/latency.json; exit 1; }
 cat $out/latency.json
 KFEC_WORKER=0 timeout -k 10 90 ./tools/latency_bench > $out/latency_launch.json 2>&1 || { cat $out/latency_launch.json; exit 1; }
 cat $out/latency_launch.json

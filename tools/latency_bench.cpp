@@ -31,6 +31,12 @@ int main()
     std::string js = "{\"metric\": \"latency path, fec=20:3 B=1440, one host thread (us per call)\"";
     // single group, host memory in and out
     const int reps = 2000;
+    if (kfec_worker_ping(ctx) == 0) {  // the resident worker's communication floor (an empty request)
+        for (int i = 0; i < 50; ++i) kfec_worker_ping(ctx);
+        auto tp = clk::now();
+        for (int i = 0; i < reps; ++i) kfec_worker_ping(ctx);
+        js += ", \"worker_ping_us\": " + std::to_string(us_since(tp) / reps);
+    }
     for (int i = 0; i < 50; ++i)
         if (int rc = kfec_encode(ctx, data.data(), K * B, B, par.data())) { printf("kfec_encode rc %d\n", rc); return 2; }
     auto t0 = clk::now();
