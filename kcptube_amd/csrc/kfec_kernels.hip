@@ -45,6 +45,9 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #ifndef KFEC_SYN_MAX_R
 #define KFEC_SYN_MAX_R 8  // decode in syndrome form up to this R (0: coefficient form always; A/B builds)
 #endif
+#ifndef KFEC_SYN_SMALLK_PD
+#define KFEC_SYN_SMALLK_PD 0  // > 0: granules in flight per lane of the syndrome decode for K <= 12 (A/B knob)
+#endif
 #ifndef KFEC_SYN_MINW
 #define KFEC_SYN_MINW 1  // __launch_bounds__ minimum waves per SIMD of the syndrome-form decode kernel
 #endif
@@ -1250,127 +1253,6 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
 #endif
 }
 
-// ---- small K (fec=10:3 and the like): the dense syndrome decode as a persistent loop --------------------
-// With K <= 12 a lane of syn_kernel has only ~K + m granules to move, so its two dependent memory latencies
-// (the group's record, then the shares the record selects) and the PD-deep load pipeline's fill and drain are
-// most of its life (10:3: VALU busy 0.48 of the time, SQ_WAIT_INST_ANY 1.7x the VALU instructions).  Here a
-// workgroup stays resident and walks the items with a grid stride; each lane
-//   * issues ALL of its group's loads at once (the used parity rows and up to KM data granules),
-//   * prefetches the NEXT item's record header and the byte of C its wave's table build needs before it
-//     waits for the current shares, so the record latency is off the critical path,
-// and the per-wave C tables are rebuilt per iteration from the prefetched bytes (no workgroup barrier).
-// Items, resources, tables and the final mix are exactly syn_kernel's, so the bytes are identical.
-template <int RT, int KM>
-__global__ void __launch_bounds__(kMacBlock) syn_small_kernel(SynArgs a)
-{
-    constexpr int W = Gran<32>::W;
-    constexpr int TD = SynLayout<RT>::TD;
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_ct[];  // [wave][group slot][RT][TD]
-    if (a.list_count && syn_listed(a, *a.list_count)) return;  // the listed kernel has it (whole workgroup)
-    const uint32_t cols = a.cols, K = a.K, total = a.total, pitch = (uint32_t)a.pitch;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t stride = gridDim.x * kMacBlock;
-    const uint32_t nslot = syn_wave_groups(cols);
-    uint32_t *ctw = s_ct + wv * nslot * RT * TD;
-    // this lane's record header / C byte for the items of the iteration whose workgroup base is `base`
-    auto header = [&](uint32_t base) -> uint4 {
-        const uint32_t item = base + threadIdx.x;
-        if (item >= total) return make_uint4(0xFFu, 0, 0, 0);  // status != 0: nothing to do
-        return *reinterpret_cast<const uint4 *>(a.rec + (uint64_t)(item / cols) * a.rec_stride);
-    };
-    auto cbyte = [&](uint32_t base) -> uint32_t {
-        const uint32_t wb = min(base + (threadIdx.x & ~63u), total - 1);
-        const uint32_t wfirst = wb / cols, wlast = min(wb + 63, total - 1) / cols;
-        const uint32_t gs = lane / (RT * RT), ur = lane - gs * (RT * RT);
-        if (base >= total || gs > wlast - wfirst) return 0u;
-        const uint8_t *rec = a.rec + (uint64_t)(wfirst + gs) * a.rec_stride;
-        const uint32_t u = ur / RT, r = ur - u * RT;
-        return rec[0] == 0 ? rec[40 + 8 * u + r] : 0u;
-    };
-    typedef const __attribute__((address_space(4))) uint32_t cu32;  // uniform: scalar loads into SGPRs
-    uint32_t base = blockIdx.x * kMacBlock;
-    uint4 h = header(base);
-    uint32_t cb = cbyte(base);
-    for (; base < total; base += stride) {
-        const uint4 hn = header(base + stride);  // prefetch: in flight while this item's shares load
-        const uint32_t cbn = cbyte(base + stride);
-        const uint32_t item = base + threadIdx.x;
-        const bool in = item < total;
-        const uint32_t g = in ? item / cols : 0u;
-        const uint32_t col = in ? item - g * cols : 0u;
-        const uint32_t off = gran_off<32>(col, a.B);
-        const uint32_t gfirst = base / cols;
-        const uint32_t m = (h.x & 0xFFu) == 0 ? (h.x >> 8) & 0xFFu : 0u;
-        const uint32_t used = (h.x >> 16) & 0xFFu;
-        const uint64_t p0 = (uint64_t)h.z | ((uint64_t)h.w << 32);
-        // this wave's C tables (lanes < groups * RT * RT), from the bytes prefetched last iteration
-        {
-            const uint32_t wb = min(base + (threadIdx.x & ~63u), total - 1);
-            const uint32_t ng = min(wb + 63, total - 1) / cols - wb / cols + 1;
-            if (lane < ng * RT * RT) {
-                const uint32_t gs = lane / (RT * RT), ur = lane - gs * (RT * RT), u = ur / RT, r = ur - u * RT;
-                uint32_t t[5];
-                gf_perm_tables(cb, t);
-#pragma unroll
-                for (int i = 0; i < 5; ++i) ctw[gs * RT * TD + u * TD + 5 * r + i] = t[i];
-            }
-        }
-        uint32_t acc[RT][W];
-        if (m > 0) {
-            const uint32_t ngr = min(base + kMacBlock - 1, total - 1) / cols - gfirst + 1;
-            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(a.data + (uint64_t)gfirst * K * a.pitch), (short)0, (int)(ngr * K * pitch), 0x00020000);
-            const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(a.parity + (uint64_t)gfirst * a.R * a.pitch), (short)0, (int)(ngr * a.R * pitch), 0x00020000);
-            const uint32_t gs = g - gfirst;
-            const uint32_t drow = gs * K * pitch + off, prow = gs * a.R * pitch + off;
-#pragma unroll
-            for (int r = 0; r < RT; ++r) {
-                const Gran<32> y = bload<32>(rp, ((used >> r) & 1u) ? prow + r * pitch : kAbsent);
-#pragma unroll
-                for (int w = 0; w < W; ++w) acc[r][w] = y.d[w];
-            }
-            Gran<32> x[KM];
-#pragma unroll
-            for (int j = 0; j < KM; ++j)
-                x[j] = bload<32>(rd, ((uint32_t)j < K && ((p0 >> j) & 1ull)) ? drow + j * pitch : kAbsent);
-#pragma unroll
-            for (int j = 0; j < KM; ++j) {
-                if ((uint32_t)j < K) {
-                    const cu32 *tg = (const cu32 *)(a.etab + (size_t)j * a.etab_rows * 5);
-                    uint32_t t[5 * RT];
-#pragma unroll
-                    for (int i = 0; i < 5 * RT; ++i) t[i] = tg[i];
-#pragma unroll
-                    for (int w = 0; w < W; ++w) {
-                        const uint32_t xv = x[j].d[w];
-                        const uint32_t s0 = xv & 0x07070707u, s1 = (xv >> 3) & 0x07070707u, s2 = (xv >> 6) & 0x03030303u;
-#pragma unroll
-                        for (int r = 0; r < RT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
-                    }
-                }
-            }
-        }
-        // the tables were written by lanes of this wave (in-order LDS); the fence keeps the compiler from
-        // moving the reads above the writes
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (m > 0) {
-            const uint32_t wfirst = min(base + (threadIdx.x & ~63u), total - 1) / cols;
-            syn_final<32, RT>(a, acc, ctw + (g - wfirst) * RT * TD, m, g, off, col);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the next iteration rewrites the tables
-        h = hn;
-        cb = cbn;
-    }
-}
-
-#ifndef KFEC_SYN_SMALL
-#define KFEC_SYN_SMALL 1  // 0: small K takes syn_kernel like every other shape (A/B knob)
-#endif
-#ifndef KFEC_SYN_SMALL_WGS
-#define KFEC_SYN_SMALL_WGS 0  // resident workgroups per CU of syn_small_kernel (0: the occupancy API's answer)
-#endif
-
 // ---- ordered list of the groups with data to recover (out_idx[g * R] != 0xFF), for syn_kernel's listed
 // shape: per-chunk counts, one exclusive scan, a scatter that keeps group order.  kActChunk groups per
 // 256-thread workgroup, 4 per thread.
@@ -1561,44 +1443,8 @@ static int run_syn(SynArgs a, size_t lds, int cus, hipStream_t s)
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// small K: the persistent syn_small_kernel (grid = resident workgroups), plus the listed kernel as run_syn
-template <int RT, int KM>
-static int run_syn_small(SynArgs a, size_t lds, int cus, hipStream_t s)
-{
-    static int occ = [lds] {
-        int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (const void *)syn_small_kernel<RT, KM>, kMacBlock, lds) !=
-                hipSuccess || o <= 0)
-            o = 1;
-        return o;
-    }();
-    const int per_cu = KFEC_SYN_SMALL_WGS > 0 ? KFEC_SYN_SMALL_WGS : occ;
-    const uint32_t need = (a.total + kMacBlock - 1) / kMacBlock;
-    const uint32_t nb = std::max(1u, std::min(need, (uint32_t)(std::max(cus, 1) * per_cu)));
-    hipLaunchKernelGGL((syn_small_kernel<RT, KM>), dim3(nb), dim3(kMacBlock), lds, s, a);
-    if (!a.list_count) return hipGetLastError() == hipSuccess ? 0 : -3;
-    const uint64_t tasks = (uint64_t)a.G * (a.cols_pad / 64);
-    const uint32_t nl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((tasks + 3) / 4, (uint64_t)std::max(cus, 1) * 8));
-    hipLaunchKernelGGL((syn_list_kernel<32, RT, 0>), dim3(nl), dim3(kMacBlock), 0, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
-static bool syn_small_ok(int vec, int K, int rt, size_t cols)
-{
-    return KFEC_SYN_SMALL && vec == 32 && K <= 12 && rt <= 4 && syn_wave_groups(cols) * (size_t)rt * rt <= 64;
-}
-
 static int dispatch_syn(int vec, int rt, SynArgs a, size_t lds, int cus, hipStream_t s)
 {
-    if (syn_small_ok(vec, (int)a.K, rt, a.cols)) {
-        const bool k8 = a.K <= 8;
-        switch (rt) {
-        case 1: return k8 ? run_syn_small<1, 8>(a, lds, cus, s) : run_syn_small<1, 12>(a, lds, cus, s);
-        case 2: return k8 ? run_syn_small<2, 8>(a, lds, cus, s) : run_syn_small<2, 12>(a, lds, cus, s);
-        case 3: return k8 ? run_syn_small<3, 8>(a, lds, cus, s) : run_syn_small<3, 12>(a, lds, cus, s);
-        default: return k8 ? run_syn_small<4, 8>(a, lds, cus, s) : run_syn_small<4, 12>(a, lds, cus, s);
-        }
-    }
 #define KFEC_RT_CASES(V, P)                               \
     switch (rt) {                                         \
     case 1: return run_syn<V, 1, P>(a, lds, cus, s);      \
@@ -1608,6 +1454,9 @@ static int dispatch_syn(int vec, int rt, SynArgs a, size_t lds, int cus, hipStre
     default: return run_syn<V, 8, P>(a, lds, cus, s);     \
     }
     if (vec == kLatencyVec) KFEC_RT_CASES(4, 16)
+#if KFEC_SYN_SMALLK_PD > 0
+    if (a.K <= 12) KFEC_RT_CASES(32, KFEC_SYN_SMALLK_PD)
+#endif
     KFEC_RT_CASES(32, 0)
 #undef KFEC_RT_CASES
 }

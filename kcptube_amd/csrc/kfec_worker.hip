@@ -7,7 +7,7 @@
 // that, so the per-call path cannot pay one per group.
 //
 // How: a worker is W resident workgroups (default 8, one per CU) that poll a doorbell word in fine-grained
-// (coherent) pinned host memory.  The caller copies the group's shares into the slot's pinned stage, writes
+// (coherent) pinned host memory (each with 8 / W loads in flight; see KFEC_WORKER_POLL).  The caller copies the group's shares into the slot's pinned stage, writes
 // the doorbell (sequence number + op + K, N, B in ONE 64-bit store) and spins on the slot's completion words.
 // Workgroup w owns the 16-byte column granules [w*G/W, (w+1)*G/W) of every shard (G = pitch / 16): it pulls its
 // slice of the request body's shares into LDS in one burst of 16-byte loads over PCIe, computes its slice of
@@ -121,14 +121,29 @@ __device__ __forceinline__ void rows_mac(uint32_t (&acc)[4], const uint32_t *X, 
     auto skipped = [&](int j) -> bool { return (skip[j >> 6] >> (j & 63)) & 1ull; };
     int j = j0;
     for (; j + 4 <= K; j += 4) {
+        // every LDS read of the 4 shares (their dwords and all 4 * RT tables) is issued before the first MAC: the
+        // per-table load-use order left one LDS round trip per table on the critical path (1.3 us per request)
         uint32_t x[4];
+        uint4 ta[4][RT];
+        uint32_t tb[4][RT];
 #pragma unroll
         for (int u = 0; u < 4; ++u) x[u] = skipped(j + u) ? 0u : X[(j + u) * nc + c];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int q = 0; q < RT; ++q) {
+                const uint32_t *ent = tab + ((j + u) * R + rows[q]) * 8;
+                ta[u][q] = *reinterpret_cast<const uint4 *>(ent);
+                tb[u][q] = ent[4];
+            }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t s0 = x[u] & 0x07070707u, s1 = (x[u] >> 3) & 0x07070707u, s2 = (x[u] >> 6) & 0x03030303u;
 #pragma unroll
-            for (int q = 0; q < RT; ++q) acc[q] = tab_mac(acc[q], tab + ((j + u) * R + rows[q]) * 8, s0, s1, s2);
+            for (int q = 0; q < RT; ++q) {
+                const uint32_t t[5] = {ta[u][q].x, ta[u][q].y, ta[u][q].z, ta[u][q].w, tb[u][q]};
+                acc[q] = perm_mac(acc[q], t, s0, s1, s2);
+            }
         }
     }
     for (; j < K; ++j) {
@@ -158,7 +173,8 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x)
 }  // namespace
 
 __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, uint64_t *relay, uint32_t gen,
-                                                                uint32_t last_seq, uint64_t idle_ticks, int debug)
+                                                                uint32_t last_seq, uint64_t idle_ticks, int debug,
+                                                                int direct)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint64_t s_db;
@@ -180,46 +196,59 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
     for (;;) {
         // Wave 0 polls -- the whole wave, the value made wave-uniform: a loop under `tid == 0` leaves lanes 1-63
         // free to run on to the next barrier while lane 0 spins, and the compiler's structurized loop then
-        // replays the previous request forever.  Workgroup 0 alone polls the doorbell in host memory (several
-        // CUs reading one host line at once serialise in the root complex: ping 3.6 us at 1 poller, 12 us at 8)
-        // and relays each new doorbell through a device-memory word the other workgroups poll.  Rolling: 8 loads
-        // in flight ~0.1 us apart, each checked as it returns and reissued.
+        // replays the previous request forever.  Rolling: NP loads in flight ~0.1 us apart, each checked as it
+        // returns and reissued.  Two ways to spread a doorbell over the workgroups (KFEC_WORKER_POLL):
+        //   relay  (0): workgroup 0 alone polls the host line (8 loads in flight) and relays each new doorbell
+        //               through a device-memory word the others poll;
+        //   direct (1): every workgroup polls the host line with 8 / W loads in flight (one line read by many CUs
+        //               with 64 loads in flight serialised in the root complex: ping 12 us), no relay hop; the
+        //               device word then carries only workgroup 0's quit.
         if (tid < 64) {
-            uint64_t *src = w == 0 ? doorbell : relay;
+            const bool host = w == 0 || direct;
             const uint64_t t0 = wall_clock64();
             uint64_t v = 0;
-            constexpr int NP = 8;
-            uint64_t xs[NP];
-            auto poll = [&]() -> uint64_t {
-                return w == 0 ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                              : __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            };
-#pragma unroll
-            for (int k = 0; k < NP; ++k) {
-                xs[k] = poll();
-                __builtin_amdgcn_s_sleep(3);
-            }
-            bool hit = false;
-            for (;;) {
+            auto poll_loop = [&](auto np) {
+                constexpr int NP = decltype(np)::value;
+                uint64_t xs[NP];
+                auto poll = [&]() -> uint64_t {
+                    return host ? __hip_atomic_load(doorbell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                : __hip_atomic_load(relay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                };
 #pragma unroll
                 for (int k = 0; k < NP; ++k) {
-                    const uint64_t u = uniform64(xs[k]);
-                    if (!hit && u != 0 && db_seq(u) != last) {  // (0: nothing relayed since the launch's memset)
-                        v = u;  // (the relay's quit value ~0 has seq kSeqMask, never posted, and makes v ~0)
-                        hit = true;
+                    xs[k] = poll();
+                    __builtin_amdgcn_s_sleep(3);
+                }
+                bool hit = false;
+                for (;;) {
+#pragma unroll
+                    for (int k = 0; k < NP; ++k) {
+                        const uint64_t u = uniform64(xs[k]);
+                        if (!hit && u != 0 && db_seq(u) != last) {  // (0: nothing relayed since the launch's memset)
+                            v = u;  // (the relay's quit value ~0 has seq kSeqMask, never posted, and makes v ~0)
+                            hit = true;
+                        }
+                        if (!hit) {
+                            xs[k] = poll();
+                            __builtin_amdgcn_s_sleep(3);
+                        }
                     }
-                    if (!hit) {
-                        xs[k] = poll();
-                        __builtin_amdgcn_s_sleep(3);
+                    if (hit) break;
+                    if (w == 0) {
+                        if (wall_clock64() - t0 > idle_ticks) {  // idle: workgroup 0 decides, the others follow
+                            v = ~0ull;
+                            break;
+                        }
+                    } else if (direct && uniform64(__hip_atomic_load(relay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == ~0ull) {
+                        v = ~0ull;
+                        break;
                     }
                 }
-                if (hit) break;
-                if (w == 0 && wall_clock64() - t0 > idle_ticks) {  // idle: workgroup 0 decides, the others follow
-                    v = ~0ull;
-                    break;
-                }
-            }
-            if (w == 0 && W > 1) __hip_atomic_store(relay, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            };
+            if (w == 0 || !direct || W <= 1) poll_loop(std::integral_constant<int, 8>());
+            else if (W <= 4) poll_loop(std::integral_constant<int, 2>());
+            else poll_loop(std::integral_constant<int, 1>());
+            if (w == 0 && W > 1 && (!direct || v == ~0ull)) __hip_atomic_store(relay, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (tid == 0) s_db = v == ~0ull ? 0 : v;
         }
         __syncthreads();
@@ -256,7 +285,9 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
         // thread roles: JS groups of shares, each over ncw column lanes (so a workgroup slice of <= 64 columns
         // keeps all 4 waves busy, each on a quarter of the shares; the groups' partial sums meet in LDS)
         const int ncw = nc <= 64 ? 64 : (nc <= 128 ? 128 : kWThreads), JS = kWThreads / ncw;
-        const int jg = tid / ncw, cl = tid - jg * ncw;
+        // (ncw is a multiple of 64: the share group is wave-uniform -- say so, or the share loop, its skip tests
+        //  and the table addresses all run as per-lane VALU code with exec masks)
+        const int jg = __builtin_amdgcn_readfirstlane(tid / ncw), cl = tid - jg * ncw;
         uint32_t *s_part = reinterpret_cast<uint32_t *>(smem + kLdsPart);  // [JS][4][ncw]
         // 1. one burst of 16-byte loads: the body and the K rows' slices (clamped indices keep r[] in VGPRs; the
         //    clamped duplicates store the same bytes)
@@ -299,6 +330,8 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
             if (tid == 0) s_mat = body->mat_id;
         }
         uint32_t *out = reinterpret_cast<uint32_t *>(slot + kOffShares + (size_t)K * pitch) + ga * 4;
+        const uint64_t ts_tab = debug == 2 ? wall_clock64() : 0;
+        uint64_t ts_mac = 0;
         if (op == kOpEncode) {
             // row tiles of 4 (uniform across the workgroup); thread = (share group, column)
             const uint64_t none[4] = {0, 0, 0, 0};
@@ -317,6 +350,7 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
                         }
                     }
                 });
+                if (debug == 2 && r0 == 0) ts_mac = wall_clock64();
                 if (JS > 1) {
                     __syncthreads();
                     for (int e = tid; e < rt_n * nc; e += kWThreads) {
@@ -329,7 +363,7 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
                 }
             }
         } else {
-            const int m = min((int)body->m, R);  // (the host sends 1 <= m <= R)
+            const int m = __builtin_amdgcn_readfirstlane(min((int)body->m, R));  // (the host sends 1 <= m <= R)
             uint32_t *s_gj = reinterpret_cast<uint32_t *>(smem + kLdsGj);
             uint32_t *s_cinv = reinterpret_cast<uint32_t *>(smem + kLdsCinv);
             // 3. [S | I], S[t][u] = enc[P_t][M_u] (byte 1 of table word 0 is c * 1 = c)
@@ -374,15 +408,16 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
             }
             // 4. syndromes of the used parity shares over the present data rows, 4 at a time (uniform tiles), each
             //    share group's partial sums meeting in LDS; y_t overwrites row M_t in place
-            const uint64_t miss[4] = {body->miss[0], body->miss[1], body->miss[2], body->miss[3]};
+            const uint64_t miss[4] = {uniform64(body->miss[0]), uniform64(body->miss[1]), uniform64(body->miss[2]),
+                                      uniform64(body->miss[3])};
             const int jlo = jg * K / JS, jhi = (jg + 1) * K / JS;
             for (int t0 = 0; t0 < m; t0 += 4) {
                 int pr[4], mr[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int t = min(t0 + q, m - 1);
-                    pr[q] = (int)body->P[t] - K;
-                    mr[q] = (int)body->M[t];
+                    pr[q] = __builtin_amdgcn_readfirstlane((int)body->P[t] - K);
+                    mr[q] = __builtin_amdgcn_readfirstlane((int)body->M[t]);
                 }
                 const int rt_n = min(4, m - t0);
                 by_rows(rt_n, [&](auto rt) {
@@ -444,6 +479,10 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
             __hip_atomic_store(trace + 1, ts_comp - ts_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(trace + 2, ts_pub - ts_comp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(trace + 3, ck_comp - ck_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 4, op == kOpEncode ? ts_tab - ts_loaded : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 5, op == kOpEncode ? ts_mac - ts_tab : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 6, op == kOpEncode ? ts_comp - ts_mac : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 7, op == kOpEncode ? ts_comp - ts_loaded : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (tid == 0)
             __hip_atomic_store(done, (uint64_t)last | ((uint64_t)status << 32), __ATOMIC_RELEASE,
@@ -521,6 +560,14 @@ uint64_t idle_ticks()
     return t;
 }
 
+// KFEC_WORKER_POLL: 0 relay, 1 direct (see the kernel's poll; direct measured faster at every W: 20:3 encode
+// 9.3 vs 11.4 us per call at W = 8, profiles/r03_worker_sweep.txt)
+int poll_mode()
+{
+    static const int m = env_int("KFEC_WORKER_POLL", 1, 0, 1);
+    return m;
+}
+
 // KFEC_WORKER_DEBUG=2: device-side phase times of workgroup 0, summed and printed when the workers stop
 int debug_level()
 {
@@ -528,6 +575,7 @@ int debug_level()
     return d;
 }
 std::atomic<uint64_t> g_dbg_n{0}, g_dbg_load{0}, g_dbg_comp{0}, g_dbg_pub{0}, g_dbg_clk{0};
+std::atomic<uint64_t> g_dbg_ne{0}, g_dbg_etab{0}, g_dbg_emac{0}, g_dbg_ered{0}, g_dbg_ecomp{0};
 
 inline uint64_t load_acq(const uint8_t *p) { return __atomic_load_n(reinterpret_cast<const uint64_t *>(p), __ATOMIC_ACQUIRE); }
 
@@ -585,7 +633,7 @@ int launch_worker(Slot &s)
     // the relay word is cleared in stream order: after the previous worker's last workgroup, before this one
     if (hipMemsetAsync(s.d_relay, 0, 256, s.stream) != hipSuccess) return KFEC_EHIP;
     hipLaunchKernelGGL(kfec_worker_kernel, dim3(n_wgs()), dim3(kWThreads), kLdsBytes, s.stream, s.h, s.d_relay, s.gen,
-                       s.seq - 1, idle_ticks(), debug_level());
+                       s.seq - 1, idle_ticks(), debug_level(), poll_mode());
     if (hipGetLastError() != hipSuccess) {
         s.running = false;
         return KFEC_EHIP;
@@ -630,6 +678,13 @@ int post_and_wait(Slot &s, uint32_t op, int K, int N, int B)
                 g_dbg_comp += load_acq(s.h + kOffTrace + 8);
                 g_dbg_pub += load_acq(s.h + kOffTrace + 16);
                 g_dbg_clk += load_acq(s.h + kOffTrace + 24);
+                if (op == kOpEncode) {
+                    g_dbg_ne += 1;
+                    g_dbg_etab += load_acq(s.h + kOffTrace + 32);
+                    g_dbg_emac += load_acq(s.h + kOffTrace + 40);
+                    g_dbg_ered += load_acq(s.h + kOffTrace + 48);
+                    g_dbg_ecomp += load_acq(s.h + kOffTrace + 56);
+                }
             }
             return st;
         }
@@ -760,6 +815,11 @@ void worker_stop(int device)
                 (unsigned long long)g_dbg_n.load(), g_dbg_load.load() / 100.0 / g_dbg_n.load(),
                 g_dbg_comp.load() / 100.0 / g_dbg_n.load(), g_dbg_pub.load() / 100.0 / g_dbg_n.load(),
                 g_dbg_comp.load() ? 100.0 * g_dbg_clk.load() / g_dbg_comp.load() : 0.0);
+    if (debug_level() == 2 && g_dbg_ne.load())
+        fprintf(stderr, "kfec worker: encodes %llu: tables-check %.2f mac %.2f reduce+store %.2f compute %.2f us\n",
+                (unsigned long long)g_dbg_ne.load(), g_dbg_etab.load() / 100.0 / g_dbg_ne.load(),
+                g_dbg_emac.load() / 100.0 / g_dbg_ne.load(), g_dbg_ered.load() / 100.0 / g_dbg_ne.load(),
+                g_dbg_ecomp.load() / 100.0 / g_dbg_ne.load());
     DevWorkers &d = g_dev[device];
     {
         std::lock_guard<std::mutex> lk(d.init_mu);

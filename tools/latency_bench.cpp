@@ -57,6 +57,16 @@ int main()
     js += ", \"kfec_decode_1_group_3_lost_us\": " + std::to_string(us_since(t0) / reps);
     js += ", \"worker_requests\": " + std::to_string(kfec_worker_requests());
     bool ok = n_out == 3 && !std::memcmp(out.data(), data.data(), 3 * B);
+    // per-call encode cost against K (N = K + 3, B = 1440): the slope is the per-share cost of the call
+    for (size_t k : {1, 5, 10, 20}) {
+        kfec_ctx *c2 = nullptr;
+        if (kfec_create(k, k + 3, &c2)) break;
+        for (int i = 0; i < 50; ++i) kfec_encode(c2, data.data(), k * B, B, par.data());
+        auto tk = clk::now();
+        for (int i = 0; i < reps / 2; ++i) kfec_encode(c2, data.data(), k * B, B, par.data());
+        js += ", \"kfec_encode_" + std::to_string(k) + "_3_us\": " + std::to_string(us_since(tk) / (reps / 2));
+        kfec_destroy(c2);
+    }
     // small flushes of the batched queues
     for (size_t G : {1, 16, 256, 1024}) {
         kfec_txq *tq;
