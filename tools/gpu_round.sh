@@ -18,4 +18,5 @@ timeout -k 10 200 python tools/bench_seal.py > $out/seal.json || exit 1
 timeout -k 10 200 python tools/bench_wire.py --ragged > $out/wire_ragged.json || exit 1
 for t in 1 2 4 8; do timeout -k 10 300 ./tools/pipeline_bench 20 23 1440 16384 4 3 $t || exit 1; done > $out/pipeline_threads.json
 timeout -k 10 120 ./tools/latency_bench > $out/latency.json || exit 1
+KFEC_WORKER=0 timeout -k 10 120 ./tools/latency_bench > $out/latency_launch.json || exit 1
 echo round-done

@@ -4,6 +4,7 @@
 // over many calls on one host thread.  Prints one JSON line (microseconds per call).
 // Build: g++ -O2 -std=c++17 -I include tools/latency_bench.cpp -o tools/latency_bench -L kcptube_amd -lkfec
 //        -Wl,-rpath,'$ORIGIN/../kcptube_amd'
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -16,6 +17,20 @@
 using clk = std::chrono::steady_clock;
 
 static double us_since(clk::time_point t0) { return std::chrono::duration<double, std::micro>(clk::now() - t0).count(); }
+
+// median and 90th percentile of per-call times (us) of f() over n calls
+template <typename F>
+static std::string pct(const std::string &name, int n, F &&f)
+{
+    std::vector<double> v(n);
+    for (int i = 0; i < n; ++i) {
+        const auto t = clk::now();
+        f();
+        v[i] = us_since(t);
+    }
+    std::sort(v.begin(), v.end());
+    return ", \"" + name + "_p50_us\": " + std::to_string(v[n / 2]) + ", \"" + name + "_p90_us\": " + std::to_string(v[n * 9 / 10]);
+}
 
 static void drop_pkt(void *, uint64_t, uint32_t, uint8_t, const uint8_t *, size_t) {}
 static void count_dg(void *u, uint64_t, uint32_t, uint8_t, const uint8_t *, size_t) { ++*static_cast<size_t *>(u); }
@@ -42,6 +57,7 @@ int main()
     auto t0 = clk::now();
     for (int i = 0; i < reps; ++i) kfec_encode(ctx, data.data(), K * B, B, par.data());
     js += ", \"kfec_encode_1_group_us\": " + std::to_string(us_since(t0) / reps);
+    js += pct("kfec_encode_1_group", reps, [&] { kfec_encode(ctx, data.data(), K * B, B, par.data()); });
     std::vector<size_t> ids;
     std::vector<const uint8_t *> ptrs;
     for (size_t s = 3; s < K; ++s) { ids.push_back(s); ptrs.push_back(data.data() + s * B); }
@@ -55,6 +71,8 @@ int main()
     t0 = clk::now();
     for (int i = 0; i < reps; ++i) kfec_decode(ctx, ids.data(), ptrs.data(), ids.size(), B, out_ids, out.data(), &n_out);
     js += ", \"kfec_decode_1_group_3_lost_us\": " + std::to_string(us_since(t0) / reps);
+    js += pct("kfec_decode_1_group_3_lost", reps,
+              [&] { kfec_decode(ctx, ids.data(), ptrs.data(), ids.size(), B, out_ids, out.data(), &n_out); });
     js += ", \"worker_requests\": " + std::to_string(kfec_worker_requests());
     bool ok = n_out == 3 && !std::memcmp(out.data(), data.data(), 3 * B);
     // per-call encode cost against K (N = K + 3, B = 1440): the slope is the per-share cost of the call
