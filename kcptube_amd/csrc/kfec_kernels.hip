@@ -1462,9 +1462,6 @@ static int dispatch_syn(int vec, int rt, SynArgs a, size_t lds, int cus, hipStre
 }
 
 static constexpr size_t kLdsBudget = 32 * 1024;
-#ifndef KFEC_DEC_LDS_KB
-#define KFEC_DEC_LDS_KB 32  // LDS of the coefficient-form decode's per-chunk tables (fewer, longer chunks if larger)
-#endif
 static constexpr size_t kSynLdsMax = 64 * 1024;
 static constexpr size_t kMaxItemsPerLaunch = 0x7FFFFFFFu;
 
@@ -1631,8 +1628,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     const size_t ent = entry_bytes(mt);
     return for_group_ranges(G, cols, tiles, [&](size_t g0, size_t gn) {
         const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kMacBlock - 1) / cols + 2);
-        const uint32_t JC =
-            (uint32_t)std::max<size_t>(1, std::min<size_t>(K, (size_t)KFEC_DEC_LDS_KB * 1024 / (ent * gmax)));
+        const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
         MacArgs a{};
         a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
         a.parity = static_cast<const uint8_t *>(d_parity) + g0 * R * pitch;
