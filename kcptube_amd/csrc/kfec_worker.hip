@@ -368,43 +368,74 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
             uint32_t *s_cinv = reinterpret_cast<uint32_t *>(smem + kLdsCinv);
             // 3. [S | I], S[t][u] = enc[P_t][M_u] (byte 1 of table word 0 is c * 1 = c)
             const int Wd = 2 * m, ne = m * Wd;  // ne <= 512: at most 2 entries per thread
-            for (int e = tid; e < ne; e += kWThreads) {
+            auto gj_init = [&](int e) {
                 const int t = e / Wd, u = e - t * Wd;
                 s_gj[e] = u < m ? (s_tab[((int)body->M[u] * R + ((int)body->P[t] - K)) * 8] >> 8) & 0xFFu
                                 : (uint32_t)(u - m == t);
-            }
-            if (tid == 0) s_singular = 0;
-            __syncthreads();
+            };
+            auto cinv_build = [&]() {  // perm tables of Sinv[uu][t] (the right half of the reduced [S | I])
+                if (tid < m * m) {
+                    const int uu = tid / m, t = tid - uu * m;
+                    uint32_t tb[5];
+                    gf_perm_tables(s_gj[uu * Wd + m + t], tb);
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) s_cinv[tid * 8 + i] = tb[i];
+                }
+            };
             // Gauss-Jordan without pivot search: every leading minor of a square submatrix of the parity part
             // of this systematic MDS generator is non-singular; a zero pivot is still detected and reported.
-            for (int c = 0; c < m; ++c) {
-                uint32_t f[2] = {0, 0}, pv[2] = {0, 0};
-                const uint32_t piv = s_gj[c * Wd + c];
-                if (piv == 0 && tid == 0) s_singular = 1;
-                const uint32_t inv = piv ? s_exp[255 - s_log[piv]] : 0u;
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const int e = tid + k * kWThreads;
-                    if (e < ne) {
-                        const int t = e / Wd, u = e - t * Wd;
-                        f[k] = s_gj[t * Wd + c];
-                        pv[k] = wk_gmul(s_exp, s_log, s_gj[c * Wd + u], inv);
+            if (ne <= 64) {
+                // m <= 5 (every kcptube-sized loss): wave 0 alone, wave-synchronously (a wave's LDS operations
+                // complete in order; the fences keep the compiler from moving reads above writes), while the
+                // other waves go on to their share of step 4 -- the solve is off the critical path, and it costs
+                // no workgroup barrier.  Step 5 reads the tables after step 4's barrier.
+                if (tid < 64) {
+                    if (tid < ne) gj_init(tid);
+                    if (tid == 0) s_singular = 0;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    const int t = tid / Wd, u = tid - t * Wd;
+                    for (int c = 0; c < m; ++c) {
+                        const uint32_t piv = s_gj[c * Wd + c];
+                        if (piv == 0 && tid == 0) s_singular = 1;
+                        const uint32_t inv = piv ? s_exp[255 - s_log[piv]] : 0u;
+                        uint32_t f = 0, pv = 0;
+                        if (tid < ne) {
+                            f = s_gj[t * Wd + c];
+                            pv = wk_gmul(s_exp, s_log, s_gj[c * Wd + u], inv);
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        if (tid < ne) s_gj[tid] = (t == c) ? pv : (s_gj[tid] ^ wk_gmul(s_exp, s_log, f, pv));
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                     }
+                    cinv_build();
                 }
+            } else {
+                for (int e = tid; e < ne; e += kWThreads) gj_init(e);
+                if (tid == 0) s_singular = 0;
                 __syncthreads();
+                for (int c = 0; c < m; ++c) {
+                    uint32_t f[2] = {0, 0}, pv[2] = {0, 0};
+                    const uint32_t piv = s_gj[c * Wd + c];
+                    if (piv == 0 && tid == 0) s_singular = 1;
+                    const uint32_t inv = piv ? s_exp[255 - s_log[piv]] : 0u;
 #pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const int e = tid + k * kWThreads;
-                    if (e < ne) s_gj[e] = (e / Wd == c) ? pv[k] : (s_gj[e] ^ wk_gmul(s_exp, s_log, f[k], pv[k]));
+                    for (int k = 0; k < 2; ++k) {
+                        const int e = tid + k * kWThreads;
+                        if (e < ne) {
+                            const int t = e / Wd, u = e - t * Wd;
+                            f[k] = s_gj[t * Wd + c];
+                            pv[k] = wk_gmul(s_exp, s_log, s_gj[c * Wd + u], inv);
+                        }
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int e = tid + k * kWThreads;
+                        if (e < ne) s_gj[e] = (e / Wd == c) ? pv[k] : (s_gj[e] ^ wk_gmul(s_exp, s_log, f[k], pv[k]));
+                    }
+                    __syncthreads();
                 }
-                __syncthreads();
-            }
-            if (tid < m * m) {
-                const int uu = tid / m, t = tid - uu * m;
-                uint32_t tb[5];
-                gf_perm_tables(s_gj[uu * Wd + m + t], tb);
-#pragma unroll
-                for (int i = 0; i < 5; ++i) s_cinv[tid * 8 + i] = tb[i];
+                cinv_build();
             }
             // 4. syndromes of the used parity shares over the present data rows, 4 at a time (uniform tiles), each
             //    share group's partial sums meeting in LDS; y_t overwrites row M_t in place
