@@ -62,12 +62,13 @@ def build_variant(name: str, defines: dict[str, int]) -> str:
 def build_tools(force: bool = False) -> list[str]:
     """The C++ programs over the public headers: tools/pipeline_bench (kfec_pipeline.h from C++, one
     sender + receiver per host thread, bit-exact recovery check; also run by tests/test_gpu_pipeline.py) and
-    tools/latency_bench (the per-call latency path)."""
+    tools/latency_bench (the per-call latency path) and tools/worker_check (single calls through the resident
+    worker, in a given order)."""
     inc = os.path.join(ROOT, "include")
     out = []
     for name, extra in (("pipeline_bench", ["-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include", "-L", "/opt/rocm/lib",
                                             "-lamdhip64", "-pthread"]),
-                        ("latency_bench", [])):
+                        ("latency_bench", []), ("worker_check", [])):
         src = os.path.join(ROOT, "tools", name + ".cpp")
         exe = os.path.join(ROOT, "tools", name)
         deps = [src, LIB] + [os.path.join(inc, h) for h in ("kfec.h", "kfec_frame.h", "kfec_pipeline.h", "kfec_aead.h")]
