@@ -149,3 +149,46 @@ def test_worker_matches_launch_path_and_relaunches(dev):
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(r.stdout.strip())
     assert outs[0] == outs[1] and len(outs[0]) == 64
+
+
+def test_worker_stop_and_restart_with_coders(dev, oracle):
+    """Destroying a device's last coder stops its workers (STOP doorbell, kernel joined); the next coder's first
+    call relaunches them.  Repeated, with a ping in between (kfec_worker_ping)."""
+    import gc
+    from kcptube_amd import FecCode, load_library
+    lib = load_library()
+    rng = np.random.default_rng(9)
+    for _ in range(3):
+        gc.collect()  # (no other coder may be alive on the device for the stop to happen)
+        c = FecCode(20, 23)
+        assert lib.kfec_worker_ping(c._ctx) == 0
+        _roundtrip(c, oracle, 20, 23, 1440, rng)
+        del c
+        gc.collect()
+
+
+def test_worker_many_threads_random_shapes(dev, oracle):
+    """8 threads, 2 slots, shapes inside and outside the worker's limits, decodes with inconsistent shares:
+    every result equals the oracle's."""
+    from kcptube_amd import FecCode
+    errors = []
+
+    def run(t):
+        try:
+            rng = np.random.default_rng(1000 + t)
+            for _ in range(25):
+                K = int(rng.integers(1, 40))
+                N = int(min(256, K + rng.integers(1, 20)))
+                B = int(rng.integers(1, 1600))
+                c = FecCode(K, N)
+                _roundtrip(c, oracle, K, N, B, rng, n_lost=int(rng.integers(0, min(N - K, K) + 1)),
+                           corrupt=bool(rng.random() < 0.3))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(repr(e)[:500])
+
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=180)
+    assert not errors, errors[:3]
