@@ -307,7 +307,7 @@ int kfec_decode(const kfec_ctx *cctx, const size_t *share_ids, const uint8_t *co
         if (m == 0) return KFEC_OK;  // every data share present: the reference's empty map
         if (!out || !out_ids) return KFEC_EINVAL;
         if (set_dev(ctx)) return KFEC_EHIP;
-        const int wr = kfec::worker_decode(ctx->di.device, ctx->d_enc, ctx->mat_id, (int)K, (int)N, B, row_ptr, (int)m,
+        const int wr = kfec::worker_decode(ctx->di.device, ctx->d_enc, ctx->h_enc.data(), ctx->mat_id, (int)K, (int)N, B, row_ptr, (int)m,
                                            M, P, out);
         if (wr == 0) {
             for (size_t t = 0; t < m; ++t) out_ids[t] = M[t];

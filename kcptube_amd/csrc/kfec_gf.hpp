@@ -42,7 +42,7 @@ __host__ __device__ __forceinline__ uint32_t gf_xtime(uint32_t v)
 //   t[2] = c*{0,8,16,24}      t[3] = c*{32,40,48,56}      (bits 3..5)
 //   t[4] = c*{0,64,128,192}                               (bits 6..7)
 // Built from the 8 doublings of c by linearity (c*(a^b) = c*a ^ c*b): no table lookups.
-__device__ __forceinline__ void gf_perm_tables(uint32_t c, uint32_t t[5])
+__host__ __device__ __forceinline__ void gf_perm_tables(uint32_t c, uint32_t t[5])
 {
     const uint32_t c1 = c & 0xFFu, c2 = gf_xtime(c1), c4 = gf_xtime(c2), c8 = gf_xtime(c4);
     const uint32_t c16 = gf_xtime(c8), c32 = gf_xtime(c16), c64 = gf_xtime(c32), c128 = gf_xtime(c64);

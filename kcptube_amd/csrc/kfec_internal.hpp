@@ -68,7 +68,7 @@ bool worker_enabled();
 uint64_t worker_served();  // requests the workers completed (process-wide)
 int worker_encode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int N, size_t B, const uint8_t *input,
                   uint8_t *parity_out);
-int worker_decode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int N, size_t B,
+int worker_decode(int device, const uint8_t *d_enc, const uint8_t *h_enc, uint64_t mat_id, int K, int N, size_t B,
                   const uint8_t *const *row_ptr, int m, const uint8_t *M, const uint8_t *P, uint8_t *out);
 void worker_stop(int device);
 int worker_ping(int device);  // 0, 1 workers off, < 0 KFEC_E*

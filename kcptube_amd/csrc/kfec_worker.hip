@@ -68,6 +68,7 @@ constexpr size_t kOffTrace = 512;   // u64: device-side phase times (KFEC_WORKER
 constexpr size_t kOffDone = 1024;   // u64 per workgroup, 128 bytes apart: seq | status << 32
 constexpr size_t kOffExited = 2048; // u64 per workgroup, 128 bytes apart: generation of a workgroup that has left
 constexpr size_t kLineW = 128;      // (one line per workgroup: no two CUs write into one host cache line)
+constexpr size_t kOffCinv = 3072;   // decode, m <= kHostSolveMax: the host's Sinv perm tables (8-dword entries)
 constexpr size_t kOffShares = 4096; // K rows x pitch: the shares, in row order; then the output rows
 constexpr size_t kSlotBytes = kOffShares + 2 * kStageMax;
 
@@ -84,12 +85,18 @@ __host__ __device__ inline uint64_t db_pack(uint32_t seq, uint32_t op, uint32_t 
 __host__ __device__ inline uint32_t db_seq(uint64_t v) { return (uint32_t)v & kSeqMask; }
 __host__ __device__ inline uint32_t db_op(uint64_t v) { return (uint32_t)(v >> 30) & 3u; }
 
+// decodes of up to this many lost shares have S^-1 solved on the host (a 5 x 10 Gauss-Jordan is ~0.1 us of
+// host time; on wave 0 it was 1.7 us on the request's critical path) and its perm tables sent with the request
+constexpr int kHostSolveMax = 5;
+constexpr int kCinvLoads = kHostSolveMax * kHostSolveMax * 32 / 16;  // 16-byte loads of the host tables
+static_assert(kOffExited + 8 * kLineW <= kOffCinv && kOffCinv + kCinvLoads * 16 <= kOffShares, "slot layout");
+
 struct WorkerBody {          // 128 bytes
     uint64_t enc;            // device address of the coder's matrix allocation (N x K bytes, then its tables)
     uint64_t mat_id;         // unique per built matrix: the LDS table cache key
     uint64_t miss[4];        // decode: bit j set <=> row j holds a parity share (data share j is missing)
     uint32_t m;              // decode: number of missing data shares (<= kMaxR)
-    uint32_t reserved;
+    uint32_t solved;         // decode: 1 = the host sent Sinv's perm tables at kOffCinv (m <= kHostSolveMax)
     uint8_t M[kMaxR];        // missing data ids, ascending (row t of the output)
     uint8_t P[kMaxR];        // the parity share id used for M[t] (fecpp.cpp:538-544)
     uint8_t pad[128 - 88];
@@ -172,9 +179,20 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x)
 
 }  // namespace
 
-__global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, uint64_t *relay, uint32_t gen,
-                                                                uint32_t last_seq, uint64_t idle_ticks, int debug,
-                                                                int direct)
+// s_waitcnt immediate for vmcnt(0) with expcnt / lgkmcnt left at their maxima (gfx9 encoding: vmcnt[3:0] and
+// [15:14], expcnt [6:4], lgkmcnt [11:8])
+constexpr int kVmcntZero = (0x7 << 4) | (0xF << 8);
+
+// an output dword: light -> a system-scope store, written through L2 to host memory (sc0 sc1)
+__device__ __forceinline__ void put_out(uint32_t *p, uint32_t v, int light)
+{
+    if (light) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else *p = v;
+}
+
+__global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, const uint8_t *in, uint64_t *relay,
+                                                                uint32_t gen, uint32_t last_seq, uint64_t idle_ticks,
+                                                                int debug, int direct, int light)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint64_t s_db;
@@ -185,12 +203,15 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
     for (int i = tid; i < 512; i += kWThreads) s_exp[i] = w_gf.exp[i];
     for (int i = tid; i < 256; i += kWThreads) s_log[i] = w_gf.log[i];
     if (tid == 0) s_mat = 0;  // matrix ids start at 1
-    uint64_t *doorbell = reinterpret_cast<uint64_t *>(slot + kOffDoorbell);
+    // (the request side -- doorbell, body, shares -- is `in`: the slot itself, or device memory the host writes
+    //  through the BAR; the answer side -- completion words, output rows -- is always the slot in host memory)
+    uint64_t *doorbell = reinterpret_cast<uint64_t *>(const_cast<uint8_t *>(in) + kOffDoorbell);
     uint64_t *done = reinterpret_cast<uint64_t *>(slot + kOffDone + kLineW * w);
     uint64_t *exited = reinterpret_cast<uint64_t *>(slot + kOffExited + kLineW * w);
     uint64_t *trace = reinterpret_cast<uint64_t *>(slot + kOffTrace);
-    const uint4 *h_body = reinterpret_cast<const uint4 *>(slot + kOffBody);
-    const uint4 *h_rows = reinterpret_cast<const uint4 *>(slot + kOffShares);
+    const uint4 *h_body = reinterpret_cast<const uint4 *>(in + kOffBody);
+    const uint4 *h_rows = reinterpret_cast<const uint4 *>(in + kOffShares);
+    const uint4 *h_cinv = reinterpret_cast<const uint4 *>(in + kOffCinv);
     uint32_t last = last_seq;
 
     for (;;) {
@@ -255,12 +276,18 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
         const uint64_t v = s_db;
         if (v == 0) break;
         const uint64_t ts_seen = debug == 2 ? wall_clock64() : 0;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the stage and body written before the doorbell
+        // the stage and body written before the doorbell.  light: they are in uncached device memory or coherent
+        // host memory, which no L2 line holds, so only this CU's L1 is dropped (agent scope), not the whole L2
+        if (light) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         last = db_seq(v);
         const uint32_t op = db_op(v);
         uint32_t status = 0;
         if (op == kOpStop || op == kOpPing) {
-            if (tid == 0) __hip_atomic_store(done, (uint64_t)last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (tid == 0) {
+                if (light) __hip_atomic_store(done, (uint64_t)last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                else __hip_atomic_store(done, (uint64_t)last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             if (op == kOpStop) break;
             continue;
         }
@@ -296,6 +323,8 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
             uint4 *s16 = reinterpret_cast<uint4 *>(smem + kLdsData);
             uint4 *b16 = reinterpret_cast<uint4 *>(smem + kLdsBody);
             const uint4 bq = h_body[tid & 7];
+            const bool cl16 = op == kOpDecode && tid < kCinvLoads;  // (used only if the body says solved)
+            const uint4 cq = cl16 ? h_cinv[tid] : uint4{0, 0, 0, 0};
             for (int i0 = 0; i0 < n16; i0 += kWThreads * 4) {
                 uint4 r[4];
                 int dst[4];
@@ -310,6 +339,7 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
                 for (int u = 0; u < 4; ++u) s16[dst[u]] = r[u];
             }
             if (tid < 8) b16[tid] = bq;
+            if (cl16) reinterpret_cast<uint4 *>(smem + kLdsCinv)[tid] = cq;
         }
         __syncthreads();
         const uint64_t ts_loaded = debug == 2 ? wall_clock64() : 0;
@@ -330,8 +360,8 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
             if (tid == 0) s_mat = body->mat_id;
         }
         uint32_t *out = reinterpret_cast<uint32_t *>(slot + kOffShares + (size_t)K * pitch) + ga * 4;
-        const uint64_t ts_tab = debug == 2 ? wall_clock64() : 0;
-        uint64_t ts_mac = 0;
+        const uint64_t ts_tab = debug == 2 ? __builtin_amdgcn_s_memtime() : 0;
+        uint64_t ts_mac = 0, ts_solve = 0, ts_syn = 0;
         if (op == kOpEncode) {
             // row tiles of 4 (uniform across the workgroup); thread = (share group, column)
             const uint64_t none[4] = {0, 0, 0, 0};
@@ -345,19 +375,19 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
                         rows_mac<RT>(acc, s_rows, nc, c, jlo, jhi, s_tab, R, rows, none);
 #pragma unroll
                         for (int q = 0; q < RT; ++q) {
-                            if (JS == 1) out[(r0 + q) * P4 + c] = acc[q];
+                            if (JS == 1) put_out(out + (r0 + q) * P4 + c, acc[q], light);
                             else s_part[(jg * 4 + q) * ncw + c] = acc[q];
                         }
                     }
                 });
-                if (debug == 2 && r0 == 0) ts_mac = wall_clock64();
+                if (debug == 2 && r0 == 0) ts_mac = __builtin_amdgcn_s_memtime();
                 if (JS > 1) {
                     __syncthreads();
                     for (int e = tid; e < rt_n * nc; e += kWThreads) {
                         const int q = e / nc, c = e - q * nc;
                         uint32_t a = 0;
                         for (int g = 0; g < JS; ++g) a ^= s_part[(g * 4 + q) * ncw + c];
-                        out[(r0 + q) * P4 + c] = a;
+                        put_out(out + (r0 + q) * P4 + c, a, light);
                     }
                     __syncthreads();
                 }
@@ -384,7 +414,10 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
             };
             // Gauss-Jordan without pivot search: every leading minor of a square submatrix of the parity part
             // of this systematic MDS generator is non-singular; a zero pivot is still detected and reported.
-            if (ne <= 64) {
+            if (body->solved) {
+                if (tid == 0) s_singular = 0;  // (the tables arrived with the shares in step 1)
+                if (debug == 2) ts_solve = ts_tab;
+            } else if (ne <= 64) {
                 // m <= 5 (every kcptube-sized loss): wave 0 alone, wave-synchronously (a wave's LDS operations
                 // complete in order; the fences keep the compiler from moving reads above writes), while the
                 // other waves go on to their share of step 4 -- the solve is off the critical path, and it costs
@@ -408,6 +441,7 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
                         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                     }
                     cinv_build();
+                    if (debug == 2) ts_solve = __builtin_amdgcn_s_memtime();
                 }
             } else {
                 for (int e = tid; e < ne; e += kWThreads) gj_init(e);
@@ -439,6 +473,7 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
             }
             // 4. syndromes of the used parity shares over the present data rows, 4 at a time (uniform tiles), each
             //    share group's partial sums meeting in LDS; y_t overwrites row M_t in place
+            if (debug == 2 && ne > 64) ts_solve = __builtin_amdgcn_s_memtime();
             const uint64_t miss[4] = {uniform64(body->miss[0]), uniform64(body->miss[1]), uniform64(body->miss[2]),
                                       uniform64(body->miss[3])};
             const int jlo = jg * K / JS, jhi = (jg + 1) * K / JS;
@@ -479,6 +514,7 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
                 }
             }
             __syncthreads();
+            if (debug == 2) ts_syn = __builtin_amdgcn_s_memtime();
             // 5. out_u = XOR_t Sinv[u][t] * y_t, 4 output rows at a time: the same MAC over the m y rows (gathered
             //    through a row map) with the m x m tables of Sinv
             for (int u0 = 0; u0 < m; u0 += 4) {
@@ -493,7 +529,7 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
                             for (int q = 0; q < RT; ++q) o[q] = tab_mac(o[q], s_cinv + ((u0 + q) * m + t) * 8, s0, s1, s2);
                         }
 #pragma unroll
-                        for (int q = 0; q < RT; ++q) out[(u0 + q) * P4 + c] = o[q];
+                        for (int q = 0; q < RT; ++q) put_out(out + (u0 + q) * P4 + c, o[q], light);
                     }
                 });
             }
@@ -501,8 +537,11 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
         }
         const uint64_t ts_comp = debug == 2 ? wall_clock64() : 0;
         const uint64_t ck_comp = debug == 2 ? __builtin_amdgcn_s_memtime() : 0;
-        // 6. publish: every thread's output stores complete at system scope before the completion word
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        // 6. publish: every thread's output stores complete at system scope before the completion word.  light:
+        //    the output stores were written through to the system (put_out), so waiting for their
+        //    acknowledgements is the whole release -- no L2 write-back pass
+        if (light) __builtin_amdgcn_s_waitcnt(kVmcntZero);
+        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
         if (debug == 2 && tid == 0 && w == 0) {  // device-side phase times of this request (100 MHz ticks)
             const uint64_t ts_pub = wall_clock64();
@@ -510,14 +549,22 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, u
             __hip_atomic_store(trace + 1, ts_comp - ts_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(trace + 2, ts_pub - ts_comp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(trace + 3, ck_comp - ck_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(trace + 4, op == kOpEncode ? ts_tab - ts_loaded : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(trace + 5, op == kOpEncode ? ts_mac - ts_tab : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(trace + 6, op == kOpEncode ? ts_comp - ts_mac : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(trace + 7, op == kOpEncode ? ts_comp - ts_loaded : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // (shader clocks) encode: tables-check, mac, reduce+store, compute; decode: tables-check, solve
+            // (wave 0), syndromes (all waves, from the tables), mix + store
+            const bool e = op == kOpEncode;
+            __hip_atomic_store(trace + 4, ts_tab - ck_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 5, e ? ts_mac - ts_tab : ts_solve - ts_tab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 6, e ? ck_comp - ts_mac : ts_syn - ts_tab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(trace + 7, e ? ck_comp - ck_loaded : ck_comp - ts_syn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        if (tid == 0)
-            __hip_atomic_store(done, (uint64_t)last | ((uint64_t)status << 32), __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tid == 0) {
+            if (light)
+                __hip_atomic_store(done, (uint64_t)last | ((uint64_t)status << 32), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            else
+                __hip_atomic_store(done, (uint64_t)last | ((uint64_t)status << 32), __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     if (tid == 0) __hip_atomic_store(exited, (uint64_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -531,6 +578,9 @@ struct Slot {
     std::mutex mu;
     uint8_t *h = nullptr;        // kSlotBytes of fine-grained pinned host memory
     uint64_t *d_relay = nullptr; // device-memory doorbell relay from workgroup 0 (zeroed before every launch)
+    uint8_t *in = nullptr;       // request side (doorbell, body, shares): d_in (BAR) or h
+    uint8_t *d_in = nullptr;     // uncached device memory the host writes through the BAR (large-BAR devices;
+                                 // uncached so that no L2 line of an earlier request outlives the host's writes)
     hipStream_t stream = nullptr;
     uint32_t seq = 0;            // last posted sequence number (0 = none yet)
     uint32_t gen = 0;            // generation of the last launched worker
@@ -600,6 +650,14 @@ int poll_mode()
 }
 
 // KFEC_WORKER_DEBUG=2: device-side phase times of workgroup 0, summed and printed when the workers stop
+// KFEC_WORKER_FENCES: 1 (default) = light fences (see the kernel's steps 0 and 6), 0 = full system-scope
+// acquire / release (an L2 invalidate per request, an L2 write-back per completion)
+int light_fences()
+{
+    static const int f = env_int("KFEC_WORKER_FENCES", 1, 0, 1);
+    return f;
+}
+
 int debug_level()
 {
     static const int d = env_int("KFEC_WORKER_DEBUG", 0, 0, 2);
@@ -607,6 +665,33 @@ int debug_level()
 }
 std::atomic<uint64_t> g_dbg_n{0}, g_dbg_load{0}, g_dbg_comp{0}, g_dbg_pub{0}, g_dbg_clk{0};
 std::atomic<uint64_t> g_dbg_ne{0}, g_dbg_etab{0}, g_dbg_emac{0}, g_dbg_ered{0}, g_dbg_ecomp{0};
+std::atomic<uint64_t> g_dbg_nd{0}, g_dbg_dtab{0}, g_dbg_dsolve{0}, g_dbg_dsyn{0}, g_dbg_dmix{0};
+
+// KFEC_WORKER_BAR: 1 = the request side lives in device memory the host writes through the PCIe BAR (posted
+// writes: the worker then reads its shares from local HBM, not across PCIe), 0 = in the pinned slot; default:
+// on where the device reports a large BAR.  (tools/bar_probe.hip: 28.8 KB by memcpy in 0.87 us.)
+bool bar_staging(int dev)
+{
+    const char *e = getenv("KFEC_WORKER_BAR");
+    if (e) return std::string(e) != "0";
+    int large = 0;
+    return hipDeviceGetAttribute(&large, hipDeviceAttributeIsLargeBar, dev) == hipSuccess && large;
+}
+
+// Request writes.  Device memory through the BAR is write-combined: stores may reach the device in any order,
+// so the body and shares are fenced before the doorbell, and the doorbell is fenced out (never read back: a
+// read across the BAR costs a round trip).
+inline void put(Slot &s, size_t off, const void *src, size_t n) { std::memcpy(s.in + off, src, n); }
+inline void ring(Slot &s, uint64_t v)
+{
+    if (s.d_in) {
+        __builtin_ia32_sfence();
+        *reinterpret_cast<volatile uint64_t *>(s.in + kOffDoorbell) = v;
+        __builtin_ia32_sfence();
+    } else {
+        __atomic_store_n(reinterpret_cast<uint64_t *>(s.in + kOffDoorbell), v, __ATOMIC_SEQ_CST);
+    }
+}
 
 inline uint64_t load_acq(const uint8_t *p) { return __atomic_load_n(reinterpret_cast<const uint64_t *>(p), __ATOMIC_ACQUIRE); }
 
@@ -634,6 +719,17 @@ DevWorkers *get_dev(int dev)
         }
         s.h = static_cast<uint8_t *>(p);
         s.d_relay = static_cast<uint64_t *>(q);
+        s.in = s.h;
+        if (bar_staging(dev)) {
+            void *b = nullptr;
+            if (hipExtMallocWithFlags(&b, kOffShares + kStageMax, hipDeviceMallocUncached) == hipSuccess &&
+                hipMemset(b, 0, kOffShares) == hipSuccess) {
+                s.d_in = static_cast<uint8_t *>(b);
+                s.in = s.d_in;
+            } else if (b) {
+                (void)hipFree(b);
+            }
+        }
         d.nslots = i + 1;
     }
     if (d.nslots == 0) d.failed = true;
@@ -663,8 +759,8 @@ int launch_worker(Slot &s)
     s.gen += 1;
     // the relay word is cleared in stream order: after the previous worker's last workgroup, before this one
     if (hipMemsetAsync(s.d_relay, 0, 256, s.stream) != hipSuccess) return KFEC_EHIP;
-    hipLaunchKernelGGL(kfec_worker_kernel, dim3(n_wgs()), dim3(kWThreads), kLdsBytes, s.stream, s.h, s.d_relay, s.gen,
-                       s.seq - 1, idle_ticks(), debug_level(), poll_mode());
+    hipLaunchKernelGGL(kfec_worker_kernel, dim3(n_wgs()), dim3(kWThreads), kLdsBytes, s.stream, s.h, s.in, s.d_relay, s.gen,
+                       s.seq - 1, idle_ticks(), debug_level(), poll_mode(), light_fences());
     if (hipGetLastError() != hipSuccess) {
         s.running = false;
         return KFEC_EHIP;
@@ -693,8 +789,7 @@ int post_and_wait(Slot &s, uint32_t op, int K, int N, int B)
     uint32_t seq = (s.seq + 1) & kSeqMask;
     if (seq == 0 || seq == kSeqMask) seq = 1;  // (kSeqMask: the seq of the relay's quit value)
     s.seq = seq;
-    __atomic_store_n(reinterpret_cast<uint64_t *>(s.h + kOffDoorbell), db_pack(seq, op, (uint32_t)K, (uint32_t)N, (uint32_t)B),
-                     __ATOMIC_SEQ_CST);
+    ring(s, db_pack(seq, op, (uint32_t)K, (uint32_t)N, (uint32_t)B));
     if (!s.running || leader_exited(s)) {
         const int rc = launch_worker(s);
         if (rc) return rc;
@@ -715,6 +810,12 @@ int post_and_wait(Slot &s, uint32_t op, int K, int N, int B)
                     g_dbg_emac += load_acq(s.h + kOffTrace + 40);
                     g_dbg_ered += load_acq(s.h + kOffTrace + 48);
                     g_dbg_ecomp += load_acq(s.h + kOffTrace + 56);
+                } else if (op == kOpDecode) {
+                    g_dbg_nd += 1;
+                    g_dbg_dtab += load_acq(s.h + kOffTrace + 32);
+                    g_dbg_dsolve += load_acq(s.h + kOffTrace + 40);
+                    g_dbg_dsyn += load_acq(s.h + kOffTrace + 48);
+                    g_dbg_dmix += load_acq(s.h + kOffTrace + 56);
                 }
             }
             return st;
@@ -730,8 +831,8 @@ int post_and_wait(Slot &s, uint32_t op, int K, int N, int B)
             }
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
                 if (debug_level())
-                    fprintf(stderr, "kfec worker: no answer; doorbell %llx done[0] %llx exited[0] %llx gen %u stream %d\n",
-                            (unsigned long long)load_acq(s.h + kOffDoorbell), (unsigned long long)load_acq(s.h + kOffDone),
+                    fprintf(stderr, "kfec worker: no answer; seq %llx done[0] %llx exited[0] %llx gen %u stream %d\n",
+                            (unsigned long long)s.seq, (unsigned long long)load_acq(s.h + kOffDone),
                             (unsigned long long)load_acq(s.h + kOffExited), s.gen, (int)hipStreamQuery(s.stream));
                 s.running = false;
                 return kWorkerDead;
@@ -763,15 +864,16 @@ int worker_encode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int 
     std::unique_lock<std::mutex> lk;
     Slot &s = acquire(*d, lk);
     const size_t pitch = (B + 15) & ~size_t(15), R = (size_t)(N - K);
-    WorkerBody *body = reinterpret_cast<WorkerBody *>(s.h + kOffBody);
-    body->enc = reinterpret_cast<uint64_t>(d_enc);
-    body->mat_id = mat_id;
-    uint8_t *rows = s.h + kOffShares;
+    WorkerBody body{};
+    body.enc = reinterpret_cast<uint64_t>(d_enc);
+    body.mat_id = mat_id;
+    put(s, kOffBody, &body, sizeof(body));
     if (pitch == B) {
-        std::memcpy(rows, input, (size_t)K * B);
+        put(s, kOffShares, input, (size_t)K * B);
     } else {
-        for (int j = 0; j < K; ++j) std::memcpy(rows + j * pitch, input + j * B, B);
+        for (int j = 0; j < K; ++j) put(s, kOffShares + j * pitch, input + j * B, B);
     }
+    const uint8_t *rows = s.h + kOffShares;  // (the output rows follow the K share rows, in the host slot)
     const int st = post_and_wait(s, kOpEncode, K, N, (int)B);
     if (st == kWorkerDead) return worker_dead(*d);
     if (st < 0) return st;
@@ -786,7 +888,39 @@ int worker_encode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int 
     return 0;
 }
 
-int worker_decode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int N, size_t B,
+// S = rows P_t, columns M_u of the coder's matrix; Gauss-Jordan on [S | I] (no pivot search, as on the
+// device: every square submatrix of the parity part is non-singular) and the perm tables of S^-1 in the
+// kernel's s_cinv layout.  false: a zero pivot (the device solve then runs and reports it).
+bool host_solve(const uint8_t *h_enc, int K, int m, const uint8_t *M, const uint8_t *P, uint32_t *tab)
+{
+    static const GfTables gt = make_gf_tables();
+    auto mul = [&](uint32_t a, uint32_t b) -> uint8_t { return (a && b) ? gt.exp[gt.log[a] + gt.log[b]] : 0; };
+    uint8_t a[kHostSolveMax][2 * kHostSolveMax];
+    for (int t = 0; t < m; ++t)
+        for (int u = 0; u < m; ++u) {
+            a[t][u] = h_enc[(size_t)P[t] * K + M[u]];
+            a[t][m + u] = (uint8_t)(t == u);
+        }
+    for (int c = 0; c < m; ++c) {
+        if (!a[c][c]) return false;
+        const uint32_t inv = gt.exp[255 - gt.log[a[c][c]]];
+        for (int u = 0; u < 2 * m; ++u) a[c][u] = mul(a[c][u], inv);
+        for (int t = 0; t < m; ++t) {
+            const uint32_t f = a[t][c];
+            if (t == c || !f) continue;
+            for (int u = 0; u < 2 * m; ++u) a[t][u] ^= mul(f, a[c][u]);
+        }
+    }
+    for (int uu = 0; uu < m; ++uu)
+        for (int t = 0; t < m; ++t) {
+            uint32_t *e = tab + (uu * m + t) * 8;
+            gf_perm_tables(a[uu][m + t], e);
+            e[5] = e[6] = e[7] = 0;
+        }
+    return true;
+}
+
+int worker_decode(int device, const uint8_t *d_enc, const uint8_t *h_enc, uint64_t mat_id, int K, int N, size_t B,
                   const uint8_t *const *row_ptr, int m, const uint8_t *M, const uint8_t *P, uint8_t *out)
 {
     if (!env_enabled() || !shape_ok(K, N, B, m)) return 1;
@@ -795,18 +929,24 @@ int worker_decode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int 
     std::unique_lock<std::mutex> lk;
     Slot &s = acquire(*d, lk);
     const size_t pitch = (B + 15) & ~size_t(15);
-    WorkerBody *body = reinterpret_cast<WorkerBody *>(s.h + kOffBody);
-    body->enc = reinterpret_cast<uint64_t>(d_enc);
-    body->mat_id = mat_id;
-    body->miss[0] = body->miss[1] = body->miss[2] = body->miss[3] = 0;
-    body->m = (uint32_t)m;
+    WorkerBody body{};  // built here, written once (never read back across the BAR)
+    body.enc = reinterpret_cast<uint64_t>(d_enc);
+    body.mat_id = mat_id;
+    body.m = (uint32_t)m;
     for (int t = 0; t < m; ++t) {
-        body->M[t] = M[t];
-        body->P[t] = P[t];
-        body->miss[M[t] >> 6] |= 1ull << (M[t] & 63);
+        body.M[t] = M[t];
+        body.P[t] = P[t];
+        body.miss[M[t] >> 6] |= 1ull << (M[t] & 63);
     }
-    uint8_t *rows = s.h + kOffShares;
-    for (int j = 0; j < K; ++j) std::memcpy(rows + j * pitch, row_ptr[j], B);
+    uint32_t tab[kHostSolveMax * kHostSolveMax * 8];
+    static const int host_solves = env_int("KFEC_WORKER_HOST_SOLVE", 1, 0, 1);  // 0: every solve on the device
+    if (host_solves && h_enc && m <= kHostSolveMax && host_solve(h_enc, K, m, M, P, tab)) {
+        body.solved = 1;
+        put(s, kOffCinv, tab, (size_t)m * m * 32);
+    }
+    put(s, kOffBody, &body, sizeof(body));
+    for (int j = 0; j < K; ++j) put(s, kOffShares + j * pitch, row_ptr[j], B);
+    const uint8_t *rows = s.h + kOffShares;
     const int st = post_and_wait(s, kOpDecode, K, N, (int)B);
     if (st == kWorkerDead) return worker_dead(*d);
     if (st < 0) return st;
@@ -846,11 +986,18 @@ void worker_stop(int device)
                 (unsigned long long)g_dbg_n.load(), g_dbg_load.load() / 100.0 / g_dbg_n.load(),
                 g_dbg_comp.load() / 100.0 / g_dbg_n.load(), g_dbg_pub.load() / 100.0 / g_dbg_n.load(),
                 g_dbg_comp.load() ? 100.0 * g_dbg_clk.load() / g_dbg_comp.load() : 0.0);
+    // (the sub-phases are shader clocks: converted at the clock measured over the compute phases)
+    const double mhz = g_dbg_comp.load() ? 100.0 * g_dbg_clk.load() / g_dbg_comp.load() : 2400.0;
     if (debug_level() == 2 && g_dbg_ne.load())
         fprintf(stderr, "kfec worker: encodes %llu: tables-check %.2f mac %.2f reduce+store %.2f compute %.2f us\n",
-                (unsigned long long)g_dbg_ne.load(), g_dbg_etab.load() / 100.0 / g_dbg_ne.load(),
-                g_dbg_emac.load() / 100.0 / g_dbg_ne.load(), g_dbg_ered.load() / 100.0 / g_dbg_ne.load(),
-                g_dbg_ecomp.load() / 100.0 / g_dbg_ne.load());
+                (unsigned long long)g_dbg_ne.load(), g_dbg_etab.load() / mhz / g_dbg_ne.load(),
+                g_dbg_emac.load() / mhz / g_dbg_ne.load(), g_dbg_ered.load() / mhz / g_dbg_ne.load(),
+                g_dbg_ecomp.load() / mhz / g_dbg_ne.load());
+    if (debug_level() == 2 && g_dbg_nd.load())
+        fprintf(stderr, "kfec worker: decodes %llu: tables-check %.2f solve(wave 0) %.2f syndromes %.2f mix+store %.2f us\n",
+                (unsigned long long)g_dbg_nd.load(), g_dbg_dtab.load() / mhz / g_dbg_nd.load(),
+                g_dbg_dsolve.load() / mhz / g_dbg_nd.load(), g_dbg_dsyn.load() / mhz / g_dbg_nd.load(),
+                g_dbg_dmix.load() / mhz / g_dbg_nd.load());
     DevWorkers &d = g_dev[device];
     {
         std::lock_guard<std::mutex> lk(d.init_mu);
@@ -870,8 +1017,7 @@ void worker_stop(int device)
             uint32_t seq = (s.seq + 1) & kSeqMask;
             if (seq == 0 || seq == kSeqMask) seq = 1;  // (kSeqMask: the seq of the relay's quit value)
             s.seq = seq;
-            __atomic_store_n(reinterpret_cast<uint64_t *>(s.h + kOffDoorbell), db_pack(seq, kOpStop, 1, 1, 0),
-                             __ATOMIC_SEQ_CST);
+            ring(s, db_pack(seq, kOpStop, 1, 1, 0));
             const auto t0 = std::chrono::steady_clock::now();
             while (!all_exited() && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) __builtin_ia32_pause();
         }

@@ -139,16 +139,18 @@ print(h.hexdigest())
 
 
 def test_worker_matches_launch_path_and_relaunches(dev):
-    """Same bytes from the worker (with a 200 us idle timeout, so it exits and is relaunched many times) and
-    from the launch path (KFEC_WORKER=0)."""
+    """Same bytes from the worker (with a 200 us idle timeout, so it exits and is relaunched many times), from
+    the worker's other modes (requests in the pinned slot instead of device memory behind the BAR, full
+    system-scope fences, every decode solve on the device) and from the launch path (KFEC_WORKER=0)."""
     code = _DIGEST.format(root=ROOT)
     outs = []
-    for env in ({"KFEC_WORKER": "1", "KFEC_WORKER_IDLE_US": "200"}, {"KFEC_WORKER": "0"}):
+    other = {"KFEC_WORKER": "1", "KFEC_WORKER_BAR": "0", "KFEC_WORKER_FENCES": "0", "KFEC_WORKER_HOST_SOLVE": "0"}
+    for env in ({"KFEC_WORKER": "1", "KFEC_WORKER_IDLE_US": "200"}, other, {"KFEC_WORKER": "0"}):
         e = dict(os.environ, **env)
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=e)
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(r.stdout.strip())
-    assert outs[0] == outs[1] and len(outs[0]) == 64
+    assert outs[0] == outs[1] == outs[2] and len(outs[0]) == 64
 
 
 def test_worker_stop_and_restart_with_coders(dev, oracle):
