@@ -57,7 +57,8 @@ constexpr size_t kLdsGj = kLdsCinv + kMaxR * kMaxR * 32;          // m x 2m Gaus
 constexpr size_t kLdsPart = kLdsGj + kMaxR * 2 * kMaxR * 4;       // partial sums of the share groups [JS][4][ncw]
 constexpr size_t kLdsGf = kLdsPart + 4 * 1024;                    // exp[512] + log[256]
 constexpr size_t kLdsBody = kLdsGf + 768;                         // the request body (128 bytes)
-constexpr size_t kLdsBytes = kLdsBody + 128;
+constexpr size_t kLdsDtab = kLdsBody + 128;                       // decode: perm tables of the host's D (m x K)
+constexpr size_t kLdsBytes = kLdsDtab + kTabMax;
 static_assert(kLdsBytes <= 64 * 1024, "a worker workgroup fits the default 64 KiB of LDS");
 
 // Slot layout in pinned host memory (offsets in bytes).  The host writes the doorbell, the body and the shares;
@@ -68,7 +69,7 @@ constexpr size_t kOffTrace = 512;   // u64: device-side phase times (KFEC_WORKER
 constexpr size_t kOffDone = 1024;   // u64 per workgroup, 128 bytes apart: seq | status << 32
 constexpr size_t kOffExited = 2048; // u64 per workgroup, 128 bytes apart: generation of a workgroup that has left
 constexpr size_t kLineW = 128;      // (one line per workgroup: no two CUs write into one host cache line)
-constexpr size_t kOffCinv = 3072;   // decode, m <= kHostSolveMax: the host's Sinv perm tables (8-dword entries)
+constexpr size_t kOffCinv = 3072;   // decode, host-solved: D = S^-1 [E | I] over the K staged rows, m x K bytes
 constexpr size_t kOffShares = 4096; // K rows x pitch: the shares, in row order; then the output rows
 constexpr size_t kSlotBytes = kOffShares + 2 * kStageMax;
 
@@ -85,10 +86,13 @@ __host__ __device__ inline uint64_t db_pack(uint32_t seq, uint32_t op, uint32_t 
 __host__ __device__ inline uint32_t db_seq(uint64_t v) { return (uint32_t)v & kSeqMask; }
 __host__ __device__ inline uint32_t db_op(uint64_t v) { return (uint32_t)(v >> 30) & 3u; }
 
-// decodes of up to this many lost shares have S^-1 solved on the host (a 5 x 10 Gauss-Jordan is ~0.1 us of
-// host time; on wave 0 it was 1.7 us on the request's critical path) and its perm tables sent with the request
-constexpr int kHostSolveMax = 5;
-constexpr int kCinvLoads = kHostSolveMax * kHostSolveMax * 32 / 16;  // 16-byte loads of the host tables
+// Decodes with m <= kHostSolveMax lost shares and m * m * K <= kHostSolveWork have their whole decode matrix
+// solved on the host: out_u = XOR_j D[u][j] * row_j over the K staged rows, D = S^-1 * (the rows' columns of
+// [E | I]) -- a few hundred table multiplies (~0.2 us), where the device's solve + syndromes + mix took 3.2 us
+// on the request's critical path.  The device then runs the encode MAC with D's tables (one pass, no solve).
+constexpr int kHostSolveMax = 8;
+constexpr int kHostSolveWork = 1024;
+constexpr int kCinvLoads = 512 / 16;  // 16-byte loads of D (m * K <= 512: shape_ok's R * K bound)
 static_assert(kOffExited + 8 * kLineW <= kOffCinv && kOffCinv + kCinvLoads * 16 <= kOffShares, "slot layout");
 
 struct WorkerBody {          // 128 bytes
@@ -96,7 +100,7 @@ struct WorkerBody {          // 128 bytes
     uint64_t mat_id;         // unique per built matrix: the LDS table cache key
     uint64_t miss[4];        // decode: bit j set <=> row j holds a parity share (data share j is missing)
     uint32_t m;              // decode: number of missing data shares (<= kMaxR)
-    uint32_t solved;         // decode: 1 = the host sent Sinv's perm tables at kOffCinv (m <= kHostSolveMax)
+    uint32_t solved;         // decode: 1 = the host sent D (m x K bytes, row-major) at kOffCinv
     uint8_t M[kMaxR];        // missing data ids, ascending (row t of the output)
     uint8_t P[kMaxR];        // the parity share id used for M[t] (fecpp.cpp:538-544)
     uint8_t pad[128 - 88];
@@ -348,7 +352,8 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, c
         uint32_t *s_tab = reinterpret_cast<uint32_t *>(smem + kLdsTab);
         uint32_t *s_rows = reinterpret_cast<uint32_t *>(smem + kLdsData);  // [K][nc] dwords
         // 2. parity-row perm tables of this matrix: s_tab[(j * R + r) * 8 + i], kept while the matrix is reused
-        if (body->mat_id != s_mat) {
+        const bool fused = op == kOpDecode && body->solved;  // (LDS broadcast: uniform)
+        if (!fused && body->mat_id != s_mat) {
             const uint32_t *g_tab =
                 reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(body->enc) + enc_tab_offset(K, N));
             const int rows = (int)enc_tab_rows(R), n = K * R * 5;
@@ -362,17 +367,36 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, c
         uint32_t *out = reinterpret_cast<uint32_t *>(slot + kOffShares + (size_t)K * pitch) + ga * 4;
         const uint64_t ts_tab = debug == 2 ? __builtin_amdgcn_s_memtime() : 0;
         uint64_t ts_mac = 0, ts_solve = 0, ts_syn = 0;
-        if (op == kOpEncode) {
+        if (op == kOpEncode || fused) {
+            // encode: the R parity rows from the matrix's tables; fused decode: the m output rows from the
+            // tables of the host's D, built here from its bytes (one entry per thread)
+            const uint32_t *tab = s_tab;
+            int RR = R;
+            if (fused) {
+                RR = __builtin_amdgcn_readfirstlane(min((int)body->m, R));
+                if (debug == 2) ts_solve = __builtin_amdgcn_s_memtime();  // (fused: "solve" = building D's tables)
+                uint32_t *s_dtab = reinterpret_cast<uint32_t *>(smem + kLdsDtab);
+                const uint8_t *coef = smem + kLdsCinv;  // D[u][j], as loaded in step 1
+                for (int e = tid; e < RR * K; e += kWThreads) {
+                    const int j = e / RR, u = e - j * RR;
+                    uint32_t tb[5];
+                    gf_perm_tables(coef[u * K + j], tb);
+                    *reinterpret_cast<uint4 *>(s_dtab + e * 8) = uint4{tb[0], tb[1], tb[2], tb[3]};
+                    s_dtab[e * 8 + 4] = tb[4];
+                }
+                __syncthreads();
+                tab = s_dtab;
+            }
             // row tiles of 4 (uniform across the workgroup); thread = (share group, column)
             const uint64_t none[4] = {0, 0, 0, 0};
             const int jlo = jg * K / JS, jhi = (jg + 1) * K / JS;
-            for (int r0 = 0; r0 < R; r0 += 4) {
-                const int rows[4] = {r0, r0 + 1, r0 + 2, r0 + 3}, rt_n = min(4, R - r0);
+            for (int r0 = 0; r0 < RR; r0 += 4) {
+                const int rows[4] = {r0, r0 + 1, r0 + 2, r0 + 3}, rt_n = min(4, RR - r0);
                 by_rows(rt_n, [&](auto rt) {
                     constexpr int RT = decltype(rt)::value;
                     for (int c = cl; c < nc; c += ncw) {
                         uint32_t acc[4] = {0, 0, 0, 0};
-                        rows_mac<RT>(acc, s_rows, nc, c, jlo, jhi, s_tab, R, rows, none);
+                        rows_mac<RT>(acc, s_rows, nc, c, jlo, jhi, tab, RR, rows, none);
 #pragma unroll
                         for (int q = 0; q < RT; ++q) {
                             if (JS == 1) put_out(out + (r0 + q) * P4 + c, acc[q], light);
@@ -380,7 +404,7 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, c
                         }
                     }
                 });
-                if (debug == 2 && r0 == 0) ts_mac = __builtin_amdgcn_s_memtime();
+                if (debug == 2 && r0 == 0) ts_mac = ts_syn = __builtin_amdgcn_s_memtime();  // (fused: "syndromes")
                 if (JS > 1) {
                     __syncthreads();
                     for (int e = tid; e < rt_n * nc; e += kWThreads) {
@@ -414,10 +438,7 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, c
             };
             // Gauss-Jordan without pivot search: every leading minor of a square submatrix of the parity part
             // of this systematic MDS generator is non-singular; a zero pivot is still detected and reported.
-            if (body->solved) {
-                if (tid == 0) s_singular = 0;  // (the tables arrived with the shares in step 1)
-                if (debug == 2) ts_solve = ts_tab;
-            } else if (ne <= 64) {
+            if (ne <= 64) {
                 // m <= 5 (every kcptube-sized loss): wave 0 alone, wave-synchronously (a wave's LDS operations
                 // complete in order; the fences keep the compiler from moving reads above writes), while the
                 // other waves go on to their share of step 4 -- the solve is off the critical path, and it costs
@@ -889,9 +910,11 @@ int worker_encode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int 
 }
 
 // S = rows P_t, columns M_u of the coder's matrix; Gauss-Jordan on [S | I] (no pivot search, as on the
-// device: every square submatrix of the parity part is non-singular) and the perm tables of S^-1 in the
-// kernel's s_cinv layout.  false: a zero pivot (the device solve then runs and reports it).
-bool host_solve(const uint8_t *h_enc, int K, int m, const uint8_t *M, const uint8_t *P, uint32_t *tab)
+// device: every square submatrix of the parity part is non-singular), then D[u][j] for the K staged rows:
+// Sinv[u][t] for row M_t (which holds parity share P_t), XOR_t Sinv[u][t] * E[P_t][j] for a present data row j
+// (out_u = XOR_t Sinv[u][t] * (P_t - XOR_j E[P_t][j] * D_j), regrouped by row).  false: a zero pivot (the
+// device solve then runs and reports it).
+bool host_solve(const uint8_t *h_enc, int K, int m, const uint8_t *M, const uint8_t *P, uint8_t *D)
 {
     static const GfTables gt = make_gf_tables();
     auto mul = [&](uint32_t a, uint32_t b) -> uint8_t { return (a && b) ? gt.exp[gt.log[a] + gt.log[b]] : 0; };
@@ -911,12 +934,26 @@ bool host_solve(const uint8_t *h_enc, int K, int m, const uint8_t *M, const uint
             for (int u = 0; u < 2 * m; ++u) a[t][u] ^= mul(f, a[c][u]);
         }
     }
-    for (int uu = 0; uu < m; ++uu)
-        for (int t = 0; t < m; ++t) {
-            uint32_t *e = tab + (uu * m + t) * 8;
-            gf_perm_tables(a[uu][m + t], e);
-            e[5] = e[6] = e[7] = 0;
+    int held[256];  // staged row -> t if it holds parity share P_t, else -1
+    for (int j = 0; j < K; ++j) held[j] = -1;
+    for (int t = 0; t < m; ++t) held[M[t]] = t;
+    for (int u = 0; u < m; ++u) {
+        uint8_t *d = D + (size_t)u * K;
+        int ls[kHostSolveMax];  // log Sinv[u][t] (-1: zero)
+        for (int t = 0; t < m; ++t) ls[t] = a[u][m + t] ? gt.log[a[u][m + t]] : -1;
+        for (int j = 0; j < K; ++j) {
+            if (held[j] >= 0) {
+                d[j] = a[u][m + held[j]];
+                continue;
+            }
+            uint32_t x = 0;
+            for (int t = 0; t < m; ++t) {
+                const uint32_t e = h_enc[(size_t)P[t] * K + j];
+                if (e && ls[t] >= 0) x ^= gt.exp[ls[t] + gt.log[e]];
+            }
+            d[j] = (uint8_t)x;
         }
+    }
     return true;
 }
 
@@ -938,11 +975,12 @@ int worker_decode(int device, const uint8_t *d_enc, const uint8_t *h_enc, uint64
         body.P[t] = P[t];
         body.miss[M[t] >> 6] |= 1ull << (M[t] & 63);
     }
-    uint32_t tab[kHostSolveMax * kHostSolveMax * 8];
+    uint8_t D[512];
     static const int host_solves = env_int("KFEC_WORKER_HOST_SOLVE", 1, 0, 1);  // 0: every solve on the device
-    if (host_solves && h_enc && m <= kHostSolveMax && host_solve(h_enc, K, m, M, P, tab)) {
+    if (host_solves && h_enc && m <= kHostSolveMax && m * m * K <= kHostSolveWork && m * K <= 512 &&
+        host_solve(h_enc, K, m, M, P, D)) {
         body.solved = 1;
-        put(s, kOffCinv, tab, (size_t)m * m * 32);
+        put(s, kOffCinv, D, (size_t)m * K);
     }
     put(s, kOffBody, &body, sizeof(body));
     for (int j = 0; j < K; ++j) put(s, kOffShares + j * pitch, row_ptr[j], B);
