@@ -702,7 +702,22 @@ bool bar_staging(int dev)
 // Request writes.  Device memory through the BAR is write-combined: stores may reach the device in any order,
 // so the body and shares are fenced before the doorbell, and the doorbell is fenced out (never read back: a
 // read across the BAR costs a round trip).
-inline void put(Slot &s, size_t off, const void *src, size_t n) { std::memcpy(s.in + off, src, n); }
+// Into BAR memory by 32-byte stores: 28.8 KB in 0.68 us against memcpy's 0.82 (tools/bar_probe.hip on the box;
+// `rep movsb` is as fast for one large copy but made the decode's per-row copies several us slower).
+typedef uint8_t u8x32 __attribute__((vector_size(32), aligned(1)));  // (one ymm register under avx2)
+__attribute__((target("avx2"))) void copy_wc_avx2(uint8_t *d, const uint8_t *s, size_t n)
+{
+    size_t i = 0;
+    for (; i + 32 <= n; i += 32) *reinterpret_cast<u8x32 *>(d + i) = *reinterpret_cast<const u8x32 *>(s + i);
+    if (i < n) std::memcpy(d + i, s + i, n - i);
+}
+
+inline void put(Slot &s, size_t off, const void *src, size_t n)
+{
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (s.d_in && avx2) copy_wc_avx2(s.in + off, static_cast<const uint8_t *>(src), n);
+    else std::memcpy(s.in + off, src, n);
+}
 inline void ring(Slot &s, uint64_t v)
 {
     if (s.d_in) {
