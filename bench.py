@@ -69,7 +69,26 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=16.0, help="target CPU-seconds of the baseline sample")
     p.add_argument("--cpu-groups", type=int, default=1 << 16, help="distinct groups of the CPU baseline sample")
+    p.add_argument("--rehearsal", action="store_true",
+                   help="allow more ranks than visible GPUs (ranks share devices as LOCAL_RANK %% count; also "
+                        "KFEC_BENCH_REHEARSAL=1): a test of the partition, never a scaling number")
     return p.parse_args()
+
+
+def rehearsal_allowed(args) -> bool:
+    return bool(args.rehearsal) or os.environ.get("KFEC_BENCH_REHEARSAL", "0") not in ("", "0")
+
+
+def check_devices(world: int, count: int, rehearsal: bool) -> str | None:
+    """None if `world` ranks may run on `count` visible devices, else the refusal message.  One rank per GPU:
+    fewer devices than ranks would put several ranks on one GPU and report a scaling number no node measured,
+    so it is refused unless the run is an explicit rehearsal."""
+    if count < 1:
+        return "no GPU visible"
+    if world > count and not rehearsal:
+        return (f"{world} ranks but only {count} visible GPU(s): one rank per GPU is required "
+                f"(pass --rehearsal or KFEC_BENCH_REHEARSAL=1 to share devices on purpose)")
+    return None
 
 
 def usable_cores() -> tuple[int, dict]:
@@ -264,6 +283,15 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # (device_count does not initialise the GPU; refuse before the rendezvous and before any device work)
+    n_dev = torch.cuda.device_count()
+    rehearsal = rehearsal_allowed(args)
+    why = check_devices(world, n_dev, rehearsal)
+    if why:
+        print(f"bench.py: {why}", file=sys.stderr)
+        sys.exit(2)
+    devices = min(world, n_dev)  # distinct devices the ranks run on
+
     from kcptube_amd import FecCode
     from kcptube_amd.partition import combine_digests, group_range
 
@@ -439,7 +467,7 @@ def main():
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": devices,  # distinct GPUs (= ranks, except in a --rehearsal on a smaller box)
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
@@ -451,8 +479,7 @@ def main():
         "config": {"workload": workload, "fec": f"{K}:{R}", "kcp_mtu": B, "pitch": pitch, "groups_per_gpu": G,
                    "global_groups": total_groups,
                    "parallelism": f"{world} independent group ranges (no collective)",
-                   # ranks map to devices as LOCAL_RANK % device_count: fewer devices than ranks is a rehearsal
-                   "devices": min(world, torch.cuda.device_count())},
+                   "ranks": world, "devices": devices, "rehearsal": world > devices},
         "roofline": roof,
         "encode_ms": round(enc_ms, 4) if do_enc else None,
         "decode_ms": round(dec_ms, 4),

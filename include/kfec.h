@@ -48,8 +48,11 @@ int kfec_create(size_t K, size_t N, kfec_ctx **out);
  * failed allocation / launch) the coder is unchanged: the new matrix is committed only once built.
  * Batch queues (kfec_pipeline.h) created on the coder must be recreated after a reset.
  * A reset must not run concurrently with any other call that uses the same coder (its queues included):
- * it frees the old matrix, which a concurrent launch may still be reading.  fecpp::fec_code has no locking
- * either; kcptube re-targets a coder from the thread that uses it (client.cpp:1755, relay.cpp:947). */
+ * it re-points the coder's K, N and matrix without a lock on the per-call path.  fecpp::fec_code has no
+ * locking either; kcptube re-targets a coder from the thread that uses it (client.cpp:1755, relay.cpp:947).
+ * Matrices are shared per (device, K, N) and immutable: create and reset build one on the first use of a shape
+ * and are a lookup afterwards (no allocation, launch or synchronisation); the old matrix stays valid for
+ * batched launches still in flight.  The cached matrices are released with the device's last coder. */
 int kfec_reset(kfec_ctx *ctx, size_t K, size_t N);
 void kfec_destroy(kfec_ctx *ctx);
 size_t kfec_get_K(const kfec_ctx *ctx);
@@ -130,8 +133,10 @@ int kfec_device(const kfec_ctx *ctx);
  * kfec_encode / kfec_decode run on a resident worker (KFEC_WORKER_WGS workgroups, default 8, per slot: no
  * launch or stream synchronisation per call) for groups with N - K <= 16, N * round16(B) <= 36 KiB and
  * (N - K) * K <= 512; other shapes take a kernel launch.  A worker leaves the GPU after KFEC_WORKER_IDLE_US
- * (default 20000) without a request and when the last coder of its device is destroyed, and is relaunched on
- * demand.  KFEC_WORKER=0 turns the workers off; KFEC_WORKER=1 makes a worker failure an error instead of a
+ * (default 20000) without a request, between requests once it has been resident KFEC_WORKER_LEASE_US
+ * (default 2000: the bound on how long a device-wide synchronisation -- hipFree, hipHostFree,
+ * hipDeviceSynchronize -- in another thread waits for it while calls continue), and when the last coder of
+ * its device is destroyed; it is relaunched on demand.  KFEC_WORKER=0 turns the workers off; KFEC_WORKER=1 makes a worker failure an error instead of a
  * switch to the launch path; KFEC_WORKER_SLOTS (1-8, default 2) sets the workers per device. */
 uint64_t kfec_worker_requests(void);
 /* One empty request through a resident worker of the coder's device (diagnostics: the communication floor of

@@ -68,7 +68,9 @@ def build_tools(force: bool = False) -> list[str]:
     out = []
     for name, extra in (("pipeline_bench", ["-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include", "-L", "/opt/rocm/lib",
                                             "-lamdhip64", "-pthread"]),
-                        ("latency_bench", []), ("worker_check", [])):
+                        ("latency_bench", ["-ldl"]), ("worker_check", []),
+                        ("side_effects", ["-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include", "-L", "/opt/rocm/lib",
+                                          "-lamdhip64", "-pthread"])):
         src = os.path.join(ROOT, "tools", name + ".cpp")
         exe = os.path.join(ROOT, "tools", name)
         deps = [src, LIB] + [os.path.join(inc, h) for h in ("kfec.h", "kfec_frame.h", "kfec_pipeline.h", "kfec_aead.h")]

@@ -1,6 +1,9 @@
 // kfec_api.cpp -- C ABI of libkfec.so (include/kfec.h): coder contexts, argument checking with the
 // reference's error conventions, single-group staging for the fecpp::fec_code drop-in, and the
-// batched device-resident entry points.  All arithmetic runs in the HIP kernels of kfec_kernels.hip.
+// batched device-resident entry points.  Every output byte (parity, recovered shards) is computed by the HIP
+// kernels (kfec_kernels.hip, kfec_worker.hip).  The host does bookkeeping and coefficients only: the
+// single-group decode selects its shares here (fecpp.cpp:528-548), and for small losses through the resident
+// worker the m x K decode coefficients are solved on the host (host_solve, kfec_worker.hip).
 #include "../../include/kfec.h"
 #include "../../include/kfec_frame.h"
 
@@ -17,18 +20,45 @@
 
 #include "kfec_internal.hpp"
 
+namespace {
+
+// The encoding matrix depends on (K, N) alone, so every coder of one device with the same (K, N) shares ONE
+// immutable device allocation (the N x K matrix, then its perm tables) and its host copy.  kcptube builds a
+// coder per connection and direction and re-targets it with reset_martix (client.cpp:1755, relay.cpp:947,
+// server.cpp:438): after the first coder of a shape, create / reset are a table lookup -- no allocation, no
+// launch, no synchronisation.  Matrices are never freed while a coder of their device lives (so a batched
+// launch still reading the old matrix after a reset stays valid, and no hipFree -- which waits for every stream
+// of the device, the resident worker's included -- runs on a coder's lifecycle); they are released with the
+// device's last coder, after its workers have stopped.
+struct Matrix {
+    size_t K = 0, N = 0;
+    uint8_t *d = nullptr;     // N x K matrix, then the perm tables (enc_alloc_bytes)
+    std::vector<uint8_t> h;   // host copy of the N x K matrix
+    uint64_t id = 0;          // unique per built matrix: the resident worker's LDS table-cache key
+};
+struct DevMatrices {
+    std::mutex mu;
+    hipStream_t stream = nullptr;  // builds run here
+    std::vector<Matrix *> all;
+};
+DevMatrices g_mats[64];
+std::atomic<uint64_t> g_mat_ids{0};
+
+}  // namespace
+
 struct kfec_ctx {
     size_t K = 0, N = 0;
     kfec::DeviceInfo di;
-    uint8_t *d_enc = nullptr;  // N x K encoding matrix on the device
-    std::vector<uint8_t> h_enc;
-    hipStream_t stream = nullptr;  // private stream of the single-group API
-    std::mutex mu;                 // single-group staging is shared by encode and decode callers
+    const uint8_t *d_enc = nullptr;  // the shared matrix of (K, N) on the device (Matrix::d)
+    const uint8_t *h_enc = nullptr;  // its host copy (Matrix::h)
+    uint64_t mat_id = 0;             // Matrix::id
+    hipStream_t stream = nullptr;    // private stream of the single-group launch path (created on first use)
+    std::mutex mu;                   // single-group staging is shared by encode and decode callers
     uint8_t *d_stage = nullptr;
     size_t stage_cap = 0;
     uint8_t *h_stage = nullptr;  // fine-grained pinned host staging the kernels read and write in place
     size_t h_stage_cap = 0;
-    uint64_t mat_id = 0;         // unique id of the current matrix (the resident worker's table cache key)
+    bool counted = false;        // kfec_create returned it (counted in g_live)
 };
 
 int kfec::current_device_cus()
@@ -50,9 +80,8 @@ namespace {
 
 bool kn_valid(size_t K, size_t N) { return !(K == 0 || N == 0 || K > 256 || N > 256 || K > N); }
 
-std::atomic<uint64_t> g_mat_ids{0};
 std::mutex g_live_mu;
-int g_live[64];  // coders per device: the resident workers of a device stop with its last coder
+int g_live[64];  // coders per device: the resident workers and the cached matrices of a device go with its last coder
 
 int probe_device(kfec::DeviceInfo &di)
 {
@@ -63,32 +92,96 @@ int probe_device(kfec::DeviceInfo &di)
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return KFEC_ENODEV;
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return KFEC_ENODEV;  // code objects are gfx950-only
+    if (dev < 0 || dev >= 64) return KFEC_ENODEV;
     di.device = dev;
     di.cus = prop.multiProcessorCount;
     return KFEC_OK;
 }
 
-// Build the (K, N) matrix into fresh buffers and commit K, N and the matrix only once all of it succeeded:
-// a failed reset leaves the context exactly as it was (the compat class keeps its old K and N too).
-int build_matrix(kfec_ctx *c, size_t K, size_t N)
+// The shared matrix of (K, N) on the current device, built on first use.  nullptr + rc on failure.
+const Matrix *get_matrix(int dev, size_t K, size_t N, int &rc)
 {
-    const size_t bytes = N * K;
-    uint8_t *d = nullptr;
-    if (hipMalloc(&d, kfec::enc_alloc_bytes(K, N)) != hipSuccess) return KFEC_ENOMEM;
-    std::vector<uint8_t> h(bytes, 0);
-    if (kfec::launch_build_matrix(d, (int)K, (int)N, c->stream) ||
-        hipMemcpyAsync(h.data(), d, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess) {
-        (void)hipStreamSynchronize(c->stream);
-        (void)hipFree(d);
-        return KFEC_EHIP;
+    DevMatrices &dm = g_mats[dev];
+    std::lock_guard<std::mutex> lk(dm.mu);
+    for (const Matrix *m : dm.all)
+        if (m->K == K && m->N == N) {
+            rc = KFEC_OK;
+            return m;
+        }
+    rc = KFEC_EHIP;
+    if (!dm.stream && hipStreamCreateWithFlags(&dm.stream, hipStreamNonBlocking) != hipSuccess) {
+        dm.stream = nullptr;
+        return nullptr;
     }
-    if (c->d_enc) (void)hipFree(c->d_enc);  // the stream is idle: no launch still reads the old matrix
-    c->d_enc = d;
-    c->h_enc.swap(h);
+    Matrix *m = new (std::nothrow) Matrix;
+    if (!m) {
+        rc = KFEC_ENOMEM;
+        return nullptr;
+    }
+    try {
+        m->h.assign(N * K, 0);
+        dm.all.reserve(dm.all.size() + 1);
+    } catch (...) {
+        delete m;
+        rc = KFEC_ENOMEM;
+        return nullptr;
+    }
+    void *d = nullptr;
+    if (hipMalloc(&d, kfec::enc_alloc_bytes(K, N)) != hipSuccess) {
+        delete m;
+        rc = KFEC_ENOMEM;
+        return nullptr;
+    }
+    m->d = static_cast<uint8_t *>(d);
+    if (kfec::launch_build_matrix(m->d, (int)K, (int)N, dm.stream) ||
+        hipMemcpyAsync(m->h.data(), m->d, N * K, hipMemcpyDeviceToHost, dm.stream) != hipSuccess ||
+        hipStreamSynchronize(dm.stream) != hipSuccess) {
+        (void)hipStreamSynchronize(dm.stream);
+        (void)hipFree(m->d);  // (first use of a shape only, and only on failure)
+        delete m;
+        return nullptr;
+    }
+    m->K = K;
+    m->N = N;
+    m->id = g_mat_ids.fetch_add(1) + 1;
+    dm.all.push_back(m);
+    rc = KFEC_OK;
+    return m;
+}
+
+// Re-target the context to (K, N); commits only once the matrix exists (a failed reset leaves it unchanged).
+int set_matrix(kfec_ctx *c, size_t K, size_t N)
+{
+    int rc = KFEC_OK;
+    const Matrix *m = get_matrix(c->di.device, K, N, rc);
+    if (!m) return rc;
+    c->d_enc = m->d;
+    c->h_enc = m->h.data();
     c->K = K;
     c->N = N;
-    c->mat_id = g_mat_ids.fetch_add(1) + 1;
+    c->mat_id = m->id;
+    return KFEC_OK;
+}
+
+// The device's last coder is gone and its workers have stopped: release the cached matrices.
+void release_matrices(int dev)
+{
+    DevMatrices &dm = g_mats[dev];
+    std::lock_guard<std::mutex> lk(dm.mu);
+    for (Matrix *m : dm.all) {
+        (void)hipFree(m->d);
+        delete m;
+    }
+    dm.all.clear();
+}
+
+int ensure_stream(kfec_ctx *c)
+{
+    if (c->stream) return KFEC_OK;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        c->stream = nullptr;
+        return KFEC_EHIP;
+    }
     return KFEC_OK;
 }
 
@@ -166,18 +259,17 @@ int kfec_create(size_t K, size_t N, kfec_ctx **out)
     kfec_ctx *c = new (std::nothrow) kfec_ctx;
     if (!c) return KFEC_ENOMEM;
     c->di = di;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
-        return KFEC_EHIP;
+    {
+        // counted before the matrix exists, so that a concurrent destroy of the device's last other coder does
+        // not release the cached matrices under this one
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        ++g_live[di.device];
+        c->counted = true;
     }
-    rc = build_matrix(c, K, N);
+    rc = set_matrix(c, K, N);
     if (rc) {
         kfec_destroy(c);
         return rc;
-    }
-    if (di.device >= 0 && di.device < 64) {
-        std::lock_guard<std::mutex> lk(g_live_mu);
-        ++g_live[di.device];
     }
     *out = c;
     return KFEC_OK;
@@ -188,24 +280,30 @@ int kfec_reset(kfec_ctx *ctx, size_t K, size_t N)
     if (!ctx || !kn_valid(K, N)) return KFEC_EINVAL;  // reference throws before touching its state
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (set_dev(ctx)) return KFEC_EHIP;
-    return build_matrix(ctx, K, N);
+    return set_matrix(ctx, K, N);
 }
 
 void kfec_destroy(kfec_ctx *ctx)
 {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->di.device);
+    const int dev = ctx->di.device;
+    (void)hipSetDevice(dev);
+    // The frees below (launch-path staging only) wait for every stream of the device, so the device's last
+    // coder stops the resident workers first; otherwise a worker's lease (kfec_worker.hip) bounds the wait.
+    bool last = false;
+    if (ctx->counted) {
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        last = --g_live[dev] == 0;
+        if (last) kfec::worker_stop(dev);
+    }
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->d_enc) (void)hipFree(ctx->d_enc);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-    const int dev = ctx->di.device;
-    const bool counted = ctx->mat_id != 0;  // kfec_create returned it
     delete ctx;
-    if (counted && dev >= 0 && dev < 64) {
+    if (last) {
         std::lock_guard<std::mutex> lk(g_live_mu);
-        if (--g_live[dev] == 0) kfec::worker_stop(dev);
+        if (g_live[dev] == 0) release_matrices(dev);  // (unless a coder was created meanwhile)
     }
 }
 
@@ -215,7 +313,7 @@ size_t kfec_get_N(const kfec_ctx *ctx) { return ctx ? ctx->N : 0; }
 int kfec_enc_matrix(const kfec_ctx *ctx, uint8_t *enc)
 {
     if (!ctx || !enc) return KFEC_EINVAL;
-    std::memcpy(enc, ctx->h_enc.data(), ctx->h_enc.size());
+    std::memcpy(enc, ctx->h_enc, ctx->N * ctx->K);
     return KFEC_OK;
 }
 
@@ -238,6 +336,7 @@ int kfec_encode(const kfec_ctx *cctx, const uint8_t *input, size_t data_length, 
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (set_dev(ctx)) return KFEC_EHIP;
     const size_t off_par = al256(K * B);
+    if (ensure_stream(ctx)) return KFEC_EHIP;
     int rc = ensure_stage(ctx, off_par + al256(R * B));
     if (rc) return rc;
     if (zero_copy()) {
@@ -307,7 +406,7 @@ int kfec_decode(const kfec_ctx *cctx, const size_t *share_ids, const uint8_t *co
         if (m == 0) return KFEC_OK;  // every data share present: the reference's empty map
         if (!out || !out_ids) return KFEC_EINVAL;
         if (set_dev(ctx)) return KFEC_EHIP;
-        const int wr = kfec::worker_decode(ctx->di.device, ctx->d_enc, ctx->h_enc.data(), ctx->mat_id, (int)K, (int)N, B, row_ptr, (int)m,
+        const int wr = kfec::worker_decode(ctx->di.device, ctx->d_enc, ctx->h_enc, ctx->mat_id, (int)K, (int)N, B, row_ptr, (int)m,
                                            M, P, out);
         if (wr == 0) {
             for (size_t t = 0; t < m; ++t) out_ids[t] = M[t];
@@ -321,6 +420,7 @@ int kfec_decode(const kfec_ctx *cctx, const size_t *share_ids, const uint8_t *co
     const size_t o_data = 0, o_par = al256(K * B), o_out = o_par + al256(R * B), o_mask = o_out + al256(R * B);
     const size_t o_idx = o_mask + 256, o_st = o_idx + al256(R + 1), o_rec = o_st + 256,
                  total = o_rec + al256(kfec::decode_workspace_bytes(1, K, R));
+    if (ensure_stream(ctx)) return KFEC_EHIP;
     int rc = ensure_stage(ctx, total);
     if (rc) return rc;
     if (zero_copy()) {

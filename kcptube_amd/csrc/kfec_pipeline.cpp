@@ -331,7 +331,7 @@ void kfec_tx_destroy(kfec_tx *tx)
 
 int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t timestamp, uint8_t *pkt, size_t *pkt_len)
 {
-    if (!tx || !pkt || !pkt_len || (len && !datagram)) return KFEC_EINVAL;
+    if (!tx || (len && !datagram)) return KFEC_EINVAL;
     kfec_txq *q = tx->q;
     const bool defer = q->defer;
     if (len > q->mtu || kn_changed(q->ctx, q->K, q->N) || (!defer && (!pkt || !pkt_len))) return KFEC_EINVAL;
@@ -947,8 +947,9 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
     if (n == 0) return KFEC_OK;
     if (hipSetDevice(o->device) != hipSuccess) return KFEC_EHIP;
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    uint8_t *hd = o->h_desc.as<uint8_t>();
-    std::memmove(hd + n * 8, hd + o->max_packets * 8, n * 4);  // [off n*8][len n*4]: one copy
+    // the host table stays as kfec_opener_add wrote it ([off max*8][len max*4]), so a flush that fails can be
+    // retried: its first n offsets and first n lengths go up as two copies into [off n*8][len n*4]
+    const uint8_t *hd = o->h_desc.as<uint8_t>();
     uint8_t *dd = o->d_desc.as<uint8_t>();
     uint8_t *dr = o->d_out.as<uint8_t>();
     const size_t L = n * o->pitch;
@@ -956,7 +957,8 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
     uint8_t *ok = dr + L + n * 4;
     const size_t arena = std::max<size_t>(o->used, 4);
     if (hipMemcpyAsync(o->d_arena.p, o->h_arena.p, arena, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(dd, hd, n * 12, hipMemcpyHostToDevice, s) != hipSuccess)
+        hipMemcpyAsync(dd, hd, n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(dd + n * 8, hd + o->max_packets * 8, n * 4, hipMemcpyHostToDevice, s) != hipSuccess)
         return KFEC_EHIP;
     const uint64_t *d_off = reinterpret_cast<const uint64_t *>(dd);
     const uint32_t *d_len = reinterpret_cast<const uint32_t *>(dd + n * 8);

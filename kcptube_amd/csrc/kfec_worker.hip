@@ -24,7 +24,9 @@
 // All GF products use the perm MAC of kfec_gf.hpp with tables in LDS; the parity-row tables of the coder's
 // matrix are copied from its device allocation (enc_tab_offset) once per matrix and kept in LDS while the
 // same matrix is used.  Lifetime: workgroup 0 leaves after KFEC_WORKER_IDLE_US without a request (default
-// 20 ms) and relays a quit value through the device-memory word the other workgroups poll; all leave on op STOP.  Each
+// 20 ms) or, between requests, once the launch is KFEC_WORKER_LEASE_US old (default 2 ms: the bound on how long
+// another thread's hipFree / hipDeviceSynchronize waits for this stream), and relays a quit value through the
+// device-memory word the other workgroups poll; all leave on op STOP.  Each
 // writes its generation to its exit word; the host relaunches the worker on the next request.  Every wave
 // reaches the exit: the loop's only waits are the bounded doorbell / quit poll and workgroup barriers.
 #include "kfec_gf.hpp"
@@ -196,8 +198,10 @@ __device__ __forceinline__ void put_out(uint32_t *p, uint32_t v, int light)
 
 __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, const uint8_t *in, uint64_t *relay,
                                                                 uint32_t gen, uint32_t last_seq, uint64_t idle_ticks,
-                                                                int debug, int direct, int light)
+                                                                uint64_t lease_ticks, int debug, int direct, int light,
+                                                                int deaf)
 {
+    const uint64_t t_start = wall_clock64();  // (the lease: see the poll below)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint64_t s_db;
     __shared__ uint64_t s_mat;
@@ -249,7 +253,8 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, c
 #pragma unroll
                     for (int k = 0; k < NP; ++k) {
                         const uint64_t u = uniform64(xs[k]);
-                        if (!hit && u != 0 && db_seq(u) != last) {  // (0: nothing relayed since the launch's memset)
+                        if (!hit && u != 0 && db_seq(u) != last && !deaf) {  // (0: nothing relayed since the launch's memset;
+                                                                             //  deaf: the fallback test's knob)
                             v = u;  // (the relay's quit value ~0 has seq kSeqMask, never posted, and makes v ~0)
                             hit = true;
                         }
@@ -260,7 +265,9 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, c
                     }
                     if (hit) break;
                     if (w == 0) {
-                        if (wall_clock64() - t0 > idle_ticks) {  // idle: workgroup 0 decides, the others follow
+                        const uint64_t now = wall_clock64();
+                        if (now - t0 > idle_ticks || now - t_start > lease_ticks) {  // idle or lease over: workgroup 0
+                                                                                     // decides, the others follow
                             v = ~0ull;
                             break;
                         }
@@ -270,7 +277,13 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, c
                     }
                 }
             };
-            if (w == 0 || !direct || W <= 1) poll_loop(std::integral_constant<int, 8>());
+            // The lease: workgroup 0 also leaves once the kernel has been resident for lease_ticks, checked only
+            // here, between requests.  Any device-wide synchronisation of the process -- hipFree, hipHostFree,
+            // hipDeviceSynchronize, which wait for every stream -- then waits at most about one lease, even
+            // while other threads keep calling; the next request relaunches the worker (a launch, ~10 us, once
+            // per lease).
+            if (w == 0 && wall_clock64() - t_start > lease_ticks) v = ~0ull;
+            else if (w == 0 || !direct || W <= 1) poll_loop(std::integral_constant<int, 8>());
             else if (W <= 4) poll_loop(std::integral_constant<int, 2>());
             else poll_loop(std::integral_constant<int, 1>());
             if (w == 0 && W > 1 && (!direct || v == ~0ull)) __hip_atomic_store(relay, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -662,6 +675,22 @@ uint64_t idle_ticks()
     return t;
 }
 
+// KFEC_WORKER_LEASE_US: longest residency of one worker launch (default 2 ms): the bound on how long a
+// device-wide synchronisation elsewhere in the process waits for the worker's stream while calls continue
+uint64_t lease_ticks()
+{
+    static const uint64_t t = (uint64_t)env_int("KFEC_WORKER_LEASE_US", 2000, 100, 10000000) * 100;
+    return t;
+}
+
+// KFEC_WORKER_TEST_DEAF=1 (tests only): the worker never answers a request, so the caller's 2 s "did not
+// answer" fallback to the launch path runs
+int test_deaf()
+{
+    static const int d = env_int("KFEC_WORKER_TEST_DEAF", 0, 0, 1);
+    return d;
+}
+
 // KFEC_WORKER_POLL: 0 relay, 1 direct (see the kernel's poll; direct measured faster at every W: 20:3 encode
 // 9.3 vs 11.4 us per call at W = 8, profiles/r03_worker_sweep.txt)
 int poll_mode()
@@ -796,7 +825,7 @@ int launch_worker(Slot &s)
     // the relay word is cleared in stream order: after the previous worker's last workgroup, before this one
     if (hipMemsetAsync(s.d_relay, 0, 256, s.stream) != hipSuccess) return KFEC_EHIP;
     hipLaunchKernelGGL(kfec_worker_kernel, dim3(n_wgs()), dim3(kWThreads), kLdsBytes, s.stream, s.h, s.in, s.d_relay, s.gen,
-                       s.seq - 1, idle_ticks(), debug_level(), poll_mode(), light_fences());
+                       s.seq - 1, idle_ticks(), lease_ticks(), debug_level(), poll_mode(), light_fences(), test_deaf());
     if (hipGetLastError() != hipSuccess) {
         s.running = false;
         return KFEC_EHIP;
@@ -870,6 +899,13 @@ int post_and_wait(Slot &s, uint32_t op, int K, int N, int B)
                     fprintf(stderr, "kfec worker: no answer; seq %llx done[0] %llx exited[0] %llx gen %u stream %d\n",
                             (unsigned long long)s.seq, (unsigned long long)load_acq(s.h + kOffDone),
                             (unsigned long long)load_acq(s.h + kOffExited), s.gen, (int)hipStreamQuery(s.stream));
+                // Post STOP so that a worker that is merely slow leaves at once; one that ignores its doorbell
+                // still leaves by itself at its idle timeout or its lease (whichever comes first), and a kernel
+                // that never reaches its poll again would hold its CUs until the process ends.
+                uint32_t stop = (s.seq + 1) & kSeqMask;
+                if (stop == 0 || stop == kSeqMask) stop = 1;
+                s.seq = stop;
+                ring(s, db_pack(stop, kOpStop, 1, 1, 0));
                 s.running = false;
                 return kWorkerDead;
             }

@@ -3,8 +3,11 @@
 ``FecCode`` keeps the reference class's interface (/root/reference/src/3rd_party/fecpp.hpp:36-81):
 same names (including the ``reset_martix`` spelling), same argument meaning, same error behaviour --
 ``ValueError`` where the reference throws ``std::invalid_argument`` and empty containers where it
-returns ``{}``.  Every byte is computed by the gfx950 HIP kernels; there is no CPU compute path, and a
-missing library or GPU raises ``KfecUnavailable`` instead of falling back.
+returns ``{}``.  Every output byte (parity, recovered shards) is computed by the gfx950 HIP kernels, and a
+missing library or GPU raises ``KfecUnavailable`` instead of falling back.  Host-side work is bookkeeping and
+coefficients only: the single-group decode picks its shares on the host (fecpp.cpp:528-548) and, for the
+resident worker's small losses, solves the m x K decode coefficients there too (``host_solve`` in
+kfec_worker.hip, a few hundred GF(2^8) table multiplies); the device then applies them to the shard bytes.
 
 The batched methods take device-resident ``torch.uint8`` tensors laid out ``[G][shards][pitch]`` and run
 asynchronously on the current (or given) HIP stream -- the GPU path of the project.

@@ -52,6 +52,7 @@ class TxQueue:
         self._q = C.c_void_p()
         _check(self._lib.kfec_txq_create(code._ctx, max_groups, max_datagram, C.byref(self._q)), "kfec_txq_create")
         self.max_datagram = max_datagram
+        self._defer = False
 
     def pending(self) -> int:
         return int(self._lib.kfec_txq_pending(self._q))
@@ -66,6 +67,7 @@ class TxQueue:
         self._aead = aead  # the cipher must outlive the queue's use of it
         _check(self._lib.kfec_txq_seal(self._q, m, h, iv_seed & ((1 << 64) - 1), DEFER_DATA if defer_data else 0),
                "kfec_txq_seal")
+        self._defer = bool(defer_data)
 
     def staged(self) -> int:
         return int(self._lib.kfec_txq_staged(self._q))
@@ -104,13 +106,16 @@ class FecSender:
         """fec_maker(datagram): the data packet (the group, once complete, is queued for the flush); b"" when
         the queue defers data packets to its flush."""
         d = (C.c_uint8 * max(len(datagram), 1)).from_buffer_copy(bytes(datagram) or b"\0")
-        pkt = (C.c_uint8 * (len(datagram) + 16))()
-        n = C.c_size_t(0)
-        rc = self._lib.kfec_tx_send(self._tx, d, len(datagram), timestamp & 0xFFFFFFFF, pkt, C.byref(n))
+        if self.q._defer:  # the header's contract: pkt and pkt_len may be NULL when data packets are deferred
+            rc = self._lib.kfec_tx_send(self._tx, d, len(datagram), timestamp & 0xFFFFFFFF, None, None)
+        else:
+            pkt = (C.c_uint8 * (len(datagram) + 16))()
+            n = C.c_size_t(0)
+            rc = self._lib.kfec_tx_send(self._tx, d, len(datagram), timestamp & 0xFFFFFFFF, pkt, C.byref(n))
         if rc == -4:
             raise KfecError("kfec_tx_send: queue full, flush first")
         _check(rc, "kfec_tx_send")
-        return bytes(pkt)[:n.value]
+        return b"" if self.q._defer else bytes(pkt)[:n.value]
 
     def __del__(self):
         try:

@@ -40,7 +40,9 @@ def build(force: bool = False) -> None:
         os.path.getmtime(ORACLE_SO) < os.path.getmtime(os.path.join(_HERE, "rs_oracle.c"))
     ):
         subprocess.check_call(["make", "-s", "-C", _HERE, os.path.join(_HERE, "liboracle.so")])
-    if os.path.isdir("/root/reference/src/3rd_party") and (force or not os.path.exists(REF_SO)):
+    if os.path.isdir("/root/reference/src/3rd_party") and (
+            force or not os.path.exists(REF_SO)
+            or os.path.getmtime(REF_SO) < os.path.getmtime(os.path.join(_HERE, "ref_shim.cpp"))):
         subprocess.check_call(["make", "-s", "-C", _HERE, "ref"])
 
 

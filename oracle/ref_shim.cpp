@@ -9,6 +9,7 @@
 // Reference interface wrapped: fecpp.hpp:36-81 (constructor, reset_martix, encode, decode).
 #include "fecpp.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -192,6 +193,53 @@ double ref_bench_roundtrip(size_t K, size_t N, size_t B, size_t G, size_t pool, 
         *recovered_out = tot;
     }
     return (double)(G * passes) * (double)(K * B) / secs;
+}
+
+// Per-call latency of ONE group on the calling thread (tools/latency_bench.cpp's reference leg): one fec_code
+// built before timing, the same group every call (warm caches, as a live KCP updater thread coding its
+// connection's groups), encode, then decode with the first `lost` data shares missing (the map holds the other
+// data shares and `lost` parity shares, as fec_find_missings builds it, client.cpp:895-938).
+// us[0..5] = encode mean / p50 / p90, decode mean / p50 / p90 (microseconds).  Returns 0, or -1 on a wrong result.
+int ref_percall_latency(size_t K, size_t N, size_t B, size_t lost, int reps, double *us)
+{
+    using clk = std::chrono::steady_clock;
+    fecpp::fec_code c(K, N);
+    std::vector<uint8_t> data(K * B);
+    for (size_t i = 0; i < data.size(); ++i) data[i] = (uint8_t)smix(i);
+    auto red = c.encode(data.data(), K * B, B);
+    if (red.size() != N - K || lost > N - K) return -1;
+    std::map<size_t, const uint8_t *> shares;
+    for (size_t s = lost; s < K; ++s) shares[s] = data.data() + s * B;
+    for (size_t r = 0; r < lost; ++r) shares[K + r] = red[r].get();
+    auto stats = [&](std::vector<double> &v, double *o) {
+        double sum = 0;
+        for (double x : v) sum += x;
+        std::sort(v.begin(), v.end());
+        o[0] = sum / v.size();
+        o[1] = v[v.size() / 2];
+        o[2] = v[v.size() * 9 / 10];
+    };
+    std::vector<double> te(reps), td(reps);
+    size_t sink = 0;
+    for (int i = 0; i < 50; ++i) sink += c.encode(data.data(), K * B, B).size() + c.decode(shares, B).size();
+    for (int i = 0; i < reps; ++i) {
+        const auto t0 = clk::now();
+        auto p = c.encode(data.data(), K * B, B);
+        te[i] = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+        sink += p.size();
+    }
+    for (int i = 0; i < reps; ++i) {
+        const auto t0 = clk::now();
+        auto m = c.decode(shares, B);
+        td[i] = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+        sink += m.size();
+    }
+    auto m = c.decode(shares, B);
+    for (size_t t = 0; t < lost; ++t)
+        if (!m.count(t) || std::memcmp(m[t].data(), data.data() + t * B, B)) return -1;
+    stats(te, us);
+    stats(td, us + 3);
+    return sink ? 0 : -1;
 }
 
 }  // extern "C"

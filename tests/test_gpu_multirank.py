@@ -33,9 +33,11 @@ def _last_json(stdout: str) -> dict:
     raise AssertionError("no JSON line in:\n" + stdout[-2000:])
 
 
-def _run(cmd, parts):
-    env = dict(os.environ, KFEC_BENCH_DIGEST=str(parts), HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+def _run(cmd, parts, rehearsal=True, timeout=240):
+    # the box has one GPU: several ranks on it is a rehearsal, which bench.py refuses unless told so
+    env = dict(os.environ, KFEC_BENCH_DIGEST=str(parts), HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1",
+               KFEC_BENCH_REHEARSAL="1" if rehearsal else "0")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, f"rc={r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
     return _last_json(r.stdout)
 
@@ -51,7 +53,9 @@ def test_bench_two_ranks_match_single_rank(config):
                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
                 "--groups", str(per_gpu)] + common, parts=2)
     one = _run([sys.executable, "bench.py", "--gpus", "1", "--groups", str(2 * per_gpu)] + common, parts=2)
-    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    n_dev = torch.cuda.device_count()
+    assert two["n_gpus"] == min(2, n_dev) and one["n_gpus"] == 1  # n_gpus counts devices, not ranks
+    assert two["config"]["ranks"] == 2 and two["config"]["rehearsal"] == (n_dev < 2)
     assert two["verified_bit_exact"] and one["verified_bit_exact"]
     assert two["config"]["global_groups"] == one["config"]["global_groups"] == 2 * per_gpu
     assert two["recovered_shards_per_step"] == one["recovered_shards_per_step"] > 0
@@ -68,6 +72,36 @@ def test_bench_gpus_flag_spawns_the_ranks_itself():
     common = ["--config", "20:3", "--no-cpu", "--steps", "2", "--warmup", "1"]
     two = _run([sys.executable, "bench.py", "--gpus", "2", "--groups", "4096"] + common, parts=2)
     one = _run([sys.executable, "bench.py", "--gpus", "1", "--groups", "8192"] + common, parts=2)
-    assert two["n_gpus"] == 2 and two["verified_bit_exact"]
+    assert two["config"]["ranks"] == 2 and two["verified_bit_exact"]
+    assert two["n_gpus"] == min(2, torch.cuda.device_count())
     assert two["config"]["global_groups"] == 8192
     assert two["combined_digest"] == one["combined_digest"]
+
+
+def test_bench_eight_ranks_match_single_rank():
+    """Config 5's partition (BASELINE configs[4]: 8 ranks, independent group ranges, no collective) rehearsed on
+    the box's GPU(s): `bench.py --gpus 8` with 2048 groups per rank must verify bit-exact and give the same
+    combined digest (KFEC_BENCH_DIGEST=8, one SHA-256 per rank's range) as one rank over all 16384 groups."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    common = ["--config", "20:3", "--no-cpu", "--steps", "2", "--warmup", "1"]
+    eight = _run([sys.executable, "bench.py", "--gpus", "8", "--groups", "2048"] + common, parts=8, timeout=300)
+    one = _run([sys.executable, "bench.py", "--gpus", "1", "--groups", "16384"] + common, parts=8)
+    assert eight["verified_bit_exact"] and one["verified_bit_exact"]
+    assert eight["config"]["ranks"] == 8 and eight["n_gpus"] == min(8, torch.cuda.device_count())
+    assert eight["config"]["global_groups"] == one["config"]["global_groups"] == 16384
+    assert eight["recovered_shards_per_step"] == one["recovered_shards_per_step"] == 3 * 16384
+    assert eight["combined_digest"] == one["combined_digest"]
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """Without the rehearsal flag, more ranks than visible GPUs is an error (exit 2) before any device work."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n = torch.cuda.device_count()
+    env = dict(os.environ, KFEC_BENCH_REHEARSAL="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n + 1), "--groups", "64", "--no-cpu", "--steps", "1",
+                        "--warmup", "0"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 2 and "visible GPU" in r.stderr

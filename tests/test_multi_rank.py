@@ -139,3 +139,21 @@ def test_bench_rank_groups_partition_the_global_space():
             for (a, b, _), (c, d, _) in zip(spans, spans[1:]):
                 assert b == c
             assert all(b - a == per_gpu for a, b, _ in spans)
+
+
+def test_bench_refuses_oversubscription_without_rehearsal():
+    """More ranks than visible GPUs is refused (exit 2) before the rendezvous, unless the run says it is a
+    rehearsal; n_gpus then counts devices.  (CPU: no GPU is visible, so even one rank is refused.)"""
+    import subprocess
+    import sys
+    import bench
+    assert bench.check_devices(8, 8, False) is None
+    assert bench.check_devices(2, 8, False) is None
+    assert "only 1 visible GPU" in bench.check_devices(8, 1, False)
+    assert bench.check_devices(8, 1, True) is None
+    assert bench.check_devices(1, 0, True) == "no GPU visible"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", KFEC_BENCH_REHEARSAL="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--no-cpu"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "bench.py:" in r.stderr

@@ -2,11 +2,17 @@
 // kfec_encode / kfec_decode on ONE fec=20:3 group from host memory (what fecpp_compat.hpp's fec_code::encode /
 // decode do per call), and kfec_txq_flush / kfec_rxq_flush of small batches (1 .. 1024 groups), each timed
 // over many calls on one host thread.  Prints one JSON line (microseconds per call).
+// The reference leg: the reference's own coder (oracle/_ref/libfecpp_ref.so, built from /root/reference's
+// fecpp*.cpp by oracle/Makefile; measurement only, loaded with dlopen at run time, never linked) times the same
+// single-group encode and 3-loss decode on the same thread in the same run (ref_* keys).
 // Build: g++ -O2 -std=c++17 -I include tools/latency_bench.cpp -o tools/latency_bench -L kcptube_amd -lkfec
 //        -Wl,-rpath,'$ORIGIN/../kcptube_amd'
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -74,6 +80,22 @@ int main()
     js += pct("kfec_decode_1_group_3_lost", reps,
               [&] { kfec_decode(ctx, ids.data(), ptrs.data(), ids.size(), B, out_ids, out.data(), &n_out); });
     js += ", \"worker_requests\": " + std::to_string(kfec_worker_requests());
+    // the reference coder on this thread, same group shape, same run
+    {
+        std::string so = "oracle/_ref/libfecpp_ref.so";
+        if (const char *e = getenv("KFEC_REF_SO")) so = e;
+        void *h = dlopen(so.c_str(), RTLD_NOW | RTLD_LOCAL);
+        using lat_fn = int (*)(size_t, size_t, size_t, size_t, int, double *);
+        lat_fn lat = h ? reinterpret_cast<lat_fn>(dlsym(h, "ref_percall_latency")) : nullptr;
+        double us[6];
+        if (lat && lat(K, N, B, 3, reps, us) == 0) {
+            js += ", \"ref_encode_us\": " + std::to_string(us[0]) + ", \"ref_encode_p50_us\": " + std::to_string(us[1]) +
+                  ", \"ref_encode_p90_us\": " + std::to_string(us[2]) + ", \"ref_decode_us\": " + std::to_string(us[3]) +
+                  ", \"ref_decode_p50_us\": " + std::to_string(us[4]) + ", \"ref_decode_p90_us\": " + std::to_string(us[5]);
+        } else {
+            js += ", \"ref_error\": \"" + std::string(h ? "ref_percall_latency failed" : "libfecpp_ref.so not found") + "\"";
+        }
+    }
     bool ok = n_out == 3 && !std::memcmp(out.data(), data.data(), 3 * B);
     // per-call encode cost against K (N = K + 3, B = 1440): the slope is the per-share cost of the call
     for (size_t k : {1, 5, 10, 20}) {
