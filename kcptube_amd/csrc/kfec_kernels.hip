@@ -57,6 +57,10 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #ifndef KFEC_MINW
 #define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the MAC kernels
 #endif
+#ifndef KFEC_DEC_TTAB
+#define KFEC_DEC_TTAB 1  // coefficient-form decode (R > 8): LDS entries point into one table of all 256 coefficients'
+                         // perm tables (1) instead of holding each coefficient's expanded tables (0; A/B knob)
+#endif
 
 // ---------------------------------------------------------------------------------------------------
 // small device helpers
@@ -715,16 +719,24 @@ struct Gran {
     uint32_t d[W];
 };
 
+// Shares are always in global memory (HBM, or pinned host memory mapped into the device's address space), so
+// the loads go through global-address-space pointers: a share pointer read back from LDS (the decode's
+// entries) would otherwise become a flat load, which also counts on lgkmcnt -- every wait for an LDS read
+// (the next shard's tables) then also waited for the shard loads in flight.
+typedef unsigned int gx4_t __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) gx4_t gu4;
+typedef const __attribute__((address_space(1))) uint32_t gu32;
+
 template <int VEC>
 __device__ __forceinline__ Gran<VEC> load_gran(const uint8_t *p, uint32_t col, uint32_t B)
 {
     Gran<VEC> v;
     if constexpr (VEC == 32) {
-        const uint4 x = reinterpret_cast<const uint4 *>(p)[0], y = reinterpret_cast<const uint4 *>(p)[1];
+        const gx4_t x = ((gu4 *)p)[0], y = ((gu4 *)p)[1];
         v.d[0] = x.x; v.d[1] = x.y; v.d[2] = x.z; v.d[3] = x.w;
         v.d[4] = y.x; v.d[5] = y.y; v.d[6] = y.z; v.d[7] = y.w;
     } else if constexpr (VEC == 4) {
-        v.d[0] = *reinterpret_cast<const uint32_t *>(p);
+        v.d[0] = *(gu32 *)p;
     } else {  // bytewise: 4 bytes at p, only those below B
         static_assert(VEC == 1, "granule");
         uint32_t x = 0;
@@ -777,6 +789,15 @@ struct MacLayout {
     static constexpr int TBL_DW = ((5 * MT + 3) / 4) * 4;  // table dwords per (group, shard): 5 per row
     static constexpr int ENTRY = 16 + 4 * TBL_DW;          // + 8-byte share pointer, 8 pad
 };
+
+// Coefficient-form decode entries (KFEC_DEC_TTAB): the workgroup's LDS starts with T, the perm tables of all 256
+// coefficient values (8-dword stride, built once per workgroup); an entry per (group slot, shard) is the share
+// pointer and, per output row of the tile, the byte offset of its coefficient's table in T (u16).  An entry is
+// 24 bytes instead of 16 + 40 * 4, so every shard of a workgroup's groups fits one expansion (fec=200:55,
+// B=1440: 7 groups x 200 shards, 33.6 KB): one global-load round trip and one barrier per workgroup instead of
+// one per 26-shard chunk, and no per-entry table construction.
+constexpr int kDecEntry = 24;
+constexpr uint32_t kTBytes = 256 * 32;
 
 // Workgroup b -> (column chunk, row tile).  With R > MT the tiles of one column chunk are numbered
 // b, b+8, b+16, ...: the dispatcher deals workgroups round-robin over the 8 XCDs, so those run back to back
@@ -851,6 +872,60 @@ __device__ __forceinline__ void mac_expand(const MacArgs &a, uint8_t *s_ent, uin
     }
 }
 
+// T: gf_perm_tables(c) at s_T + 32 c for every byte c (no barrier: the caller's follows)
+__device__ __forceinline__ void dec_build_t(uint8_t *s_T)
+{
+    for (uint32_t c = threadIdx.x; c < 256; c += blockDim.x) {
+        uint32_t t[5];
+        gf_perm_tables(c, t);
+        uint32_t *d = reinterpret_cast<uint32_t *>(s_T + c * 32);
+        *reinterpret_cast<uint4 *>(d) = uint4{t[0], t[1], t[2], t[3]};
+        d[4] = t[4];
+    }
+}
+
+// entries of shards [c0, c0 + nj) for group slots [0, ng): share pointer + MT u16 offsets into T
+template <int MT>
+__device__ __forceinline__ void dec_expand(const MacArgs &a, uint8_t *s_ent, uint32_t gfirst, uint32_t ng, uint32_t c0,
+                                           uint32_t nj, uint32_t row0)
+{
+    static_assert(MT == 8, "entry: 8 offsets");
+    const uint32_t items = ng * nj, K4 = (a.K + 3) & ~3u;
+    constexpr int EB = 4;  // entries per thread whose loads are issued together
+    for (uint32_t e0 = 0; e0 < items; e0 += EB * blockDim.x) {
+        uint32_t hd[EB], sv[EB], cv[EB][MT];
+#pragma unroll
+        for (int b = 0; b < EB; ++b) {
+            const uint32_t e = min(e0 + b * blockDim.x + threadIdx.x, items - 1);  // clamped: loads unconditional
+            const uint32_t jj = e % nj, gs = e / nj, j = c0 + jj;
+            const uint8_t *rec = a.rec + (uint64_t)(gfirst + gs) * a.rec_stride;
+            hd[b] = *reinterpret_cast<const uint16_t *>(rec);  // status | m << 8
+            sv[b] = rec[4 + j];
+#pragma unroll
+            for (int r = 0; r < MT; ++r) cv[b][r] = rec[4 + K4 + min(row0 + r, a.R - 1) * K4 + j];
+        }
+#pragma unroll
+        for (int b = 0; b < EB; ++b) {
+            const uint32_t e = e0 + b * blockDim.x + threadIdx.x;
+            if (e >= items) break;
+            const uint32_t jj = e % nj, gs = e / nj;
+            const uint64_t g = gfirst + gs;
+            const uint32_t src = sv[b];
+            const uint8_t *p = (src < a.K) ? a.data + (g * a.K + src) * a.pitch : a.parity + (g * a.R + (src - a.K)) * a.pitch;
+            uint8_t *ent = s_ent + (gs * a.JC + jj) * kDecEntry;
+            *reinterpret_cast<const uint8_t **>(ent) = p;
+            const bool ok = (hd[b] & 0xFFu) == 0;
+            const uint32_t m = hd[b] >> 8;
+            uint32_t o[MT];
+#pragma unroll
+            for (int r = 0; r < MT; ++r) o[r] = (ok && row0 + r < m) ? cv[b][r] * 32u : 0u;  // T[0] = zero tables
+            uint32_t *ow = reinterpret_cast<uint32_t *>(ent + 8);
+#pragma unroll
+            for (int r = 0; r < MT; r += 2) ow[r / 2] = o[r] | (o[r + 1] << 16);
+        }
+    }
+}
+
 // One lane = one (group, V-byte column) item; consecutive lanes take consecutive columns and wrap into the
 // next group, so a wave-instruction reads 2 KiB of one shard row (V = 32).  One workgroup per 256 items
 // (non-persistent grid: the dispatcher refills each CU as workgroups retire).  Per lane: K loads of V bytes
@@ -874,10 +949,13 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     const uint32_t row0 = tile * MT;
     const uint32_t K = a.K, cols = a.cols;
     const bool enc_once = !DEC && K <= a.JC;
+    constexpr bool ttab = DEC && KFEC_DEC_TTAB && MT == 8;
+    uint8_t *s_E = ttab ? s_ent + kTBytes : s_ent;  // entries (after T)
     if (enc_once) {
         mac_expand<MT, false>(a, s_ent, 0, 1, 0, K, row0);
         __syncthreads();
     }
+    if constexpr (ttab) dec_build_t(s_ent);  // (ordered by the first chunk's barrier below)
     const uint32_t item = base + threadIdx.x;
     const bool in = item < a.total;
     const uint32_t g = in ? item / cols : 0;
@@ -908,26 +986,51 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     for (uint32_t c0 = 0; c0 < K; c0 += a.JC) {
         const uint32_t nj = min(a.JC, K - c0);
         if (!enc_once) {
-            __syncthreads();
-            mac_expand<MT, DEC>(a, s_ent, gfirst, DEC ? ng : 1u, c0, nj, row0);
+            if (!ttab || c0 > 0) __syncthreads();  // (ttab: nothing to protect before the first chunk)
+            if constexpr (ttab) dec_expand<MT>(a, s_E, gfirst, ng, c0, nj, row0);
+            else mac_expand<MT, DEC>(a, s_ent, gfirst, DEC ? ng : 1u, c0, nj, row0);
             __syncthreads();
         }
         if (rows == 0) continue;
-        const uint8_t *ent0 = s_ent + (gs * a.JC) * L::ENTRY;
+        constexpr uint32_t ENT = ttab ? kDecEntry : L::ENTRY;
+        const uint8_t *ent0 = s_E + (gs * a.JC) * ENT;
         auto share_ptr = [&](uint32_t jj) -> const uint8_t * {
             if constexpr (DEC) {
-                return *reinterpret_cast<const uint8_t *const *>(ent0 + jj * L::ENTRY) + off;
+                return *reinterpret_cast<const uint8_t *const *>(ent0 + jj * ENT) + off;
             } else {
                 return enc_base + (uint64_t)(c0 + jj) * a.pitch;
             }
         };
+        // ttab: the T offsets of a shard are read one shard ahead (ofs_lo / ofs_hi), so the table reads of the
+        // shard being multiplied depend on no LDS read still in flight
+        uint64_t ofs_lo = 0, ofs_hi = 0;
+        auto read_ofs = [&](uint32_t jj) {
+            if constexpr (ttab) {
+                const uint64_t *q = reinterpret_cast<const uint64_t *>(ent0 + min(jj, nj - 1) * ENT + 8);
+                ofs_lo = q[0];
+                ofs_hi = q[1];
+            }
+        };
         auto mac = [&](const Gran<VEC> &cur, uint32_t jj) {
-            const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + jj * L::ENTRY + 16);
             uint32_t t[L::TBL_DW];
+            if constexpr (ttab) {
+                const uint64_t lo = ofs_lo, hi = ofs_hi;
+                read_ofs(jj + 1);
 #pragma unroll
-            for (int i = 0; i < L::TBL_DW / 4; ++i) {
-                const uint4 q = tv[i];
-                t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+                for (int r = 0; r < MT; ++r) {
+                    const uint32_t o = (uint32_t)((r < 4 ? lo : hi) >> (16 * (r & 3))) & 0xFFFFu;
+                    const uint8_t *te = s_ent + o;
+                    const uint4 q = *reinterpret_cast<const uint4 *>(te);
+                    t[5 * r] = q.x; t[5 * r + 1] = q.y; t[5 * r + 2] = q.z; t[5 * r + 3] = q.w;
+                    t[5 * r + 4] = *reinterpret_cast<const uint32_t *>(te + 16);
+                }
+            } else {
+                const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + jj * ENT + 16);
+#pragma unroll
+                for (int i = 0; i < L::TBL_DW / 4; ++i) {
+                    const uint4 q = tv[i];
+                    t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
+                }
             }
 #pragma unroll
             for (int w = 0; w < W; ++w) {
@@ -944,6 +1047,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
         Gran<VEC> x[PD];
 #pragma unroll
         for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min((uint32_t)u, nj - 1)), col, a.B);
+        read_ofs(0);
         uint32_t jb = 0;
         for (; jb + PD <= nj; jb += PD) {
 #pragma unroll
@@ -1361,7 +1465,7 @@ template <int VEC, int MT, bool DEC, int PDX = 0>
 static int run_mac(MacArgs a, hipStream_t s)
 {
     using L = MacLayout<MT>;
-    const size_t lds = (size_t)a.gmax * a.JC * L::ENTRY;
+    const size_t lds = (DEC && KFEC_DEC_TTAB && MT == 8) ? kTBytes + (size_t)a.gmax * a.JC * kDecEntry : (size_t)a.gmax * a.JC * L::ENTRY;
     const uint32_t chunks = (a.total + kMacBlock - 1) / kMacBlock;
     const uint32_t nb = a.tiles > 1 ? ((chunks + 7) & ~7u) * a.tiles : chunks;
     hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), lds, s, a);
@@ -1462,6 +1566,7 @@ static int dispatch_syn(int vec, int rt, SynArgs a, size_t lds, int cus, hipStre
 }
 
 static constexpr size_t kLdsBudget = 32 * 1024;
+static constexpr size_t kDecLdsBudget = 40 * 1024;  // T-table decode entries (+ 8 KiB of T): 3 workgroups per CU
 static constexpr size_t kSynLdsMax = 64 * 1024;
 static constexpr size_t kMaxItemsPerLaunch = 0x7FFFFFFFu;
 
@@ -1628,7 +1733,8 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     const size_t ent = entry_bytes(mt);
     return for_group_ranges(G, cols, tiles, [&](size_t g0, size_t gn) {
         const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kMacBlock - 1) / cols + 2);
-        const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
+        const uint32_t JC = (KFEC_DEC_TTAB && mt == 8) ? (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kDecLdsBudget / (kDecEntry * gmax)))
+                                          : (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
         MacArgs a{};
         a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
         a.parity = static_cast<const uint8_t *>(d_parity) + g0 * R * pitch;
