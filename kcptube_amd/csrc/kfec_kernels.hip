@@ -950,12 +950,13 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     const uint32_t K = a.K, cols = a.cols;
     const bool enc_once = !DEC && K <= a.JC;
     constexpr bool ttab = DEC && KFEC_DEC_TTAB && MT == 8;
+    uint8_t *s_T = s_ent;
     uint8_t *s_E = ttab ? s_ent + kTBytes : s_ent;  // entries (after T)
     if (enc_once) {
         mac_expand<MT, false>(a, s_ent, 0, 1, 0, K, row0);
         __syncthreads();
     }
-    if constexpr (ttab) dec_build_t(s_ent);  // (ordered by the first chunk's barrier below)
+    if constexpr (ttab) dec_build_t(s_T);  // (ordered by the first chunk's barrier below)
     const uint32_t item = base + threadIdx.x;
     const bool in = item < a.total;
     const uint32_t g = in ? item / cols : 0;
@@ -1019,7 +1020,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
 #pragma unroll
                 for (int r = 0; r < MT; ++r) {
                     const uint32_t o = (uint32_t)((r < 4 ? lo : hi) >> (16 * (r & 3))) & 0xFFFFu;
-                    const uint8_t *te = s_ent + o;
+                    const uint8_t *te = s_T + o;
                     const uint4 q = *reinterpret_cast<const uint4 *>(te);
                     t[5 * r] = q.x; t[5 * r + 1] = q.y; t[5 * r + 2] = q.z; t[5 * r + 3] = q.w;
                     t[5 * r + 4] = *reinterpret_cast<const uint32_t *>(te + 16);

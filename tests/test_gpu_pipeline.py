@@ -310,6 +310,28 @@ def test_cpp_program_over_the_pipeline_header(dev):
     assert r["bad"] == 0 and r["recovered"] == r["recovered_expected"] == 2 * 512 * 3 * 3
 
 
+@pytest.mark.parametrize("seal", ["none", "chacha20"])
+def test_cpp_program_sealed_deferred_pipeline(dev, seal):
+    """tools/pipeline_bench.cpp with PB_SEAL: the sealed queue from C++ as the header documents it -- kfec_tx_send
+    with pkt = NULL and pkt_len = NULL under KFEC_TXQ_DEFER_DATA, every packet sealed by the flush, opened on the
+    device by kfec_opener and pushed into kfec_rx -- 4096 groups per flush, every lost datagram back bit-exact.
+    The host cost of a deferred send stays flat with the flush size (it was quadratic: the staged-packet table
+    grew by one element per send)."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "pipeline_bench")
+    if not os.path.exists(exe):
+        pytest.skip("tools/pipeline_bench not built (kcptube_amd.build.build_tools)")
+    p = subprocess.run([exe, "20", "23", "1440", "4096", "3", "3", "1"], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PB_SEAL=seal))
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["seal"] == seal and r["bad"] == 0 and r["recovered"] == r["recovered_expected"] == 4096 * 3 * 3
+    assert r["tx_host_ns_per_packet"] < 2000, r  # ~150 ns measured; 15 us per packet when it was quadratic
+    assert 0 < r["data_pkt_delay_us_p50"] <= r["data_pkt_delay_us_p99"]
+
+
 _SEAL_MODES = {"none": 0, "plain_xor": 1}
 
 
