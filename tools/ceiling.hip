@@ -38,6 +38,19 @@ __global__ void __launch_bounds__(256) read_chunk(const uint8_t *a, uint8_t *sin
 }
 
 template <int U>
+__global__ void __launch_bounds__(256) read_chunk_nt(const uint8_t *a, uint8_t *sink)
+{
+    const uint8_t *p = a + ((size_t)blockIdx.x * U * 256 + threadIdx.x) * 16;
+    u32x4 v[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p + (size_t)i * 4096));
+    u32x4 acc = v[0];
+#pragma unroll
+    for (int i = 1; i < U; ++i) acc ^= v[i];
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) st16(sink, acc, false);
+}
+
+template <int U>
 __global__ void __launch_bounds__(256) write_chunk(uint8_t *b, bool nt)
 {
     uint8_t *p = b + ((size_t)blockIdx.x * U * 256 + threadIdx.x) * 16;
@@ -75,6 +88,26 @@ __global__ void __launch_bounds__(256) enc_lin(const uint8_t *d, uint8_t *par, b
     if (threadIdx.x < 14) st16(o + (256 + threadIdx.x) * 16, acc, nt);
 }
 
+// enc_lin with nontemporal loads (NTL) and optionally nt stores: the whole group is one contiguous read
+template <bool NTL>
+__global__ void __launch_bounds__(256) enc_lin_ntl(const uint8_t *d, uint8_t *par, bool nt)
+{
+    const uint8_t *p = d + (size_t)blockIdx.x * 28800;
+    u32x4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const unsigned q = i * 256 + threadIdx.x;
+        const unsigned qq = q < 1800 ? q : 1799;  // (clamped: no branch around the load)
+        v[i] = NTL ? __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p + qq * 16)) : ld16(p + qq * 16);
+    }
+    u32x4 acc = v[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) acc ^= v[i];
+    uint8_t *o = par + (size_t)blockIdx.x * 4320;
+    st16(o + threadIdx.x * 16, acc, nt);
+    if (threadIdx.x < 14) st16(o + (256 + threadIdx.x) * 16, acc, nt);
+}
+
 // one wave per group, 4 groups per workgroup
 __global__ void __launch_bounds__(256) enc_lin_wave(const uint8_t *d, uint8_t *par, unsigned G, bool nt)
 {
@@ -97,6 +130,56 @@ __global__ void __launch_bounds__(256) enc_lin_wave(const uint8_t *d, uint8_t *p
     for (int i = 0; i < 5; ++i) {
         const unsigned q = i * 64 + l;
         if (q < 270) st16(o + q * 16, acc, nt);
+    }
+}
+
+__device__ __forceinline__ u32x4 ld16nt(const uint8_t *p) { return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p)); }
+
+// the flattened encode's traffic with nontemporal loads: V = 32 as the shipped kernel (lane l: bytes [32l, 32l+32),
+// two 16-B loads 16 B apart), V = 16 (one 16-B load per lane: every wave-instruction reads 1 KB contiguous),
+// V = 32 split (lane l: 16-B columns l and l + 64 of its wave's 2 KB: two loads, each 1 KB contiguous per wave)
+template <int V, int PD, bool SPLIT>
+__global__ void __launch_bounds__(256) enc_cols_ntl(const uint8_t *d, uint8_t *par, unsigned total16, unsigned cols16, bool nt)
+{
+    constexpr int NV = V / 16;
+    // item space in 16-B columns; a wave owns 64 * NV consecutive columns
+    const unsigned wave0 = (blockIdx.x * 256 + (threadIdx.x & ~63u)) * NV, l = threadIdx.x & 63u;
+    unsigned it[NV];
+#pragma unroll
+    for (int w = 0; w < NV; ++w) it[w] = SPLIT ? wave0 + w * 64 + l : wave0 + l * NV + w;
+    const uint8_t *p[NV];
+    bool in[NV];
+#pragma unroll
+    for (int w = 0; w < NV; ++w) {
+        in[w] = it[w] < total16;
+        const unsigned g = in[w] ? it[w] / cols16 : 0, c = in[w] ? it[w] - g * cols16 : 0;
+        p[w] = d + (size_t)g * 28800 + c * 16;
+    }
+    u32x4 acc[NV];
+#pragma unroll
+    for (int w = 0; w < NV; ++w) acc[w] = u32x4{0, 0, 0, 0};
+    u32x4 x[PD][NV];
+#pragma unroll
+    for (int u = 0; u < PD; ++u)
+#pragma unroll
+        for (int w = 0; w < NV; ++w) x[u][w] = ld16nt(p[w] + u * 1440);
+#pragma unroll
+    for (int j = 0; j < 20; ++j) {
+        const int u = j % PD;
+#pragma unroll
+        for (int w = 0; w < NV; ++w) {
+            const u32x4 cur = x[u][w];
+            if (j + PD < 20) x[u][w] = ld16nt(p[w] + (j + PD) * 1440);
+            acc[w] ^= cur;
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < NV; ++w) {
+        if (!in[w]) continue;
+        const unsigned g = it[w] / cols16, c = it[w] - g * cols16;
+        uint8_t *o = par + (size_t)g * 4320 + c * 16;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) st16(o + r * 1440, acc[w] + (u32x4){(unsigned)r, 0, 0, 0}, nt);
     }
 }
 
@@ -172,6 +255,8 @@ int main(int argc, char **argv)
     run("read_chunk<4>", nr4 * 4.0 * 4096, [&] { read_chunk<4><<<nr4, 256>>>(a, sink); });
     run("read_chunk<8>", nr8 * 8.0 * 4096, [&] { read_chunk<8><<<nr8, 256>>>(a, sink); });
     run("read_chunk<16>", nr16 * 16.0 * 4096, [&] { read_chunk<16><<<nr16, 256>>>(a, sink); });
+    run("read_chunk_nt<8>", nr8 * 8.0 * 4096, [&] { read_chunk_nt<8><<<nr8, 256>>>(a, sink); });
+    run("read_chunk_nt<16>", nr16 * 16.0 * 4096, [&] { read_chunk_nt<16><<<nr16, 256>>>(a, sink); });
     run("write_chunk<4>", nw4 * 4.0 * 4096, [&] { write_chunk<4><<<nw4, 256>>>(b, false); });
     run("write_chunk<8>", nw8 * 8.0 * 4096, [&] { write_chunk<8><<<nw8, 256>>>(b, false); });
     run("write_chunk<8> nt", nw8 * 8.0 * 4096, [&] { write_chunk<8><<<nw8, 256>>>(b, true); });
@@ -181,6 +266,9 @@ int main(int argc, char **argv)
     const double enc = (double)G * (28800 + 4320);
     run("enc_lin (WG/group)", enc, [&] { enc_lin<<<G, 256>>>(a, b, false); });
     run("enc_lin (WG/group) nt", enc, [&] { enc_lin<<<G, 256>>>(a, b, true); });
+    run("enc_lin_ntl<0> nt-st", enc, [&] { enc_lin_ntl<false><<<G, 256>>>(a, b, true); });
+    run("enc_lin_ntl<1> nt-st", enc, [&] { enc_lin_ntl<true><<<G, 256>>>(a, b, true); });
+    run("enc_lin_ntl<1>", enc, [&] { enc_lin_ntl<true><<<G, 256>>>(a, b, false); });
     run("enc_lin_wave", enc, [&] { enc_lin_wave<<<G / 4, 256>>>(a, b, G, false); });
     run("enc_lin_wave nt", enc, [&] { enc_lin_wave<<<G / 4, 256>>>(a, b, G, true); });
     const unsigned t16 = G * 90, t32 = G * 45;
@@ -192,6 +280,14 @@ int main(int argc, char **argv)
         run(nm, enc, [&] { enc_cols<32, 2><<<cus * occ, 256>>>(a, b, t32, 45, true); });
         snprintf(nm, 64, "enc_cols<32,4> occ%d nt", occ);
         run(nm, enc, [&] { enc_cols<32, 4><<<cus * occ, 256>>>(a, b, t32, 45, true); });
+    }
+    {
+        const unsigned tot16 = G * 90, nb16 = (tot16 + 255) / 256, nb32 = (tot16 + 511) / 512;
+        run("enc_cols_ntl<16,4>", enc, [&] { enc_cols_ntl<16, 4, false><<<nb16, 256>>>(a, b, tot16, 90, true); });
+        run("enc_cols_ntl<32,4> (as shipped)", enc, [&] { enc_cols_ntl<32, 4, false><<<nb32, 256>>>(a, b, tot16, 90, true); });
+        run("enc_cols_ntl<32,4> split", enc, [&] { enc_cols_ntl<32, 4, true><<<nb32, 256>>>(a, b, tot16, 90, true); });
+        run("enc_cols_ntl<16,8>", enc, [&] { enc_cols_ntl<16, 8, false><<<nb16, 256>>>(a, b, tot16, 90, true); });
+        run("enc_cols_ntl<32,2> split", enc, [&] { enc_cols_ntl<32, 2, true><<<nb32, 256>>>(a, b, tot16, 90, true); });
     }
     run("enc_cols<16,4> nonpersist nt", enc, [&] { enc_cols<16, 4><<<(t16 + 255) / 256, 256>>>(a, b, t16, 90, true); });
     run("enc_cols<32,2> nonpersist nt", enc, [&] { enc_cols<32, 2><<<(t32 + 255) / 256, 256>>>(a, b, t32, 45, true); });
