@@ -19,8 +19,11 @@ Also reported (rank 0):
   roofline      the dominant kernel (the encode MAC launch; decode for decode-only configs) from HIP events
                 on its stream, plus the whole step (encode + decode algorithmic bytes / ms_per_step) as total
                 and read-only fractions of the 8 TB/s spec AND of this box's measured linear-read ceiling
-                (tools/libkfec_calib.so, timed in the same run); for fec=200:55 (VALU-bound) the byte-MAC
-                rate against the measured GF-MAC VALU ceiling of the same instruction mix.
+                (tools/libkfec_calib.so, timed in the same run), and against the "mix ceiling": the same
+                launch's reads + writes per group in their ideal streaming form (one workgroup per group,
+                contiguous 16-B loads, nt stores, no GF arithmetic), timed in the same run; for fec=200:55
+                (VALU-bound) the byte-MAC rate against the measured GF-MAC VALU ceiling of the same
+                instruction mix.
   cpu_baseline  the reference coder (oracle/_ref, compiled from the reference's own sources) on all usable
                 host cores over >= 64k distinct groups (rank 0, N = 1 only).
 """
@@ -175,6 +178,8 @@ class Calib:
             self.lib.calib_issue.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
             self.lib.calib_issue_instructions.argtypes = [ctypes.c_uint32]
             self.lib.calib_issue_instructions.restype = ctypes.c_uint64
+            self.lib.calib_mix.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                           ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
 
     def _time(self, torch, launch, reps=5):
         s = torch.cuda.current_stream()
@@ -198,6 +203,21 @@ class Calib:
         n = buf.numel() * buf.element_size()
         ms = self._time(torch, lambda st: self.lib.calib_read(buf.data_ptr(), n, sink.data_ptr(), st))
         return None if ms is None else self.lib.calib_read_bytes(n) / (ms * 1e-3) / 1e9
+
+    def mix_ceiling(self, torch, src, dst, groups, rbytes, wbytes):
+        """GB/s of the ideal streaming form of a launch's byte mix: `groups` x (rbytes read contiguously from
+        src + wbytes written to dst), one workgroup per group, no GF arithmetic (tools/calib.hip mix_stream)."""
+        if not self.lib:
+            return None
+        r16, w16 = int(rbytes) // 16 * 16, int(round(wbytes / 16.0)) * 16
+        groups = min(int(groups), (src.numel() * src.element_size()) // r16,
+                     (dst.numel() * dst.element_size()) // max(w16, 1) if w16 else 1 << 62)
+        if groups <= 0 or r16 <= 0:
+            return None
+        sink = torch.zeros(16, dtype=torch.int32, device=src.device)
+        ms = self._time(torch, lambda st: self.lib.calib_mix(src.data_ptr(), dst.data_ptr(), groups, r16, w16,
+                                                            sink.data_ptr(), st))
+        return None if ms is None else groups * (r16 + w16) / (ms * 1e-3) / 1e9
 
     def gfmac_ceiling(self, torch, dev, cus):
         """Issue bound of the perm MAC on this box, byte-MACs/s: every SIMD issuing nothing but the
@@ -436,6 +456,12 @@ def main():
 
     calib = Calib()
     read_ceiling = calib.read_ceiling(torch, data) if rank == 0 else None
+    # the dominant launch's byte mix (per decoded / encoded group: reads, writes) in its ideal streaming form
+    if do_enc:
+        mix_r, mix_w, mix_g = K * B, R * B, G
+    else:
+        mix_r, mix_w, mix_g = K * B, (n_rec * B / n_dec if n_dec else 0), max(n_dec, 1)
+    mix_ceiling = calib.mix_ceiling(torch, data, out, mix_g, mix_r, mix_w) if rank == 0 and args.config != "200:55" else None
     roof = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),
@@ -447,7 +473,11 @@ def main():
             "read_ceiling": round(read_ceiling, 1) if read_ceiling else None,
             "step_frac_of_ceiling": round(step_gbs / read_ceiling, 4) if read_ceiling else None,
             "step_frac_read_of_ceiling": round(step_read_gbs / read_ceiling, 4) if read_ceiling else None,
-            "frac_of_ceiling": round(achieved / read_ceiling, 4) if read_ceiling else None}
+            "frac_of_ceiling": round(achieved / read_ceiling, 4) if read_ceiling else None,
+            # the same launch against the ideal streaming form of its own read + write mix (calib_mix)
+            "mix_ceiling": round(mix_ceiling, 1) if mix_ceiling else None,
+            "mix_ceiling_bytes_per_group": [mix_r, round(mix_w, 1)],
+            "frac_of_mix_ceiling": round(achieved / mix_ceiling, 4) if mix_ceiling else None}
     if args.config == "200:55" and rank == 0:
         # VALU-bound: byte-MACs per second of each kernel against the perm MAC's issue bound on this box
         cus = torch.cuda.get_device_properties(dev).multi_processor_count

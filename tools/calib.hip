@@ -4,6 +4,9 @@
 //   calib_read(p, bytes, stream)     linear 16-B-per-lane read of [p, p + bytes), one contiguous 16 KiB chunk
 //                                    per 256-lane workgroup (4 loads in flight per lane), non-persistent grid:
 //                                    the HBM read ceiling of this box (6.48 TB/s on r01 boxes).
+//   calib_mix(src, dst, groups, rbytes, wbytes, sink, stream)
+//                                    the ideal streaming form of a coder launch's byte mix (mix_stream below):
+//                                    what HBM gives the same reads + writes when nothing else is in the way.
 //   calib_issue(op, sink, blocks, stream)
 //                                    issue rate of one VALU instruction of the perm MAC (op 0 v_perm_b32,
 //                                    1 v_bitop3_b32, 2 v_xor_b32): 16 independent inline-asm chains per lane,
@@ -31,6 +34,29 @@ __global__ void __launch_bounds__(256) read_chunk4(const uint8_t *a, size_t nchu
     for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const u32x4 *>(p + (size_t)i * 4096);
     const u32x4 acc = v[0] ^ v[1] ^ v[2] ^ v[3];
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) sink[0] = acc.x;  // keeps the loads alive
+}
+
+// the ideal streaming form of a coder launch's byte mix: one 256-lane workgroup per group reads its rbytes
+// contiguously (16-B lanes, up to 8 loads in flight per lane), XORs them, writes wbytes contiguously (nt, as the
+// coder's stores).  Same bytes as the coder, no GF arithmetic, no column gather: the "mix ceiling".
+__global__ void __launch_bounds__(256) mix_stream(const uint8_t *src, uint8_t *dst, uint32_t rq, uint32_t wq, uint32_t *sink)
+{
+    const uint8_t *p = src + (size_t)blockIdx.x * rq * 16;
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint32_t q0 = 0; q0 < rq; q0 += 8 * 256) {
+        u32x4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t q = min(q0 + i * 256 + threadIdx.x, rq - 1);  // clamped: no branch around the loads
+            v[i] = *reinterpret_cast<const u32x4 *>(p + (size_t)q * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc ^= v[i];
+    }
+    uint8_t *o = dst + (size_t)blockIdx.x * wq * 16;
+    for (uint32_t q = threadIdx.x; q < wq; q += 256)
+        __builtin_nontemporal_store(acc + (u32x4){q, 0, 0, 0}, reinterpret_cast<u32x4 *>(o + (size_t)q * 16));
+    if ((acc.x ^ acc.y) == 0x9E3779B9u && wq == 0) sink[0] = acc.z;
 }
 
 constexpr int kIssueIters = 2048;
@@ -66,6 +92,15 @@ int calib_read(const void *p, size_t bytes, uint32_t *sink, void *stream)
     if (nchunks == 0 || nchunks > 0x7FFFFFFFu) return -1;
     hipLaunchKernelGGL(read_chunk4, dim3((uint32_t)nchunks), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const uint8_t *>(p), nchunks, sink);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// groups x (rbytes read + wbytes written), both multiples of 16, src / dst at least groups x rbytes / wbytes
+int calib_mix(const void *src, void *dst, size_t groups, size_t rbytes, size_t wbytes, uint32_t *sink, void *stream)
+{
+    if (groups == 0 || groups > 0x7FFFFFFFu || rbytes < 16 || rbytes % 16 || wbytes % 16) return -1;
+    hipLaunchKernelGGL(mix_stream, dim3((uint32_t)groups), dim3(256), 0, (hipStream_t)stream, static_cast<const uint8_t *>(src),
+                       static_cast<uint8_t *>(dst), (uint32_t)(rbytes / 16), (uint32_t)(wbytes / 16), sink);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

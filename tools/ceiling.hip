@@ -11,6 +11,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/ceiling tools/ceiling.hip
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -216,6 +217,65 @@ __global__ void __launch_bounds__(256) enc_cols(const uint8_t *d, uint8_t *par, 
     }
 }
 
+// shape study for any fec=K:R, B: the coder's column pattern (lane = (group, 32-B column), the K shards of
+// the column read PD in flight, R columns written) against the contiguous form (one workgroup per group reading
+// its K x B bytes in order, writing R x B), both XOR-only
+template <int PD>
+__global__ void __launch_bounds__(256) gen_cols(const uint8_t *d, uint8_t *par, unsigned total, unsigned cols, unsigned K,
+                                                unsigned R, unsigned B)
+{
+    const unsigned it = blockIdx.x * 256 + threadIdx.x;
+    if (it >= total) return;
+    const unsigned g = it / cols, c = it - g * cols;
+    const unsigned o = min(c * 32, ((B + 3) & ~3u) - 32);
+    const uint8_t *p = d + (size_t)g * K * B + o;
+    u32x4 a0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0};
+    u32x4 x[PD][2];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+        const unsigned j = min((unsigned)u, K - 1);
+        x[u][0] = ld16(p + (size_t)j * B);
+        x[u][1] = ld16(p + (size_t)j * B + 16);
+    }
+    unsigned jb = 0;
+    for (; jb + PD <= K; jb += PD) {
+#pragma unroll
+        for (int u = 0; u < PD; ++u) {
+            a0 ^= x[u][0];
+            a1 ^= x[u][1];
+            const unsigned j = min(jb + u + PD, K - 1);
+            x[u][0] = ld16(p + (size_t)j * B);
+            x[u][1] = ld16(p + (size_t)j * B + 16);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PD; ++u)
+        if (jb + u < K) {
+            a0 ^= x[u][0];
+            a1 ^= x[u][1];
+        }
+    uint8_t *q = par + (size_t)g * R * B + o;
+    for (unsigned r = 0; r < R; ++r) {
+        st16(q + (size_t)r * B, a0 + (u32x4){r, 0, 0, 0}, true);
+        st16(q + (size_t)r * B + 16, a1, true);
+    }
+}
+
+__global__ void __launch_bounds__(256) gen_lin(const uint8_t *d, uint8_t *par, unsigned rq, unsigned wq)
+{
+    const uint8_t *p = d + (size_t)blockIdx.x * rq * 16;
+    u32x4 acc = {0, 0, 0, 0};
+    for (unsigned q0 = 0; q0 < rq; q0 += 8 * 256) {
+        u32x4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = ld16(p + (size_t)min(q0 + i * 256 + threadIdx.x, rq - 1) * 16);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc ^= v[i];
+    }
+    uint8_t *o = par + (size_t)blockIdx.x * wq * 16;
+    for (unsigned q = threadIdx.x; q < wq; q += 256) st16(o + (size_t)q * 16, acc, true);
+}
+
 int main(int argc, char **argv)
 {
     const size_t G = 1u << 20;
@@ -292,6 +352,20 @@ int main(int argc, char **argv)
     run("enc_cols<16,4> nonpersist nt", enc, [&] { enc_cols<16, 4><<<(t16 + 255) / 256, 256>>>(a, b, t16, 90, true); });
     run("enc_cols<32,2> nonpersist nt", enc, [&] { enc_cols<32, 2><<<(t32 + 255) / 256, 256>>>(a, b, t32, 45, true); });
     run("enc_cols<32,4> nonpersist nt", enc, [&] { enc_cols<32, 4><<<(t32 + 255) / 256, 256>>>(a, b, t32, 45, true); });
+    // shape study: 1M groups of fec=K:R at B (the buffers hold 30.2 GB / 4.5 GB)
+    for (auto kr : {std::array<unsigned, 3>{20, 3, 1440}, {10, 3, 1400}, {10, 3, 1408}, {10, 3, 1440}, {20, 3, 1408}}) {
+        const unsigned K = kr[0], R = kr[1], B = kr[2];
+        const size_t Gs = std::min<size_t>(G, std::min(dbytes / ((size_t)K * B), pbytes / ((size_t)R * B)));
+        const unsigned cols = (B + 31) / 32, total = (unsigned)(Gs * cols);
+        const double moved = (double)Gs * (K + R) * B;
+        char nm[64];
+        snprintf(nm, 64, "gen_cols<4> %u:%u B=%u", K, R, B);
+        run(nm, moved, [&] { gen_cols<4><<<(total + 255) / 256, 256>>>(a, b, total, cols, K, R, B); });
+        if ((K * B) % 16 == 0 && (R * B) % 16 == 0) {
+            snprintf(nm, 64, "gen_lin %u:%u B=%u", K, R, B);
+            run(nm, moved, [&] { gen_lin<<<(unsigned)Gs, 256>>>(a, b, K * B / 16, R * B / 16); });
+        }
+    }
     const hipError_t e2 = hipDeviceSynchronize();
     printf("status %s\n", hipGetErrorString(e2));
     return 0;
