@@ -335,6 +335,12 @@ __device__ __forceinline__ uint4 ocb_offset(const Lds &t, uint4 o0, uint32_t i)
     return o0;
 }
 
+// A row's work per packet is its full blocks, spread over the 8 lanes, plus up to two enciphers that only one
+// lane can do: the pad of a partial last block, E_K(Offset_*), and the tag.  A lane that takes a different code
+// path makes the whole wave wait for it, so done per packet those two cost the row two extra AES times on top
+// of the ~12 it spends on 91 blocks (fec-sized 1449-byte packets).  Instead a row takes its packets 8 at a time:
+// the full blocks of each packet in turn, then lane b finishes packet b of the batch -- pad, checksum, tag --
+// so the pads of 8 packets cost one AES time, and so do their tags.
 template <bool OPEN>
 __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
 {
@@ -366,40 +372,45 @@ __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
     }
     const uint4 lstar = a.key->lstar, ldollar = a.key->ldollar, sad = a.key->sad;
     const uint32_t lane = threadIdx.x % kRow, c = 4 * (threadIdx.x % kRep);  // c: this lane's table copy, in bytes
-    for (uint64_t p = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRow; p < a.P;
-         p += (uint64_t)gridDim.x * kRowsPerBlock) {
-        const uint32_t L = a.len[p];
-        const uint64_t off = a.off[p];
-        uint32_t n, iv, ptag[4] = {0u, 0u, 0u, 0u};
-        if (OPEN) {
-            if (L < KFEC_AEAD_OVERHEAD || L - KFEC_AEAD_OVERHEAD > a.dst_pitch) {
-                if (lane == 0) {
-                    a.out_len[p] = 0;
-                    a.ok[p] = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kRowsPerBlock;
+    for (uint64_t p0 = (uint64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / kRow; p0 < a.P; p0 += kRow * stride) {
+        // lane b's packet of the batch: what its tail needs
+        bool t_on = false;       // a packet to finish (valid length)
+        uint64_t t_p = 0, t_off = 0;
+        uint32_t t_n = 0, t_iv = 0;
+        uint4 t_sum = make_uint4(0u, 0u, 0u, 0u), t_fo = t_sum, t_part = t_sum, t_ptag = t_sum;
+        for (uint32_t b = 0; b < kRow; ++b) {
+            const uint64_t p = p0 + b * stride;
+            if (p >= a.P) break;  // (uniform over the row)
+            const uint32_t L = a.len[p];
+            const uint64_t off = a.off[p];
+            uint32_t n, iv;
+            if (OPEN) {
+                if (L < KFEC_AEAD_OVERHEAD || L - KFEC_AEAD_OVERHEAD > a.dst_pitch) {
+                    if (lane == 0) {
+                        a.out_len[p] = 0;
+                        a.ok[p] = 0;
+                    }
+                    continue;
                 }
-                continue;
+                n = L - KFEC_AEAD_OVERHEAD;
+                iv = lane == b ? load16(a.src, a.src_dw, off + n + 16).x & 0xFFFFu : 0u;
+            } else {
+                if (L == 0 || (uint64_t)L + KFEC_AEAD_OVERHEAD > a.dst_pitch) {  // "empty data" / no room
+                    if (lane == 0) a.out_len[p] = 0;
+                    continue;
+                }
+                n = L;
+                iv = a.iv[p];
             }
-            n = L - KFEC_AEAD_OVERHEAD;
-            const uint4 tg = load16(a.src, a.src_dw, off + n);
-            ptag[0] = tg.x; ptag[1] = tg.y; ptag[2] = tg.z; ptag[3] = tg.w;
-            iv = load16(a.src, a.src_dw, off + n + 16).x & 0xFFFFu;
-        } else {
-            if (L == 0 || (uint64_t)L + KFEC_AEAD_OVERHEAD > a.dst_pitch) {  // "empty data" / no room
-                if (lane == 0) a.out_len[p] = 0;
-                continue;
-            }
-            n = L;
-            iv = a.iv[p];
-        }
-        const uint4 o0 = a.off0[iv];
-        const uint32_t m = n / 16, rem = n % 16, nblk = m + (rem ? 1u : 0u);
-        uint8_t *dst = a.dst + p * a.dst_pitch;
-        uint4 sum = make_uint4(0u, 0u, 0u, 0u);
-        for (uint32_t i = 1 + lane; i <= nblk; i += kRow) {  // 1-based block index
-            const uint32_t qb = 16 * (i - 1);
-            uint4 in = load16(a.src, a.src_dw, off + qb);
-            uint32_t *d32 = reinterpret_cast<uint32_t *>(dst + qb);
-            if (i <= m) {
+            if (OPEN) iv = __shfl(iv, b, kRow);
+            const uint4 o0 = a.off0[iv];
+            const uint32_t m = n / 16, rem = n % 16;
+            uint8_t *dst = a.dst + p * a.dst_pitch;
+            uint4 sum = make_uint4(0u, 0u, 0u, 0u);
+            for (uint32_t i = 1 + lane; i <= m; i += kRow) {  // the full blocks (1-based index)
+                const uint32_t qb = 16 * (i - 1);
+                const uint4 in = load16(a.src, a.src_dw, off + qb);
                 const uint4 oi = ocb_offset(s, o0, i);
                 uint4 out;
                 if constexpr (OPEN) {
@@ -409,67 +420,78 @@ __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
                     out = u4_xor(aes_enc(s, c, u4_xor(in, oi)), oi);
                     sum = u4_xor(sum, in);
                 }
-                *reinterpret_cast<uint4 *>(d32) = out;
-            } else {  // the partial last block: Pad = E_K(Offset_m xor L_*)
-                const uint4 pad = aes_enc(s, c, u4_xor(ocb_offset(s, o0, m), lstar));
-                in = mask16(in, rem);
-                const uint4 out = mask16(u4_xor(in, pad), rem);
-                uint4 pt = OPEN ? out : in;
-                uint32_t w[4] = {pt.x, pt.y, pt.z, pt.w};
+                *reinterpret_cast<uint4 *>(dst + qb) = out;
+            }
 #pragma unroll
-                for (int q = 0; q < 4; ++q) w[q] |= (uint32_t)q == rem / 4 ? 0x80u << (8 * (rem % 4)) : 0u;
-                sum = u4_xor(sum, make_uint4(w[0], w[1], w[2], w[3]));
-                const uint32_t o4[4] = {out.x, out.y, out.z, out.w};
-                // open: whole dwords (the zero pad is part of the output); seal: bytes below n only
-                const uint32_t nd = OPEN ? (rem + 3) / 4 : rem / 4;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if ((uint32_t)q < nd) d32[q] = o4[q];
-                if (!OPEN && (rem & 3)) {
-                    uint8_t *bp = dst + qb + 4 * (rem / 4);
-                    for (uint32_t q = 0; q < (rem & 3); ++q) bp[q] = (uint8_t)(o4[rem / 4] >> (8 * q));
+            for (int d = 1; d < kRow; d <<= 1) {
+                sum.x ^= __shfl_xor(sum.x, d, kRow);
+                sum.y ^= __shfl_xor(sum.y, d, kRow);
+                sum.z ^= __shfl_xor(sum.z, d, kRow);
+                sum.w ^= __shfl_xor(sum.w, d, kRow);
+            }
+            if (lane == b) {
+                t_on = true;
+                t_p = p;
+                t_off = off;
+                t_n = n;
+                t_iv = iv;
+                t_sum = sum;
+                // Offset_* = Offset_m, xor L_* after a partial block: the pad's input and the tag's offset
+                t_fo = ocb_offset(s, o0, m);
+                if (rem) {
+                    t_fo = u4_xor(t_fo, lstar);
+                    t_part = mask16(load16(a.src, a.src_dw, off + 16 * m), rem);
                 }
+                if (OPEN) t_ptag = load16(a.src, a.src_dw, off + n);
             }
         }
+        // lane b finishes packet b: the pads of the row's packets in one AES time, then their tags in another
+        const uint32_t rem = t_n % 16, m = t_n / 16;
+        const uint4 pad = aes_enc(s, c, t_fo);
+        uint8_t *dst = a.dst + t_p * a.dst_pitch;
+        if (t_on && rem) {
+            const uint4 out = mask16(u4_xor(t_part, pad), rem);
+            const uint4 pt = OPEN ? out : t_part;
+            uint32_t w[4] = {pt.x, pt.y, pt.z, pt.w};
 #pragma unroll
-        for (int d = 1; d < kRow; d <<= 1) {
-            sum.x ^= __shfl_xor(sum.x, d, kRow);
-            sum.y ^= __shfl_xor(sum.y, d, kRow);
-            sum.z ^= __shfl_xor(sum.z, d, kRow);
-            sum.w ^= __shfl_xor(sum.w, d, kRow);
+            for (int q = 0; q < 4; ++q) w[q] |= (uint32_t)q == rem / 4 ? 0x80u << (8 * (rem % 4)) : 0u;
+            t_sum = u4_xor(t_sum, make_uint4(w[0], w[1], w[2], w[3]));
+            const uint32_t o4[4] = {out.x, out.y, out.z, out.w};
+            uint32_t *d32 = reinterpret_cast<uint32_t *>(dst + 16 * m);
+            // open: whole dwords (the zero pad is part of the output); seal: bytes below n only
+            const uint32_t nd = OPEN ? (rem + 3) / 4 : rem / 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if ((uint32_t)q < nd) d32[q] = o4[q];
+            if (!OPEN && (rem & 3)) {
+                uint8_t *bp = dst + 16 * m + 4 * (rem / 4);
+                for (uint32_t q = 0; q < (rem & 3); ++q) bp[q] = (uint8_t)(o4[rem / 4] >> (8 * q));
+            }
         }
-        // Tag = E_K(Checksum xor Offset xor L_$) xor HASH(K, A), Offset = Offset_m (xor L_* after a partial block)
-        uint4 fo = ocb_offset(s, o0, m);
-        if (rem) fo = u4_xor(fo, lstar);
-        uint4 tg = make_uint4(0u, 0u, 0u, 0u);
-        if (lane == 0) tg = u4_xor(aes_enc(s, c, u4_xor(u4_xor(sum, fo), ldollar)), sad);
-        const uint32_t tag[4] = {__shfl(tg.x, 0, kRow), __shfl(tg.y, 0, kRow), __shfl(tg.z, 0, kRow),
-                                 __shfl(tg.w, 0, kRow)};
+        // Tag = E_K(Checksum xor Offset_* xor L_$) xor HASH(K, A)
+        const uint4 tg = u4_xor(aes_enc(s, c, u4_xor(u4_xor(t_sum, t_fo), ldollar)), sad);
+        if (!t_on) continue;
         if (OPEN) {
-            const bool good = tag[0] == ptag[0] && tag[1] == ptag[1] && tag[2] == ptag[2] && tag[3] == ptag[3];
-            if (!good) {  // no unauthenticated plaintext leaves the kernel
+            const bool good = tg.x == t_ptag.x && tg.y == t_ptag.y && tg.z == t_ptag.z && tg.w == t_ptag.w;
+            if (!good) {  // no unauthenticated plaintext leaves the kernel (the row's stores came first)
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);
-                const uint32_t nd = (n + 3) / 4;
-                for (uint32_t i = lane; i < nd; i += kRow) d32[i] = 0u;
+                const uint32_t nd = (t_n + 3) / 4;
+                for (uint32_t i = 0; i < nd; ++i) d32[i] = 0u;
             }
-            if (lane == 0) {
-                a.out_len[p] = good ? n : 0u;
-                a.ok[p] = good ? 1 : 0;
-            }
+            a.out_len[t_p] = good ? t_n : 0u;
+            a.ok[t_p] = good ? 1 : 0;
         } else {
-            // tag || iv_raw || zeros to the next multiple of 4: bytes n .. n + 21, 3 per lane
-            const uint32_t end = (n + KFEC_AEAD_OVERHEAD + 3) & ~3u;
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const uint32_t i = 3 * lane + q;
-                if (n + i < end) {
-                    const uint32_t w = i < 4 ? tag[0] : i < 8 ? tag[1] : i < 12 ? tag[2] : i < 16 ? tag[3] : iv;
-                    dst[n + i] = (uint8_t)(i < 18 ? (w >> (8 * (i & 3))) & 0xFFu : 0u);
-                }
+            // tag || iv_raw || zeros to the next multiple of 4: bytes n .. round4(n + 18)
+            const uint32_t tag[4] = {tg.x, tg.y, tg.z, tg.w};
+            const uint32_t end = (t_n + KFEC_AEAD_OVERHEAD + 3) & ~3u;
+            for (uint32_t i = 0; t_n + i < end; ++i) {
+                const uint32_t w = i < 4 ? tag[0] : i < 8 ? tag[1] : i < 12 ? tag[2] : i < 16 ? tag[3] : t_iv;
+                dst[t_n + i] = (uint8_t)(i < 18 ? (w >> (8 * (i & 3))) & 0xFFu : 0u);
             }
-            if (lane == 0) a.out_len[p] = n + KFEC_AEAD_OVERHEAD;
+            a.out_len[t_p] = t_n + KFEC_AEAD_OVERHEAD;
         }
+        (void)t_off;
     }
 }
 

@@ -19,4 +19,7 @@ timeout -k 10 200 python tools/bench_wire.py --ragged > $out/wire_ragged.json ||
 for t in 1 2 4 8; do timeout -k 10 300 ./tools/pipeline_bench 20 23 1440 16384 4 3 $t || exit 1; done > $out/pipeline_threads.json
 timeout -k 10 120 ./tools/latency_bench > $out/latency.json || exit 1
 KFEC_WORKER=0 timeout -k 10 120 ./tools/latency_bench > $out/latency_launch.json || exit 1
+timeout -k 10 120 ./tools/side_effects 400 > $out/side_effects.jsonl || exit 1
+timeout -k 10 300 python tools/concurrent_bench.py > $out/concurrent.json || exit 1
+for mode in none chacha20; do for G in 16 256 4096; do F=$(( G >= 4096 ? 5 : 33 )); PB_SEAL=$mode timeout -k 10 120 ./tools/pipeline_bench 20 23 1440 $G $F 3 1 || exit 1; done; done > $out/pipeline_sealed.jsonl
 echo round-done
