@@ -573,15 +573,11 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
     __shared__ uint8_t s_M[256];      // missing data ids, ascending
     __shared__ uint8_t s_P[256];      // parity share used for missing rank t: the highest present ids, descending
     __shared__ uint8_t s_src[256];    // source share of column j
-    __shared__ __attribute__((aligned(8))) uint16_t s_lden[256];  // log den of the source of column j
+    __shared__ uint16_t s_lden[256];  // log den of the source of column j
     __shared__ uint16_t s_lnum[256];  // log num_u without the (x_{M_u} ^ x_i) factor
-    __shared__ __attribute__((aligned(4))) uint8_t s_xs[256];  // point of the source of column j
-    __shared__ uint8_t s_xM[256];     // point of missing id M_u
-    __shared__ uint8_t s_e3[768];     // exp[i mod 255] for i < 768: a coefficient's log needs no reduction
     const int K = a.K, N = a.N, R = a.R, tid = threadIdx.x;
     const int K4 = (K + 3) & ~3, kd = K4 / 4;
     stage_gf(s_exp, s_log);
-    for (int i = tid; i < 768; i += kPrepThreads) s_e3[i] = c_gf.exp[i % 255];
     __syncthreads();
     auto xpt = [&](int sid) -> uint32_t { return sid ? (uint32_t)s_exp[sid] : 0u; };  // s_exp[255] = 1
     for (int sid = tid; sid < N; sid += kPrepThreads) {
@@ -640,17 +636,11 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
             if (sid < K && ((dm[q] >> b) & 1ull)) s_M[rank_below(dm, sid)] = (uint8_t)sid;
         }
         __syncthreads();
-        for (int j = tid; j < K4; j += kPrepThreads) {
-            if (j >= K) {  // (the pad columns of the last dword: never used, kept defined)
-                s_xs[j] = 0;
-                s_lden[j] = 0;
-                continue;
-            }
+        for (int j = tid; j < K; j += kPrepThreads) {
             const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
             const int i = miss ? (int)s_P[rank_below(dm, j)] : j;
             s_src[j] = (uint8_t)i;
             const uint32_t xi = xpt(i);
-            s_xs[j] = (uint8_t)xi;
             uint32_t acc = 0;
             for (int c = 0; c < R; ++c) acc += s_log[xi ^ s_xC[c]];
             s_lden[j] = (uint16_t)((s_full[i] + 255u - acc % 255u) % 255u);
@@ -658,7 +648,6 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
         for (int u = tid; u < m; u += kPrepThreads) {
             const int mu = s_M[u];
             const uint32_t xm = xpt(mu);
-            s_xM[u] = (uint8_t)xm;
             uint32_t acc = 0;
             for (int c = 0; c < R; ++c)
                 if (s_C[c] != mu) acc += s_log[xm ^ s_xC[c]];
@@ -674,25 +663,20 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
                 if (4 * d + b < K) v |= (uint32_t)s_src[4 * d + b] << (8 * b);
             srcw[d] = v;
         }
-        // thread = (row u, column dword d < kd <= 64): the column's 4 points and log dens are read once, then per
-        // row and byte one log and one antilog lookup (ln + 510 - log - lden lies in [2, 764]: s_e3, no modulo)
-        {
-            const int d = tid & 63;
-            if (d < kd) {
-                const uint32_t xs4 = reinterpret_cast<const uint32_t *>(s_xs)[d];
-                const uint2 ld4 = reinterpret_cast<const uint2 *>(s_lden)[d];
-                const int ldn[4] = {(int)(ld4.x & 0xFFFFu), (int)(ld4.x >> 16), (int)(ld4.y & 0xFFFFu), (int)(ld4.y >> 16)};
-                for (int u = tid >> 6; u < m; u += kPrepThreads / 64) {
-                    const uint32_t xm = s_xM[u];
-                    const int ln = (int)s_lnum[u] + 510;
-                    uint32_t v = 0;
+        for (int e = tid; e < m * kd; e += kPrepThreads) {
+            const int u = e / kd, d = e - u * kd;
+            const uint32_t xm = xpt(s_M[u]);
+            const int ln = s_lnum[u];
+            uint32_t v = 0;
 #pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        if (4 * d + b < K)
-                            v |= (uint32_t)s_e3[ln - (int)s_log[xm ^ ((xs4 >> (8 * b)) & 0xFFu)] - ldn[b]] << (8 * b);
-                    coefw[u * kd + d] = v;
+            for (int b = 0; b < 4; ++b) {
+                const int j = 4 * d + b;
+                if (j < K) {
+                    const int ex = (ln + 510 - (int)s_log[xm ^ xpt(s_src[j])] - (int)s_lden[j]) % 255;
+                    v |= (uint32_t)s_exp[ex] << (8 * b);
                 }
             }
+            coefw[u * kd + d] = v;
         }
         for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
         if (tid == 0) {
