@@ -212,6 +212,9 @@ CASES = [
     (100, 104, 64, 64, 20, 4, "K > 64 with R <= 8: second present word"),
     (250, 255, 16, 16, 10, 5, "K > 192 with R <= 8: fourth present word"),
     (20, 23, 1440, 1440, 64, 0, "zero loss: nothing recovered, nothing read"),
+    (40, 60, 1440, 1440, 64, 20, "R=20, V=32: T-table decode entries, ~7 groups per workgroup, one chunk"),
+    (30, 42, 97, 97, 21, 12, "R=12, odd pitch: bytewise T-table decode, entries in several chunks"),
+    (60, 80, 1440, 1440, 33, None, "R=20, random 0..21 erasures over all 80: mixed m, some groups empty"),
 ]
 
 
