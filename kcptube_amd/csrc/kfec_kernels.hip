@@ -54,6 +54,16 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #ifndef KFEC_EXPAND_EB
 #define KFEC_EXPAND_EB 8  // mac_expand: items per thread whose loads are issued together (1: load-use per item)
 #endif
+#ifndef KFEC_SYN_EARLY
+#define KFEC_SYN_EARLY 1  // syn_kernel: C-table bytes loaded with the record header, expanded after the shard loop
+#endif
+#ifndef KFEC_SYN_TPRE
+#define KFEC_SYN_TPRE 1  // syn_loop: the next shard's E tables loaded into SGPRs one shard ahead (0: at use; A/B knob)
+#endif
+#ifndef KFEC_SYN_ROWMASK
+#define KFEC_SYN_ROWMASK 1  // listed syndrome decode: 0 every parity row, 1 only the rows the group uses,
+                            // 2 as 1 but single-row groups run a two-row variant (A/B knob)
+#endif
 #ifndef KFEC_MINW
 #define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the MAC kernels
 #endif
@@ -1128,19 +1138,39 @@ constexpr uint32_t kAbsent = 0x80000000u;  // beyond every resource (the host ke
 
 // C tables of one group into LDS: tp[u * TD + 5 r + i] (zero for a group that recovers nothing)
 template <int RT>
-__device__ __forceinline__ void syn_expand_one(const uint8_t *rec, uint32_t ur, uint32_t *tp)
+__device__ __forceinline__ void syn_expand_put(uint32_t c, uint32_t ur, uint32_t *tp)
 {
     constexpr int TD = SynLayout<RT>::TD;
     const uint32_t u = ur / RT, r = ur - u * RT;
     uint32_t t[5];
-    gf_perm_tables(rec[0] == 0 ? rec[40 + 8 * u + r] : 0u, t);
+    gf_perm_tables(c, t);
 #pragma unroll
     for (int i = 0; i < 5; ++i) tp[u * TD + 5 * r + i] = t[i];
 }
 
+// C[u][r] of entry ur = u * RT + r of a record (0 unless status 0); both bytes are loaded unconditionally, so
+// the two loads are in flight together
+template <int RT>
+__device__ __forceinline__ uint32_t syn_coef(const uint8_t *rec, uint32_t ur)
+{
+    const uint32_t u = ur / RT, r = ur - u * RT;
+    const uint32_t st = rec[0], c = rec[40 + 8 * u + r];
+    return st == 0 ? c : 0u;
+}
+
+template <int RT>
+__device__ __forceinline__ void syn_expand_one(const uint8_t *rec, uint32_t ur, uint32_t *tp)
+{
+    syn_expand_put<RT>(syn_coef<RT>(rec, ur), ur, tp);
+}
+
 // y_r = parity_r ^ XOR_{j present} E[r][j] * D_j for one lane's column (rd / rp: resources over its group's
 // data / parity rows, drow / prow: byte offsets of the lane's granule in the group's first data / parity row)
-template <int VEC, int RT, int PD>
+// ROWS: the parity rows computed (bit r = row r; a compile-time mask, so each variant is the plain unrolled loop).
+// A group that lost m data shards uses m parity rows: syn_list_kernel (one group per task, so the mask is
+// uniform) leaves out the rows its group does not use -- at ~1% loss mostly 2 of 3 (fec=20:3 listed decode
+// 1.41 -> 1.23 ms, profiles/r04_rowmask_ab.txt).
+template <int VEC, int RT, int PD, uint32_t ROWS = (1u << RT) - 1u>
 __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][Gran<VEC>::W], __amdgpu_buffer_rsrc_t rd,
                                          __amdgpu_buffer_rsrc_t rp, uint32_t drow, uint32_t prow, uint32_t used,
                                          uint64_t p0, const uint8_t *rec)
@@ -1161,11 +1191,24 @@ __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][G
         return ((wq >> (j & 63u)) & 1ull) ? drow + j * pitch : kAbsent;
     };
     typedef const __attribute__((address_space(4))) uint32_t cu32;  // uniform: scalar loads into SGPRs
-    auto mac = [&](const Gran<VEC> &cur, uint32_t j) {
-        const cu32 *tg = (const cu32 *)(a.etab + (size_t)j * a.etab_rows * 5);
-        uint32_t t[5 * RT];
+    uint32_t tn[5 * RT];  // KFEC_SYN_TPRE: shard j's tables, loaded while shard j - 1 is multiplied
+    auto tload = [&](uint32_t j) {
+        const cu32 *tg = (const cu32 *)(a.etab + (size_t)min(j, K - 1) * a.etab_rows * 5);
 #pragma unroll
-        for (int i = 0; i < 5 * RT; ++i) t[i] = tg[i];
+        for (int i = 0; i < 5 * RT; ++i) tn[i] = tg[i];
+    };
+    if (KFEC_SYN_TPRE) tload(0);
+    auto mac = [&](const Gran<VEC> &cur, uint32_t j) {
+        uint32_t t[5 * RT];
+        if (KFEC_SYN_TPRE) {
+#pragma unroll
+            for (int i = 0; i < 5 * RT; ++i) t[i] = tn[i];
+            tload(j + 1);
+        } else {
+            const cu32 *tg = (const cu32 *)(a.etab + (size_t)j * a.etab_rows * 5);
+#pragma unroll
+            for (int i = 0; i < 5 * RT; ++i) t[i] = tg[i];
+        }
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             const uint32_t xv = cur.d[w];
@@ -1173,7 +1216,8 @@ __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][G
             const uint32_t s1 = (xv >> 3) & 0x07070707u;
             const uint32_t s2 = (xv >> 6) & 0x03030303u;
 #pragma unroll
-            for (int r = 0; r < RT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+            for (int r = 0; r < RT; ++r)
+                if ((ROWS >> r) & 1u) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
         }
     };
     // PD shards in flight, every load unconditional (see mac_kernel)
@@ -1194,7 +1238,7 @@ __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][G
 }
 
 // out_u = XOR_r C[u][r] * y_r for u < m, stored to recovered slot u of group g
-template <int VEC, int RT>
+template <int VEC, int RT, uint32_t ROWS = (1u << RT) - 1u>
 __device__ __forceinline__ void syn_final(const SynArgs &a, const uint32_t (&acc)[RT][Gran<VEC>::W], const uint32_t *ct,
                                           uint32_t m, uint32_t g, uint32_t off, uint32_t col)
 {
@@ -1217,6 +1261,7 @@ __device__ __forceinline__ void syn_final(const SynArgs &a, const uint32_t (&acc
                 uint32_t v = 0;
 #pragma unroll
                 for (int r = 0; r < RT; ++r) {
+                    if (!((ROWS >> r) & 1u)) continue;  // (C[u][r] = 0 for a row no lane of the wave uses)
                     const uint32_t yv = acc[r][w];
                     v = perm_mac(v, t + 5 * r, yv & 0x07070707u, (yv >> 3) & 0x07070707u, (yv >> 6) & 0x03030303u);
                 }
@@ -1225,6 +1270,31 @@ __device__ __forceinline__ void syn_final(const SynArgs &a, const uint32_t (&acc
             store_gran<VEC>(a.out + obase + (uint64_t)u * a.pitch, o, col, a.B);
         }
     }
+}
+
+// f(std::integral_constant<uint32_t, ROWS>) for the wave-uniform row mask `rows` (RT <= 3: one variant per
+// non-empty mask; wider tiles always compute every row)
+template <int RT, typename F>
+__device__ __forceinline__ void by_row_mask(uint32_t rows, F &&f)
+{
+    // KFEC_SYN_ROWMASK 2: single-row waves take a two-row variant (fewer registers)
+    constexpr uint32_t one0 = KFEC_SYN_ROWMASK == 1 ? 1u : 3u, one1 = KFEC_SYN_ROWMASK == 1 ? 2u : 3u,
+                       one2 = KFEC_SYN_ROWMASK == 1 ? 4u : 5u;
+    if constexpr (RT == 2 && KFEC_SYN_ROWMASK != 0) {
+        if (rows == 1) return f(std::integral_constant<uint32_t, one0>());
+        if (rows == 2) return f(std::integral_constant<uint32_t, one1>());
+    } else if constexpr (RT == 3 && KFEC_SYN_ROWMASK != 0) {
+        switch (rows) {
+        case 1: return f(std::integral_constant<uint32_t, one0>());
+        case 2: return f(std::integral_constant<uint32_t, one1>());
+        case 3: return f(std::integral_constant<uint32_t, 3>());
+        case 4: return f(std::integral_constant<uint32_t, one2>());
+        case 5: return f(std::integral_constant<uint32_t, 5>());
+        case 6: return f(std::integral_constant<uint32_t, 6>());
+        default: break;
+        }
+    }
+    f(std::integral_constant<uint32_t, (1u << RT) - 1u>());
 }
 
 // Two launch shapes, chosen per launch ON THE DEVICE from the number of groups with data to recover (the
@@ -1266,18 +1336,22 @@ __global__ void __launch_bounds__(kMacBlock) syn_list_kernel(SynArgs a)
         const uint32_t m = (h.x >> 8) & 0xFFu;  // listed groups have status 0 and m > 0
         const uint32_t used = (h.x >> 16) & 0xFFu;
         const uint64_t p0 = (uint64_t)h.z | ((uint64_t)h.w << 32);
-        uint32_t acc[RT][W];
-        if (in) {
-            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(a.data + (uint64_t)g * a.K * a.pitch), (short)0, (int)(a.K * a.pitch), 0x00020000);
-            const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(a.parity + (uint64_t)g * a.R * a.pitch), (short)0, (int)(a.R * a.pitch), 0x00020000);
-            syn_loop<VEC, RT, PD>(a, acc, rd, rp, off, off, used, p0, rec);
-        }
-        // the tables were written by lanes of this wave: LDS operations of one wave complete in order, the
-        // fence keeps the compiler from moving the reads above the writes
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (in) syn_final<VEC, RT>(a, acc, ct, m, g, off, col);
+        const uint32_t wrows = __builtin_amdgcn_readfirstlane(used);  // (one group per task: uniform)
+        by_row_mask<RT>(wrows, [&](auto rows_c) {
+            constexpr uint32_t ROWS = decltype(rows_c)::value;
+            uint32_t acc[RT][W];
+            if (in) {
+                const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                    (void *)(a.data + (uint64_t)g * a.K * a.pitch), (short)0, (int)(a.K * a.pitch), 0x00020000);
+                const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+                    (void *)(a.parity + (uint64_t)g * a.R * a.pitch), (short)0, (int)(a.R * a.pitch), 0x00020000);
+                syn_loop<VEC, RT, PD, ROWS>(a, acc, rd, rp, off, off, used, p0, rec);
+            }
+            // the tables were written by lanes of this wave: LDS operations of one wave complete in order, the
+            // fence keeps the compiler from moving the reads above the writes
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (in) syn_final<VEC, RT, ROWS>(a, acc, ct, m, g, off, col);
+        });
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the next task rewrites the tables
     }
 }
@@ -1305,10 +1379,19 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
     const uint32_t wbase = min(base + (threadIdx.x & ~63u), a.total - 1);
     const uint32_t wfirst = wbase / cols, wlast = min(wbase + 63, a.total - 1) / cols;
     uint32_t *ctw = s_ct + (threadIdx.x / 64) * syn_wave_groups(cols) * RT * TD;
-    for (uint32_t e = threadIdx.x & 63u; e < (wlast - wfirst + 1) * RT * RT; e += 64) {
+    const uint32_t ne = (wlast - wfirst + 1) * RT * RT;
+#if KFEC_SYN_EARLY
+    // the first 64 entries' coefficient bytes are loaded now, with the record header below, and expanded into
+    // LDS after the shard loop: the shard loads wait for one dependent load (the header), not three
+    const uint32_t e0 = threadIdx.x & 63u;
+    const uint32_t e0g = min(e0, ne - 1) / (RT * RT);
+    const uint32_t c_e0 = syn_coef<RT>(a.rec + (uint64_t)(wfirst + e0g) * a.rec_stride, min(e0, ne - 1) - e0g * (RT * RT));
+#else
+    for (uint32_t e = threadIdx.x & 63u; e < ne; e += 64) {
         const uint32_t gs = e / (RT * RT);
         syn_expand_one<RT>(a.rec + (uint64_t)(wfirst + gs) * a.rec_stride, e - gs * (RT * RT), ctw + gs * RT * TD);
     }
+#endif
 #else
     const uint32_t glast = min(base + kMacBlock - 1, a.total - 1) / cols;
     const uint32_t ng = glast - gfirst + 1;
@@ -1336,6 +1419,8 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
         p0 = (uint64_t)h.z | ((uint64_t)h.w << 32);
     }
     const bool active = m > 0;
+    // (every parity row: the row-mask variants of syn_list_kernel cost this shape a register budget of 143
+    // VGPRs and 3% at m = R, and gain nothing with random 1-3 erasures of 13; profiles/r04_rowmask_ab.txt)
     uint32_t acc[RT][W];
     if (active) {
         // resources over this workgroup's groups (wave-uniform: blockIdx and kernel arguments only)
@@ -1348,6 +1433,13 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
                               p0, rec);
     }
 #if KFEC_SYN_WAVE_CT
+#if KFEC_SYN_EARLY
+    if (e0 < ne) syn_expand_put<RT>(c_e0, e0 - e0g * (RT * RT), ctw + e0g * RT * TD);
+    for (uint32_t e = e0 + 64; e < ne; e += 64) {  // (more than 64 entries: pitch < 64 bytes per group)
+        const uint32_t gs = e / (RT * RT);
+        syn_expand_one<RT>(a.rec + (uint64_t)(wfirst + gs) * a.rec_stride, e - gs * (RT * RT), ctw + gs * RT * TD);
+    }
+#endif
     // written by lanes of this wave: LDS operations of one wave complete in order; the fence keeps the
     // compiler from moving the reads above the writes
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
