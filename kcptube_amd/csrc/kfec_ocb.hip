@@ -172,6 +172,12 @@ __global__ void ocb_iv_kernel(const uint32_t *key, uint4 *off0)
 }
 
 // ---- per-packet kernel -------------------------------------------------------------------------------
+#ifndef KFEC_OCB_BITOP3
+#define KFEC_OCB_BITOP3 1  // byte-1 table addresses by v_bitop3_b32 instead of v_perm_b32 (A/B knob)
+#endif
+#ifndef KFEC_OCB_ILP
+#define KFEC_OCB_ILP 2  // full blocks per lane through the AES rounds together (1 or 2; A/B knob)
+#endif
 constexpr int kRow = 8;
 constexpr int kOcbBlock = 512;
 constexpr int kRowsPerBlock = kOcbBlock / kRow;
@@ -232,7 +238,9 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int k) { return __builtin_a
 template <int J, int K>
 __device__ __forceinline__ uint32_t rep_at(const uint32_t (*T)[2][kRep], uint32_t x, uint32_t c4)
 {
-    const uint32_t o = __builtin_amdgcn_perm(x, c4, 0x0C0C0000u | ((4u + K) << 8));
+    // byte 1 is already in bits 8..15: (x & 0xFF00) | c4 is one v_bitop3_b32, a full-rate op (v_perm_b32 is not)
+    const uint32_t o = K == 1 && KFEC_OCB_BITOP3 ? __builtin_amdgcn_bitop3_b32(x, 0xFF00u, c4, 0xEA)
+                                                 : __builtin_amdgcn_perm(x, c4, 0x0C0C0000u | ((4u + K) << 8));
     return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(T) + o + 128 * J);
 }
 
@@ -324,6 +332,61 @@ __device__ __forceinline__ uint4 aes_dec(const OcbLds<true> &t, uint32_t c4, uin
     return make_uint4(o0 ^ k.x, o1 ^ k.y, o2 ^ k.z, o3 ^ k.w);
 }
 
+// two blocks through the rounds together (KFEC_OCB_ILP 2): twice the independent table reads in flight per
+// wave, for the latency the 4 waves per SIMD that the tables' LDS allows do not hide
+__device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, uint32_t c4, uint4 &x, uint4 &y)
+{
+    uint32_t s0 = x.x ^ t.rk[0].x, s1 = x.y ^ t.rk[0].y, s2 = x.z ^ t.rk[0].z, s3 = x.w ^ t.rk[0].w;
+    uint32_t u0 = y.x ^ t.rk[0].x, u1 = y.y ^ t.rk[0].y, u2 = y.z ^ t.rk[0].z, u3 = y.w ^ t.rk[0].w;
+#pragma unroll 1
+    for (int r = 1; r < 14; ++r) {
+        const uint4 k = t.rk[r];
+        const uint32_t t0 = tcol(t.te, c4, s0, s1, s2, s3, k.x);
+        const uint32_t v0 = tcol(t.te, c4, u0, u1, u2, u3, k.x);
+        const uint32_t t1 = tcol(t.te, c4, s1, s2, s3, s0, k.y);
+        const uint32_t v1 = tcol(t.te, c4, u1, u2, u3, u0, k.y);
+        const uint32_t t2 = tcol(t.te, c4, s2, s3, s0, s1, k.z);
+        const uint32_t v2 = tcol(t.te, c4, u2, u3, u0, u1, k.z);
+        const uint32_t t3 = tcol(t.te, c4, s3, s0, s1, s2, k.w);
+        const uint32_t v3 = tcol(t.te, c4, u3, u0, u1, u2, k.w);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+        u0 = v0; u1 = v1; u2 = v2; u3 = v3;
+    }
+    const uint4 k = t.rk[14];
+    const uint32_t (*T)[2][kRep] = t.te;
+    auto last = [&](uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+        return sbox_col(rep_at<0, 0>(T, a0, c4), rep_at<0, 1>(T, a1, c4), rep_at<0, 2>(T, a2, c4), rep_at<0, 3>(T, a3, c4));
+    };
+    x = make_uint4(last(s0, s1, s2, s3) ^ k.x, last(s1, s2, s3, s0) ^ k.y, last(s2, s3, s0, s1) ^ k.z, last(s3, s0, s1, s2) ^ k.w);
+    y = make_uint4(last(u0, u1, u2, u3) ^ k.x, last(u1, u2, u3, u0) ^ k.y, last(u2, u3, u0, u1) ^ k.z, last(u3, u0, u1, u2) ^ k.w);
+}
+
+__device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, uint32_t c4, uint4 &x, uint4 &y)
+{
+    uint32_t s0 = x.x ^ t.dk[0].x, s1 = x.y ^ t.dk[0].y, s2 = x.z ^ t.dk[0].z, s3 = x.w ^ t.dk[0].w;
+    uint32_t u0 = y.x ^ t.dk[0].x, u1 = y.y ^ t.dk[0].y, u2 = y.z ^ t.dk[0].z, u3 = y.w ^ t.dk[0].w;
+#pragma unroll 1
+    for (int r = 1; r < 14; ++r) {
+        const uint4 k = t.dk[r];
+        const uint32_t t0 = tcol(t.td, c4, s0, s3, s2, s1, k.x);
+        const uint32_t v0 = tcol(t.td, c4, u0, u3, u2, u1, k.x);
+        const uint32_t t1 = tcol(t.td, c4, s1, s0, s3, s2, k.y);
+        const uint32_t v1 = tcol(t.td, c4, u1, u0, u3, u2, k.y);
+        const uint32_t t2 = tcol(t.td, c4, s2, s1, s0, s3, k.z);
+        const uint32_t v2 = tcol(t.td, c4, u2, u1, u0, u3, k.z);
+        const uint32_t t3 = tcol(t.td, c4, s3, s2, s1, s0, k.w);
+        const uint32_t v3 = tcol(t.td, c4, u3, u2, u1, u0, k.w);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+        u0 = v0; u1 = v1; u2 = v2; u3 = v3;
+    }
+    const uint4 k = t.dk[14];
+    auto last = [&](uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+        return isb<0>(t, c4, a0) | isb<1>(t, c4, a1) << 8 | isb<2>(t, c4, a2) << 16 | isb<3>(t, c4, a3) << 24;
+    };
+    x = make_uint4(last(s0, s3, s2, s1) ^ k.x, last(s1, s0, s3, s2) ^ k.y, last(s2, s1, s0, s3) ^ k.z, last(s3, s2, s1, s0) ^ k.w);
+    y = make_uint4(last(u0, u3, u2, u1) ^ k.x, last(u1, u0, u3, u2) ^ k.y, last(u2, u1, u0, u3) ^ k.z, last(u3, u2, u1, u0) ^ k.w);
+}
+
 template <class Lds>
 __device__ __forceinline__ uint4 ocb_offset(const Lds &t, uint4 o0, uint32_t i)
 {
@@ -342,7 +405,7 @@ __device__ __forceinline__ uint4 ocb_offset(const Lds &t, uint4 o0, uint32_t i)
 // the full blocks of each packet in turn, then lane b finishes packet b of the batch -- pad, checksum, tag --
 // so the pads of 8 packets cost one AES time, and so do their tags.
 template <bool OPEN>
-__global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
+__global__ void __launch_bounds__(kOcbBlock, 4) ocb_kernel(OcbArgs a)  // (4 waves per SIMD: two workgroups per CU)
 {
     __shared__ OcbLds<OPEN> s;
     {
@@ -408,6 +471,29 @@ __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
             const uint32_t m = n / 16, rem = n % 16;
             uint8_t *dst = a.dst + p * a.dst_pitch;
             uint4 sum = make_uint4(0u, 0u, 0u, 0u);
+#if KFEC_OCB_ILP == 2
+            for (uint32_t i = 1 + lane; i <= m; i += 2 * kRow) {  // blocks i and i + 8 (1-based) together
+                const bool two = i + kRow <= m;
+                const uint32_t j = two ? i + kRow : i;
+                const uint4 ia = load16(a.src, a.src_dw, off + 16 * (i - 1));
+                const uint4 ib = load16(a.src, a.src_dw, off + 16 * (j - 1));
+                const uint4 oa = ocb_offset(s, o0, i), ob = ocb_offset(s, o0, j);
+                uint4 xa = u4_xor(ia, oa), xb = u4_xor(ib, ob);
+                if constexpr (OPEN) aes_dec2(s, c, xa, xb);
+                else aes_enc2(s, c, xa, xb);
+                xa = u4_xor(xa, oa);
+                xb = u4_xor(xb, ob);
+                if constexpr (OPEN) {
+                    sum = u4_xor(sum, xa);
+                    if (two) sum = u4_xor(sum, xb);
+                } else {
+                    sum = u4_xor(sum, ia);
+                    if (two) sum = u4_xor(sum, ib);
+                }
+                *reinterpret_cast<uint4 *>(dst + 16 * (i - 1)) = xa;
+                if (two) *reinterpret_cast<uint4 *>(dst + 16 * (j - 1)) = xb;
+            }
+#else
             for (uint32_t i = 1 + lane; i <= m; i += kRow) {  // the full blocks (1-based index)
                 const uint32_t qb = 16 * (i - 1);
                 const uint4 in = load16(a.src, a.src_dw, off + qb);
@@ -422,6 +508,7 @@ __global__ void __launch_bounds__(kOcbBlock) ocb_kernel(OcbArgs a)
                 }
                 *reinterpret_cast<uint4 *>(dst + qb) = out;
             }
+#endif
 #pragma unroll
             for (int d = 1; d < kRow; d <<= 1) {
                 sum.x ^= __shfl_xor(sum.x, d, kRow);
