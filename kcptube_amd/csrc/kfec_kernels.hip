@@ -66,6 +66,21 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #ifndef KFEC_SYN_LDSE
 #define KFEC_SYN_LDSE 0  // 1: syn_kernel stages the E tables in LDS, read as broadcasts (A/B knob: slower than scalar loads)
 #endif
+#ifndef KFEC_PREP_FUSED
+#define KFEC_PREP_FUSED 1  // decode_prep_lagrange: denominators and numerators in one pass (0: two loops; A/B knob)
+#endif
+#ifndef KFEC_PREP_COEF2
+#define KFEC_PREP_COEF2 1  // decode_prep_lagrange coefficients from stored column points, no modulo (A/B knob)
+#endif
+#if KFEC_PREP_COEF2 && !KFEC_PREP_FUSED
+#error "KFEC_PREP_COEF2 reads the column points the fused pass (KFEC_PREP_FUSED) stores"
+#endif
+#ifndef KFEC_PREP_PREFETCH
+#define KFEC_PREP_PREFETCH 1  // decode_prep_lagrange loads the next group's present bits one group ahead (A/B knob)
+#endif
+#ifndef KFEC_PREP_MINW
+#define KFEC_PREP_MINW 8  // decode_prep_lagrange: minimum waves per SIMD (8: 64 VGPRs, 12 spilled, 3% faster than uncapped)
+#endif
 #ifndef KFEC_SYN_ROWMASK
 #define KFEC_SYN_ROWMASK 1  // listed syndrome decode: 0 every parity row, 1 only the rows the group uses,
                             // 2 as 1 but single-row groups run a two-row variant (A/B knob)
@@ -580,7 +595,7 @@ __device__ __forceinline__ int rank_below(const uint64_t (&b)[4], int s)
 //   followed by the product with the parity rows (measured at 200:55: 63.8 ms -> see DESIGN.md 5).
 constexpr int kPrepThreads = 256;
 
-__global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
+__global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagrange(PrepArgs a)
 {
     __shared__ uint8_t s_exp[512], s_log[256];
     __shared__ uint16_t s_full[256];  // FULL_s mod 255
@@ -591,6 +606,7 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
     __shared__ uint8_t s_src[256];    // source share of column j
     __shared__ uint16_t s_lden[256];  // log den of the source of column j
     __shared__ uint16_t s_lnum[256];  // log num_u without the (x_{M_u} ^ x_i) factor
+    __shared__ uint8_t s_xs[256];     // KFEC_PREP_COEF2: the point of column j's source
     const int K = a.K, N = a.N, R = a.R, tid = threadIdx.x;
     const int K4 = (K + 3) & ~3, kd = K4 / 4;
     stage_gf(s_exp, s_log);
@@ -605,12 +621,24 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
     }
     __syncthreads();
 
+    // KFEC_PREP_PREFETCH: the next group's present bits are loaded while this group is solved
+    uint64_t pn[4] = {0, 0, 0, 0};
+    if (KFEC_PREP_PREFETCH && blockIdx.x < a.G) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pn[q] = a.present[(uint64_t)blockIdx.x * 4 + q];
+    }
     for (uint64_t g = blockIdx.x; g < a.G; g += gridDim.x) {
-        uint64_t w[4], dm[4];
+        uint64_t w[4], dm[4], pc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pc[q] = KFEC_PREP_PREFETCH ? pn[q] : a.present[g * 4 + q];
+        if (KFEC_PREP_PREFETCH && g + gridDim.x < a.G) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pn[q] = a.present[(g + gridDim.x) * 4 + q];
+        }
         int cnt = 0, m = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            w[q] = a.present[g * 4 + q] & bits_below(N, q);
+            w[q] = pc[q] & bits_below(N, q);
             dm[q] = ~w[q] & bits_below(K, q);
             cnt += __popcll(w[q]);
             m += __popcll(dm[q]);
@@ -652,6 +680,29 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
             if (sid < K && ((dm[q] >> b) & 1ull)) s_M[rank_below(dm, sid)] = (uint8_t)sid;
         }
         __syncthreads();
+#if KFEC_PREP_FUSED
+        // the K column denominators and the m numerators are one kind of sum, log FULL_s - sum_c log(x_s ^ x_c),
+        // so they are one pass of K + m <= N <= 256 items (one per thread) instead of two loops that wave 0
+        // ran back to back; a numerator's excluded term c = M_u has x_s ^ x_c = 0, and log[0] = 255 = 0 mod 255
+        for (int it = tid; it < K + m; it += kPrepThreads) {
+            int sid;
+            if (it < K) {
+                const bool miss = (dm[it >> 6] >> (it & 63)) & 1ull;
+                sid = miss ? (int)s_P[rank_below(dm, it)] : it;
+                s_src[it] = (uint8_t)sid;
+            } else {
+                sid = s_M[it - K];
+            }
+            const uint32_t xs = xpt(sid);
+            if (KFEC_PREP_COEF2 && it < K) s_xs[it] = (uint8_t)xs;
+            uint32_t acc = 0;
+#pragma unroll 8
+            for (int c = 0; c < R; ++c) acc += s_log[xs ^ s_xC[c]];
+            const uint16_t v = (uint16_t)((s_full[sid] + 255u - acc % 255u) % 255u);
+            if (it < K) s_lden[it] = v;
+            else s_lnum[it - K] = v;
+        }
+#else
         for (int j = tid; j < K; j += kPrepThreads) {
             const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
             const int i = miss ? (int)s_P[rank_below(dm, j)] : j;
@@ -669,6 +720,7 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
                 if (s_C[c] != mu) acc += s_log[xm ^ s_xC[c]];
             s_lnum[u] = (uint16_t)((s_full[mu] + 255u - acc % 255u) % 255u);
         }
+#endif
         __syncthreads();
         uint32_t *srcw = reinterpret_cast<uint32_t *>(rec + 4);
         uint32_t *coefw = reinterpret_cast<uint32_t *>(rec + 4 + K4);
@@ -688,7 +740,15 @@ __global__ void __launch_bounds__(kPrepThreads) decode_prep_lagrange(PrepArgs a)
             for (int b = 0; b < 4; ++b) {
                 const int j = 4 * d + b;
                 if (j < K) {
-                    const int ex = (ln + 510 - (int)s_log[xm ^ xpt(s_src[j])] - (int)s_lden[j]) % 255;
+                    int ex;
+                    if (KFEC_PREP_COEF2) {
+                        // one LDS level less (the column's point is stored), and the exponent in [2, 764] brought
+                        // under the 510-entry antilog table by one compare instead of a modulo
+                        ex = ln + 510 - (int)s_log[xm ^ s_xs[j]] - (int)s_lden[j];
+                        ex = ex >= 510 ? ex - 255 : ex;
+                    } else {
+                        ex = (ln + 510 - (int)s_log[xm ^ xpt(s_src[j])] - (int)s_lden[j]) % 255;
+                    }
                     v |= (uint32_t)s_exp[ex] << (8 * b);
                 }
             }
