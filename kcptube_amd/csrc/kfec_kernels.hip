@@ -60,12 +60,6 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #ifndef KFEC_SYN_TPRE
 #define KFEC_SYN_TPRE 1  // syn_loop: the next shard's E tables loaded into SGPRs one shard ahead (0: at use; A/B knob)
 #endif
-#ifndef KFEC_ENC_SCALAR
-#define KFEC_ENC_SCALAR 0  // 1: encode for R <= 8 through enc_scalar_kernel (E tables in SGPRs; A/B knob: slower)
-#endif
-#ifndef KFEC_SYN_LDSE
-#define KFEC_SYN_LDSE 0  // 1: syn_kernel stages the E tables in LDS, read as broadcasts (A/B knob: slower than scalar loads)
-#endif
 #ifndef KFEC_PREP_FUSED
 #define KFEC_PREP_FUSED 1  // decode_prep_lagrange: denominators and numerators in one pass (0: two loops; A/B knob)
 #endif
@@ -1173,7 +1167,6 @@ struct SynArgs {
     const uint32_t *list_count;
     uint64_t pitch;
     uint32_t total, cols, cols_pad, G, K, R, B, rec_stride, etab_rows;
-    uint32_t lds_e;           // syn_kernel: 1 = E tables staged in LDS after the C tables (KFEC_SYN_LDSE)
 };
 
 template <int RT>
@@ -1237,33 +1230,23 @@ __device__ __forceinline__ void syn_expand_one(const uint8_t *rec, uint32_t ur, 
 // A group that lost m data shards uses m parity rows: syn_list_kernel (one group per task, so the mask is
 // uniform) leaves out the rows its group does not use -- at ~1% loss mostly 2 of 3 (fec=20:3 listed decode
 // 1.41 -> 1.23 ms, profiles/r04_rowmask_ab.txt).
-template <int VEC, int RT, int PD, uint32_t ROWS = (1u << RT) - 1u, bool ENC = false, bool LDSE = false>
+template <int VEC, int RT, int PD, uint32_t ROWS = (1u << RT) - 1u>
 __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][Gran<VEC>::W], __amdgpu_buffer_rsrc_t rd,
                                          __amdgpu_buffer_rsrc_t rp, uint32_t drow, uint32_t prow, uint32_t used,
-                                         uint64_t p0, const uint8_t *rec, const uint32_t *lds_e = nullptr)
+                                         uint64_t p0, const uint8_t *rec)
 {
     constexpr int W = Gran<VEC>::W;
     const uint32_t K = a.K, pitch = (uint32_t)a.pitch;
-    // the parity shares of the rows in use start the accumulators (issued with the first data loads);
-    // ENC (encode): zero, and every data shard is present
+    // the parity shares of the rows in use start the accumulators (issued with the first data loads)
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
-        if constexpr (ENC) {
+        const Gran<VEC> y = bload<VEC>(rp, ((used >> r) & 1u) ? prow + r * pitch : kAbsent);
 #pragma unroll
-            for (int w = 0; w < W; ++w) acc[r][w] = 0;
-        } else {
-            const Gran<VEC> y = bload<VEC>(rp, ((used >> r) & 1u) ? prow + r * pitch : kAbsent);
-#pragma unroll
-            for (int w = 0; w < W; ++w) acc[r][w] = y.d[w];
-        }
+        for (int w = 0; w < W; ++w) acc[r][w] = y.d[w];
     }
-    uint64_t p1 = 0, p2 = 0, p3 = 0;
-    if constexpr (!ENC) {
-        const uint64_t *pr = reinterpret_cast<const uint64_t *>(rec + 8);
-        p1 = K > 64 ? pr[1] : 0ull; p2 = K > 128 ? pr[2] : 0ull; p3 = K > 192 ? pr[3] : 0ull;
-    }
+    const uint64_t *pr = reinterpret_cast<const uint64_t *>(rec + 8);
+    const uint64_t p1 = K > 64 ? pr[1] : 0ull, p2 = K > 128 ? pr[2] : 0ull, p3 = K > 192 ? pr[3] : 0ull;
     auto dofs = [&](uint32_t j) -> uint32_t {
-        if constexpr (ENC) return drow + j * pitch;
         const uint64_t wq = j < 64 ? p0 : (j < 128 ? p1 : (j < 192 ? p2 : p3));
         return ((wq >> (j & 63u)) & 1ull) ? drow + j * pitch : kAbsent;
     };
@@ -1274,17 +1257,10 @@ __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][G
 #pragma unroll
         for (int i = 0; i < 5 * RT; ++i) tn[i] = tg[i];
     };
-    if (KFEC_SYN_TPRE && !LDSE) tload(0);
+    if (KFEC_SYN_TPRE) tload(0);
     auto mac = [&](const Gran<VEC> &cur, uint32_t j) {
-        uint32_t t[SynLayout<RT>::TD];
-        if constexpr (LDSE) {  // [K][TD] tables in LDS (syn_kernel stages them), broadcast reads
-            const uint4 *tv = reinterpret_cast<const uint4 *>(lds_e + j * SynLayout<RT>::TD);
-#pragma unroll
-            for (int i = 0; i < SynLayout<RT>::TD / 4; ++i) {
-                const uint4 q = tv[i];
-                t[4 * i] = q.x; t[4 * i + 1] = q.y; t[4 * i + 2] = q.z; t[4 * i + 3] = q.w;
-            }
-        } else if (KFEC_SYN_TPRE) {
+        uint32_t t[5 * RT];
+        if (KFEC_SYN_TPRE) {
 #pragma unroll
             for (int i = 0; i < 5 * RT; ++i) t[i] = tn[i];
             tload(j + 1);
@@ -1485,15 +1461,6 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
         syn_expand_one<RT>(a.rec + (uint64_t)(gfirst + gs) * a.rec_stride, e - gs * (RT * RT), s_ct + gs * RT * TD);
     }
 #endif
-    // E tables of every shard, [K][TD] after the C tables (one copy per workgroup; a uniform flag)
-    uint32_t *s_e = s_ct + (KFEC_SYN_WAVE_CT ? (kMacBlock / 64) * syn_wave_groups(cols) : min(a.G, (kMacBlock - 1) / cols + 2)) * RT * TD;
-    if (KFEC_SYN_LDSE && a.lds_e) {
-        for (uint32_t i = threadIdx.x; i < K * TD; i += kMacBlock) {
-            const uint32_t j = i / TD, k = i - j * TD;
-            s_e[i] = k < 5 * RT ? a.etab[(size_t)j * a.etab_rows * 5 + k] : 0u;
-        }
-        __syncthreads();
-    }
     const uint32_t item = base + threadIdx.x;
     const bool in = item < a.total;
     const uint32_t g = in ? item / cols : gfirst;
@@ -1522,12 +1489,8 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
             (void *)(a.data + (uint64_t)gfirst * K * a.pitch), (short)0, (int)(ngr * K * a.pitch), 0x00020000);
         const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(a.parity + (uint64_t)gfirst * a.R * a.pitch), (short)0, (int)(ngr * a.R * a.pitch), 0x00020000);
-        if (KFEC_SYN_LDSE && a.lds_e)
-            syn_loop<VEC, RT, PD, (1u << RT) - 1u, false, true>(a, acc, rd, rp, gs * K * (uint32_t)a.pitch + off,
-                                                                gs * a.R * (uint32_t)a.pitch + off, used, p0, rec, s_e);
-        else
-            syn_loop<VEC, RT, PD>(a, acc, rd, rp, gs * K * (uint32_t)a.pitch + off, gs * a.R * (uint32_t)a.pitch + off,
-                                  used, p0, rec);
+        syn_loop<VEC, RT, PD>(a, acc, rd, rp, gs * K * (uint32_t)a.pitch + off, gs * a.R * (uint32_t)a.pitch + off, used,
+                              p0, rec);
     }
 #if KFEC_SYN_WAVE_CT
 #if KFEC_SYN_EARLY
@@ -1545,36 +1508,6 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
     __syncthreads();  // C tables
     if (active) syn_final<VEC, RT>(a, acc, s_ct + gs * RT * TD, m, g, off, col);
 #endif
-}
-
-// Encode for R <= 8 with the syndrome decode's loop (KFEC_ENC_SCALAR): parity_r = XOR_j E[r][j] * D_j, lane =
-// (group, column) in the flattened item order, the E tables read with scalar loads one shard ahead (no LDS, no
-// workgroup barrier), the data through one buffer resource over the workgroup's groups.
-template <int VEC, int RT, int PDX>
-__global__ void __launch_bounds__(kMacBlock) enc_scalar_kernel(SynArgs a)
-{
-    constexpr int W = Gran<VEC>::W;
-    constexpr int PD = PDX ? PDX : (VEC >= 32 ? KFEC_PD : 2 * KFEC_PD);
-    const uint32_t base = blockIdx.x * kMacBlock;
-    if (base >= a.total) return;
-    const uint32_t cols = a.cols, K = a.K;
-    const uint32_t gfirst = base / cols;
-    const uint32_t item = base + threadIdx.x;
-    const bool in = item < a.total;
-    const uint32_t g = in ? item / cols : gfirst;
-    const uint32_t col = in ? item - g * cols : 0;
-    const uint32_t off = gran_off<VEC>(col, a.B);
-    const uint32_t ngr = min(base + kMacBlock - 1, a.total - 1) / cols - gfirst + 1;
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(a.data + (uint64_t)gfirst * K * a.pitch), (short)0, (int)(ngr * K * a.pitch), 0x00020000);
-    uint32_t acc[RT][W];
-    syn_loop<VEC, RT, PD, (1u << RT) - 1u, true>(a, acc, rd, rd, (g - gfirst) * K * (uint32_t)a.pitch + off, 0, 0,
-                                                 0, nullptr);
-    if (!in) return;
-    const uint64_t obase = (uint64_t)g * a.R * a.pitch + off;
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-        if ((uint32_t)r < a.R) store_gran<VEC>(a.out + obase + (uint64_t)r * a.pitch, acc[r], col, a.B);
 }
 
 // ---- ordered list of the groups with data to recover (out_idx[g * R] != 0xFF), for syn_kernel's listed
@@ -1817,32 +1750,6 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     const int tiles = (R + mt - 1) / mt;
     const size_t ent = entry_bytes(mt);
     const uint32_t JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / ent));
-    // (scalar-table encode: the workgroup's groups must fit one buffer resource)
-    const size_t gmax_wg = (kMacBlock - 1) / cols + 2;
-    if (KFEC_ENC_SCALAR && vec == 32 && R <= 8 && gmax_wg * (size_t)K * pitch < (size_t(1) << 31)) {
-        const int rt = syn_rt(R);
-        return for_group_ranges(G, cols, 1, [&](size_t g0, size_t gn) {
-            SynArgs a{};
-            a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
-            a.out = static_cast<uint8_t *>(d_parity) + g0 * R * pitch;
-            a.etab = reinterpret_cast<const uint32_t *>(d_enc + enc_tab_offset(K, N));
-            a.etab_rows = (uint32_t)enc_tab_rows(R);
-            a.pitch = pitch;
-            a.total = (uint32_t)(gn * cols);
-            a.cols = (uint32_t)cols;
-            a.G = (uint32_t)gn;
-            a.K = K; a.R = R; a.B = (uint32_t)B;
-            const uint32_t nb = std::max(1u, (a.total + kMacBlock - 1) / kMacBlock);
-            switch (rt) {
-            case 1: hipLaunchKernelGGL((enc_scalar_kernel<32, 1, 0>), dim3(nb), dim3(kMacBlock), 0, s, a); break;
-            case 2: hipLaunchKernelGGL((enc_scalar_kernel<32, 2, 0>), dim3(nb), dim3(kMacBlock), 0, s, a); break;
-            case 3: hipLaunchKernelGGL((enc_scalar_kernel<32, 3, 0>), dim3(nb), dim3(kMacBlock), 0, s, a); break;
-            case 4: hipLaunchKernelGGL((enc_scalar_kernel<32, 4, 0>), dim3(nb), dim3(kMacBlock), 0, s, a); break;
-            default: hipLaunchKernelGGL((enc_scalar_kernel<32, 8, 0>), dim3(nb), dim3(kMacBlock), 0, s, a); break;
-            }
-            return hipGetLastError() == hipSuccess ? 0 : -3;
-        });
-    }
     return for_group_ranges(G, cols, tiles, [&](size_t g0, size_t gn) {
         MacArgs a{};
         a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
@@ -1936,10 +1843,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         uint32_t *chunk_cnt = count + 64;
         uint32_t *list = chunk_cnt + decode_list_chunks(G);
         const size_t cols_pad = (cols + 63) / 64 * 64;
-        // E tables in LDS when they fit beside the C tables (KFEC_SYN_LDSE)
-        const size_t lds_e = (size_t)K * syn_td(rt) * 4;
-        const bool use_lds_e = KFEC_SYN_LDSE && lds_syn + lds_e <= kSynLdsMax;
-        const size_t lds = lds_syn + (use_lds_e ? lds_e : 0);
+        const size_t lds = lds_syn;
         return for_group_ranges(G, cols, 1, [&](size_t g0, size_t gn) {
             // the ordered list of this launch's groups with data to recover, and its length, on the device
             // (not for the latency shape's few groups: there the dense kernel alone runs, two launches fewer
@@ -1970,7 +1874,6 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
             a.G = (uint32_t)gn;
             a.K = K; a.R = R; a.B = (uint32_t)B;
             a.rec_stride = (uint32_t)rs;
-            a.lds_e = use_lds_e ? 1u : 0u;
             return dispatch_syn(vec, rt, a, lds, di.cus, s);
         });
     }
