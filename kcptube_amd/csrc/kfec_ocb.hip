@@ -214,6 +214,8 @@ struct OcbLds<false> {
     uint4 rk[15];
     uint4 dk[15];
     uint4 l[32];
+    uint4 rkr[15];              // the round keys with every word rotated by 16 (tcol folds the key into the rotate)
+    uint4 dkr[15];
     uint32_t te[256][2][kRep];  // row v: the 32 copies of Te0[v], then of Te1[v] (256 B)
 };
 template <>
@@ -221,6 +223,8 @@ struct OcbLds<true> {
     uint4 rk[15];
     uint4 dk[15];
     uint4 l[32];
+    uint4 rkr[15];
+    uint4 dkr[15];
     uint32_t td[256][2][kRep];
     uint32_t isb[64][kRep];
     uint32_t te0[256];
@@ -244,12 +248,13 @@ __device__ __forceinline__ uint32_t rep_at(const uint32_t (*T)[2][kRep], uint32_
     return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(T) + o + 128 * J);
 }
 
-// one column of a round: T0[b0(a)] ^ T1[b1(b)] ^ rotl16(T0[b2(cc)] ^ T1[b3(d)]) ^ k
+// one column of a round: T0[b0(a)] ^ T1[b1(b)] ^ rotl16(T0[b2(cc)] ^ T1[b3(d)]) ^ k, with kr = rotl16(k) folded
+// into the rotated half: rotl16(T0[..] ^ T1[..] ^ kr) = rotl16(T0[..] ^ T1[..]) ^ k -- three VALU ops, not four
 __device__ __forceinline__ uint32_t tcol(const uint32_t (*T)[2][kRep], uint32_t c4, uint32_t a, uint32_t b, uint32_t cc,
-                                         uint32_t d, uint32_t k)
+                                         uint32_t d, uint32_t kr)
 {
-    const uint32_t hi = rep_at<0, 2>(T, cc, c4) ^ rep_at<1, 3>(T, d, c4);
-    return xor3(rep_at<0, 0>(T, a, c4), rep_at<1, 1>(T, b, c4), rotl(hi, 16)) ^ k;
+    const uint32_t hi = xor3(rep_at<0, 2>(T, cc, c4), rep_at<1, 3>(T, d, c4), kr);
+    return xor3(rep_at<0, 0>(T, a, c4), rep_at<1, 1>(T, b, c4), rotl(hi, 16));
 }
 
 // Te0 holds S(x) in byte 1 (Te0[x] = {2S, S, S, 3S})
@@ -264,7 +269,7 @@ __device__ __forceinline__ uint4 aes_enc(const OcbLds<false> &t, uint32_t c4, ui
     uint32_t s0 = in.x ^ t.rk[0].x, s1 = in.y ^ t.rk[0].y, s2 = in.z ^ t.rk[0].z, s3 = in.w ^ t.rk[0].w;
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
-        const uint4 k = t.rk[r];
+        const uint4 k = t.rkr[r];
         const uint32_t t0 = tcol(t.te, c4, s0, s1, s2, s3, k.x);
         const uint32_t t1 = tcol(t.te, c4, s1, s2, s3, s0, k.y);
         const uint32_t t2 = tcol(t.te, c4, s2, s3, s0, s1, k.z);
@@ -316,7 +321,7 @@ __device__ __forceinline__ uint4 aes_dec(const OcbLds<true> &t, uint32_t c4, uin
     uint32_t s0 = in.x ^ t.dk[0].x, s1 = in.y ^ t.dk[0].y, s2 = in.z ^ t.dk[0].z, s3 = in.w ^ t.dk[0].w;
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
-        const uint4 k = t.dk[r];
+        const uint4 k = t.dkr[r];
         // InvShiftRows: output column c row r takes input column c - r
         const uint32_t t0 = tcol(t.td, c4, s0, s3, s2, s1, k.x);
         const uint32_t t1 = tcol(t.td, c4, s1, s0, s3, s2, k.y);
@@ -340,7 +345,7 @@ __device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, uint32_t c4, ui
     uint32_t u0 = y.x ^ t.rk[0].x, u1 = y.y ^ t.rk[0].y, u2 = y.z ^ t.rk[0].z, u3 = y.w ^ t.rk[0].w;
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
-        const uint4 k = t.rk[r];
+        const uint4 k = t.rkr[r];
         const uint32_t t0 = tcol(t.te, c4, s0, s1, s2, s3, k.x);
         const uint32_t v0 = tcol(t.te, c4, u0, u1, u2, u3, k.x);
         const uint32_t t1 = tcol(t.te, c4, s1, s2, s3, s0, k.y);
@@ -367,7 +372,7 @@ __device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, uint32_t c4, uin
     uint32_t u0 = y.x ^ t.dk[0].x, u1 = y.y ^ t.dk[0].y, u2 = y.z ^ t.dk[0].z, u3 = y.w ^ t.dk[0].w;
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
-        const uint4 k = t.dk[r];
+        const uint4 k = t.dkr[r];
         const uint32_t t0 = tcol(t.td, c4, s0, s3, s2, s1, k.x);
         const uint32_t v0 = tcol(t.td, c4, u0, u3, u2, u1, k.x);
         const uint32_t t1 = tcol(t.td, c4, s1, s0, s3, s2, k.y);
@@ -418,6 +423,8 @@ __global__ void __launch_bounds__(kOcbBlock, 4) ocb_kernel(OcbArgs a)  // (4 wav
             const int src = i < 120 ? i : i + 8;
             s32[i] = k32[src];
         }
+        uint32_t *r32 = reinterpret_cast<uint32_t *>(s.rkr);  // rkr then dkr, as rk then dk
+        for (int i = threadIdx.x; i < 120; i += kOcbBlock) r32[i] = rotl(k32[i], 16);
         if constexpr (OPEN) {
             for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
                 s.td[i / (2 * kRep)][i / kRep % 2][i % kRep] = a.key->td[i / kRep % 2][i / (2 * kRep)];
