@@ -175,6 +175,9 @@ __global__ void ocb_iv_kernel(const uint32_t *key, uint4 *off0)
 #ifndef KFEC_OCB_BITOP3
 #define KFEC_OCB_BITOP3 1  // byte-1 table addresses by v_bitop3_b32 instead of v_perm_b32 (A/B knob)
 #endif
+#ifndef KFEC_OCB_PAIR
+#define KFEC_OCB_PAIR 1  // two-block cipher: two rounds per loop trip, no register moves between trips (A/B knob)
+#endif
 #ifndef KFEC_OCB_ILP
 #define KFEC_OCB_ILP 2  // full blocks per lane through the AES rounds together (1 or 2; A/B knob)
 #endif
@@ -343,6 +346,32 @@ __device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, uint32_t c4, ui
 {
     uint32_t s0 = x.x ^ t.rk[0].x, s1 = x.y ^ t.rk[0].y, s2 = x.z ^ t.rk[0].z, s3 = x.w ^ t.rk[0].w;
     uint32_t u0 = y.x ^ t.rk[0].x, u1 = y.y ^ t.rk[0].y, u2 = y.z ^ t.rk[0].z, u3 = y.w ^ t.rk[0].w;
+#if KFEC_OCB_PAIR
+    // rounds 1 .. 13, two per loop trip with the state alternating between (s, u) and (p, q), so no trip
+    // ends in register moves
+    auto round = [&](int r, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t b0, uint32_t b1,
+                     uint32_t b2, uint32_t b3, uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3, uint32_t &e0,
+                     uint32_t &e1, uint32_t &e2, uint32_t &e3) {
+        const uint4 k = t.rkr[r];
+        o0 = tcol(t.te, c4, a0, a1, a2, a3, k.x);
+        e0 = tcol(t.te, c4, b0, b1, b2, b3, k.x);
+        o1 = tcol(t.te, c4, a1, a2, a3, a0, k.y);
+        e1 = tcol(t.te, c4, b1, b2, b3, b0, k.y);
+        o2 = tcol(t.te, c4, a2, a3, a0, a1, k.z);
+        e2 = tcol(t.te, c4, b2, b3, b0, b1, k.z);
+        o3 = tcol(t.te, c4, a3, a0, a1, a2, k.w);
+        e3 = tcol(t.te, c4, b3, b0, b1, b2, k.w);
+    };
+    uint32_t p0, p1, p2, p3, q0, q1, q2, q3;
+    round(1, s0, s1, s2, s3, u0, u1, u2, u3, p0, p1, p2, p3, q0, q1, q2, q3);
+#pragma unroll 1
+    for (int r = 2; r < 14; r += 2) {
+        round(r, p0, p1, p2, p3, q0, q1, q2, q3, s0, s1, s2, s3, u0, u1, u2, u3);
+        round(r + 1, s0, s1, s2, s3, u0, u1, u2, u3, p0, p1, p2, p3, q0, q1, q2, q3);
+    }
+    s0 = p0; s1 = p1; s2 = p2; s3 = p3;
+    u0 = q0; u1 = q1; u2 = q2; u3 = q3;
+#else
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
         const uint4 k = t.rkr[r];
@@ -357,6 +386,7 @@ __device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, uint32_t c4, ui
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
         u0 = v0; u1 = v1; u2 = v2; u3 = v3;
     }
+#endif
     const uint4 k = t.rk[14];
     const uint32_t (*T)[2][kRep] = t.te;
     auto last = [&](uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
@@ -370,6 +400,30 @@ __device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, uint32_t c4, uin
 {
     uint32_t s0 = x.x ^ t.dk[0].x, s1 = x.y ^ t.dk[0].y, s2 = x.z ^ t.dk[0].z, s3 = x.w ^ t.dk[0].w;
     uint32_t u0 = y.x ^ t.dk[0].x, u1 = y.y ^ t.dk[0].y, u2 = y.z ^ t.dk[0].z, u3 = y.w ^ t.dk[0].w;
+#if KFEC_OCB_PAIR
+    auto round = [&](int r, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t b0, uint32_t b1,
+                     uint32_t b2, uint32_t b3, uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3, uint32_t &e0,
+                     uint32_t &e1, uint32_t &e2, uint32_t &e3) {
+        const uint4 k = t.dkr[r];
+        o0 = tcol(t.td, c4, a0, a3, a2, a1, k.x);
+        e0 = tcol(t.td, c4, b0, b3, b2, b1, k.x);
+        o1 = tcol(t.td, c4, a1, a0, a3, a2, k.y);
+        e1 = tcol(t.td, c4, b1, b0, b3, b2, k.y);
+        o2 = tcol(t.td, c4, a2, a1, a0, a3, k.z);
+        e2 = tcol(t.td, c4, b2, b1, b0, b3, k.z);
+        o3 = tcol(t.td, c4, a3, a2, a1, a0, k.w);
+        e3 = tcol(t.td, c4, b3, b2, b1, b0, k.w);
+    };
+    uint32_t p0, p1, p2, p3, q0, q1, q2, q3;
+    round(1, s0, s1, s2, s3, u0, u1, u2, u3, p0, p1, p2, p3, q0, q1, q2, q3);
+#pragma unroll 1
+    for (int r = 2; r < 14; r += 2) {
+        round(r, p0, p1, p2, p3, q0, q1, q2, q3, s0, s1, s2, s3, u0, u1, u2, u3);
+        round(r + 1, s0, s1, s2, s3, u0, u1, u2, u3, p0, p1, p2, p3, q0, q1, q2, q3);
+    }
+    s0 = p0; s1 = p1; s2 = p2; s3 = p3;
+    u0 = q0; u1 = q1; u2 = q2; u3 = q3;
+#else
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
         const uint4 k = t.dkr[r];
@@ -384,6 +438,7 @@ __device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, uint32_t c4, uin
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
         u0 = v0; u1 = v1; u2 = v2; u3 = v3;
     }
+#endif
     const uint4 k = t.dk[14];
     auto last = [&](uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
         return isb<0>(t, c4, a0) | isb<1>(t, c4, a1) << 8 | isb<2>(t, c4, a2) << 16 | isb<3>(t, c4, a3) << 24;
