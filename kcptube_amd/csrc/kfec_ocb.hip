@@ -263,7 +263,10 @@ __device__ __forceinline__ uint32_t tcol(const uint32_t (*T)[2][kRep], uint32_t 
 // Te0 holds S(x) in byte 1 (Te0[x] = {2S, S, S, 3S})
 __device__ __forceinline__ uint32_t sbox_col(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3)
 {
-    return ((w0 >> 8) & 0xFFu) | (w1 & 0xFF00u) | ((w2 << 8) & 0xFF0000u) | ((w3 << 16) & 0xFF000000u);
+    // byte 1 of each word: two v_perm_b32 gather two bytes each, one OR joins the halves
+    const uint32_t lo = __builtin_amdgcn_perm(w1, w0, 0x0C0C0501u);  // {w0.b1, w1.b1, 0, 0}
+    const uint32_t hi = __builtin_amdgcn_perm(w3, w2, 0x05010C0Cu);  // {0, 0, w2.b1, w3.b1}
+    return lo | hi;
 }
 
 // encryption from the replicated tables (seal), row lane c (c4 = 4 c)
