@@ -206,10 +206,13 @@ struct OcbArgs {
 // and the 32 lanes of a read hit 32 different banks whatever their bytes: no conflicts.  Te2 / Te3 are Te0 /
 // Te1 rotated by 16 bits (Td likewise), so a column is T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d]) ^ k: two
 // replicated tables and one rotate per column.
-//   seal: te[v][j][c] = Te_j[v], j = 0, 1 (64 KiB).  open: td[v][j][c] = Td_j[v] (64 KiB), isb[w][c] = the
+//   seal: te[v][j][c] = Te_j[v], j = 0, 1 (64 KiB).  open: td[v][j][c] = Td_j[v] (64 KiB), isb4 / isb = the
 //   inverse S-box bytes 4w .. 4w + 3 (8 KiB), and Te0 once (the pad of a partial block and the tag: at most
 //   two blocks per packet).
 constexpr int kRep = 32;
+#ifndef KFEC_OCB_ISB4
+#define KFEC_OCB_ISB4 1  // open's last round from a byte-replicated InvS table, columns joined by permutes (A/B knob)
+#endif
 template <bool OPEN>
 struct OcbLds;
 template <>
@@ -229,7 +232,11 @@ struct OcbLds<true> {
     uint4 rkr[15];
     uint4 dkr[15];
     uint32_t td[256][2][kRep];
+#if KFEC_OCB_ISB4
+    uint32_t isb4[256][8];  // row v: 8 copies of InvS(v) in all four bytes (8 KiB; copy = lane % 8)
+#else
     uint32_t isb[64][kRep];
+#endif
     uint32_t te0[256];
 };
 
@@ -313,6 +320,25 @@ __device__ __forceinline__ uint4 aes_enc(const OcbLds<true> &t, uint32_t, uint4 
     return make_uint4(o0 ^ k.x, o1 ^ k.y, o2 ^ k.z, o3 ^ k.w);
 }
 
+#if KFEC_OCB_ISB4
+// InvS of byte K of x, replicated in all four bytes: row v is 32 bytes, so the offset is byte K of x in bits
+// 5..12 and 4 (lane % 8) in bits 2..4 (c4 & 31)
+template <int K>
+__device__ __forceinline__ uint32_t isb4_at(const OcbLds<true> &t, uint32_t c4, uint32_t x)
+{
+    const uint32_t o = (K == 0 ? x << 5 : x >> (8 * K - 5)) & 0x1FE0u;
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(t.isb4) + (o | (c4 & 31u)));
+}
+
+// the last round's column: InvS of byte 0 of a0, byte 1 of a1, byte 2 of a2, byte 3 of a3, joined by permutes
+__device__ __forceinline__ uint32_t isb_col(const OcbLds<true> &t, uint32_t c4, uint32_t a0, uint32_t a1, uint32_t a2,
+                                            uint32_t a3)
+{
+    const uint32_t lo = __builtin_amdgcn_perm(isb4_at<1>(t, c4, a1), isb4_at<0>(t, c4, a0), 0x0C0C0400u);
+    const uint32_t hi = __builtin_amdgcn_perm(isb4_at<3>(t, c4, a3), isb4_at<2>(t, c4, a2), 0x04000C0Cu);
+    return lo | hi;
+}
+#else
 // inverse S-box byte K of x from the replicated packed table
 template <int K>
 __device__ __forceinline__ uint32_t isb(const OcbLds<true> &t, uint32_t c4, uint32_t x)
@@ -320,6 +346,13 @@ __device__ __forceinline__ uint32_t isb(const OcbLds<true> &t, uint32_t c4, uint
     const uint32_t v = (x >> (8 * K)) & 0xFFu;
     return (t.isb[v >> 2][c4 >> 2] >> (8 * (v & 3u))) & 0xFFu;
 }
+
+__device__ __forceinline__ uint32_t isb_col(const OcbLds<true> &t, uint32_t c4, uint32_t a0, uint32_t a1, uint32_t a2,
+                                            uint32_t a3)
+{
+    return isb<0>(t, c4, a0) | isb<1>(t, c4, a1) << 8 | isb<2>(t, c4, a2) << 16 | isb<3>(t, c4, a3) << 24;
+}
+#endif
 
 // the equivalent inverse cipher (FIPS 197 5.3.5) from the replicated Td0 / Td1, row lane c (c4 = 4 c)
 __device__ __forceinline__ uint4 aes_dec(const OcbLds<true> &t, uint32_t c4, uint4 in)
@@ -336,10 +369,10 @@ __device__ __forceinline__ uint4 aes_dec(const OcbLds<true> &t, uint32_t c4, uin
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     const uint4 k = t.dk[14];
-    const uint32_t o0 = isb<0>(t, c4, s0) | isb<1>(t, c4, s3) << 8 | isb<2>(t, c4, s2) << 16 | isb<3>(t, c4, s1) << 24;
-    const uint32_t o1 = isb<0>(t, c4, s1) | isb<1>(t, c4, s0) << 8 | isb<2>(t, c4, s3) << 16 | isb<3>(t, c4, s2) << 24;
-    const uint32_t o2 = isb<0>(t, c4, s2) | isb<1>(t, c4, s1) << 8 | isb<2>(t, c4, s0) << 16 | isb<3>(t, c4, s3) << 24;
-    const uint32_t o3 = isb<0>(t, c4, s3) | isb<1>(t, c4, s2) << 8 | isb<2>(t, c4, s1) << 16 | isb<3>(t, c4, s0) << 24;
+    const uint32_t o0 = isb_col(t, c4, s0, s3, s2, s1);
+    const uint32_t o1 = isb_col(t, c4, s1, s0, s3, s2);
+    const uint32_t o2 = isb_col(t, c4, s2, s1, s0, s3);
+    const uint32_t o3 = isb_col(t, c4, s3, s2, s1, s0);
     return make_uint4(o0 ^ k.x, o1 ^ k.y, o2 ^ k.z, o3 ^ k.w);
 }
 
@@ -444,7 +477,7 @@ __device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, uint32_t c4, uin
 #endif
     const uint4 k = t.dk[14];
     auto last = [&](uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
-        return isb<0>(t, c4, a0) | isb<1>(t, c4, a1) << 8 | isb<2>(t, c4, a2) << 16 | isb<3>(t, c4, a3) << 24;
+        return isb_col(t, c4, a0, a1, a2, a3);
     };
     x = make_uint4(last(s0, s3, s2, s1) ^ k.x, last(s1, s0, s3, s2) ^ k.y, last(s2, s1, s0, s3) ^ k.z, last(s3, s2, s1, s0) ^ k.w);
     y = make_uint4(last(u0, u3, u2, u1) ^ k.x, last(u1, u0, u3, u2) ^ k.y, last(u2, u1, u0, u3) ^ k.z, last(u3, u2, u1, u0) ^ k.w);
@@ -486,11 +519,15 @@ __global__ void __launch_bounds__(kOcbBlock, 4) ocb_kernel(OcbArgs a)  // (4 wav
         if constexpr (OPEN) {
             for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
                 s.td[i / (2 * kRep)][i / kRep % 2][i % kRep] = a.key->td[i / kRep % 2][i / (2 * kRep)];
+#if KFEC_OCB_ISB4
+            for (int i = threadIdx.x; i < 256 * 8; i += kOcbBlock) s.isb4[i / 8][i % 8] = a.key->isb[i / 8] * 0x01010101u;
+#else
             for (int i = threadIdx.x; i < 64 * kRep; i += kOcbBlock) {
                 const int w = i / kRep;
                 s.isb[w][i % kRep] = a.key->isb[4 * w] | a.key->isb[4 * w + 1] << 8 | a.key->isb[4 * w + 2] << 16 |
                                      a.key->isb[4 * w + 3] << 24;
             }
+#endif
             for (int i = threadIdx.x; i < 256; i += kOcbBlock) s.te0[i] = a.key->te[0][i];
         } else {
             for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
