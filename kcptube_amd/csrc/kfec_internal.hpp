@@ -16,7 +16,7 @@ namespace kfec {
 //   [4+K4, 4+K4+R*K4)      coef[u][j] row u (u < m) of the inverse decode matrix for missing shard u,
 // with K4 = K rounded up to 4 so that the prep kernel writes whole dwords.  Syndrome form (R <= 8, see
 // write_syn in kfec_kernels.hip): [0] status, [1] m, [2] used-parity bits, [8, 40) present data bits,
-// [40, 104) the 8 x 8 C matrix.
+// [40, 40 + 8 RT) the RT rows of the C matrix (RT = R up to 4, else 8; kfec_kernels.hip syn_record_stride).
 inline size_t rec_k4(size_t K) { return (K + 3) & ~size_t(3); }
 inline size_t record_stride(size_t K, size_t R)
 {

@@ -75,6 +75,9 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #ifndef KFEC_PREP_MINW
 #define KFEC_PREP_MINW 8  // decode_prep_lagrange: minimum waves per SIMD (8: 64 VGPRs, 12 spilled, 3% faster than uncapped)
 #endif
+#ifndef KFEC_SYN_REC_COMPACT
+#define KFEC_SYN_REC_COMPACT 1  // syndrome records of 40 + 8 RT bytes (64 at R = 3: one full line per group)
+#endif
 #ifndef KFEC_SYN_ROWMASK
 #define KFEC_SYN_ROWMASK 1  // listed syndrome decode: 0 every parity row, 1 only the rows the group uses,
                             // 2 as 1 but single-row groups run a two-row variant (A/B knob)
@@ -238,8 +241,16 @@ __device__ __forceinline__ void write_empty(const PrepArgs &a, uint64_t g, uint8
 // Syndrome-form record (syn_kernel, R <= 8): [0] status 0, [1] m, [2] bit r set = parity row K + r is one
 // of the m shares used, [3..7] 0, [8, 40) the present DATA shard bits (4 x u64, so the MAC kernel gets
 // its header and the first 64 bits in one 16-byte load), [40 + 8u + r] = C[u][r] = Sinv[u][t] for the rank
-// t with P_t = K + r (0 for unused rows and for u >= m): all 8 rows are written so any row tile RT <= 8
-// reads zeros beyond m.
+// t with P_t = K + r (0 for unused rows and for u >= m): rows u < RT are written (the ones the syn kernels
+// read), so the kernels read zeros beyond m.
+// Row tile of the syndrome form (the C rows a syn kernel reads: RT x RT bytes) and the record stride: the
+// header, the present bits and RT rows of C -- 64 bytes at R = 3, one whole line per group
+__host__ __device__ constexpr int syn_rt(int R) { return R <= 4 ? (R > 0 ? R : 1) : 8; }
+__host__ __device__ inline size_t syn_record_stride(size_t K, size_t R)
+{
+    return KFEC_SYN_REC_COMPACT ? (size_t)((40 + 8 * syn_rt((int)R) + 15) & ~15) : record_stride(K, R);
+}
+
 template <int MAXM, typename F>
 __device__ __forceinline__ void write_syn(const PrepArgs &a, uint64_t g, int m, const int (&M)[MAXM],
                                           const int (&P)[MAXM], const uint64_t (&w)[4], F sinv)
@@ -262,10 +273,11 @@ __device__ __forceinline__ void write_syn(const PrepArgs &a, uint64_t g, int m, 
     rw[0] = (uint64_t)(((uint32_t)m << 8) | (used << 16));
 #pragma unroll
     for (int q = 0; q < 4; ++q) rw[1 + q] = w[q] & bits_below(a.K, q);
+    // rows u < RT only (the record ends there); rows past m are zero
+    const int rt = syn_rt((int)a.R);
 #pragma unroll
-    for (int u = 0; u < MAXM; ++u) rw[5 + u] = row[u];
-#pragma unroll
-    for (int u = MAXM; u < 8; ++u) rw[5 + u] = 0;
+    for (int u = 0; u < 8; ++u)
+        if (u < rt) rw[5 + u] = u < MAXM ? row[u] : 0ull;
 #pragma unroll
     for (int t = 0; t < MAXM; ++t)
         if (t < a.R) a.out_idx[g * a.R + t] = (t < m) ? (uint8_t)M[t] : (uint8_t)0xFF;
@@ -1674,7 +1686,6 @@ static int entry_bytes(int mt)
     }
 }
 
-static int syn_rt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
 
 static size_t syn_td(int rt)
 {
@@ -1779,7 +1790,7 @@ int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N,
     const int R = N - K;
     if (G == 0) return 0;
     uint8_t *rec = static_cast<uint8_t *>(d_workspace);
-    const size_t rs = record_stride(K, R);
+    const size_t rs = syn ? syn_record_stride(K, R) : record_stride(K, R);
     PrepArgs p{};
     p.present = d_present;
     p.enc = d_enc;
@@ -1839,6 +1850,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s, syn)) return -3;
     if (R == 0 || B == 0) return 0;
     if (syn) {
+        const size_t rs_syn = syn_record_stride(K, R);  // (the prep wrote syndrome records)
         uint32_t *count = reinterpret_cast<uint32_t *>(rec + decode_list_offset(G, K, R));
         uint32_t *chunk_cnt = count + 64;
         uint32_t *list = chunk_cnt + decode_list_chunks(G);
@@ -1862,7 +1874,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
             a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
             a.parity = static_cast<const uint8_t *>(d_parity) + g0 * R * pitch;
             a.out = static_cast<uint8_t *>(d_out) + g0 * R * pitch;
-            a.rec = rec + g0 * rs;
+            a.rec = rec + g0 * rs_syn;
             a.etab = reinterpret_cast<const uint32_t *>(d_enc + enc_tab_offset(K, N));
             a.list = list;
             a.list_count = small ? nullptr : count;  // nullptr: dense only (syn_kernel runs, no listed launch)
@@ -1873,7 +1885,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
             a.cols_pad = (uint32_t)cols_pad;
             a.G = (uint32_t)gn;
             a.K = K; a.R = R; a.B = (uint32_t)B;
-            a.rec_stride = (uint32_t)rs;
+            a.rec_stride = (uint32_t)rs_syn;
             return dispatch_syn(vec, rt, a, lds, di.cus, s);
         });
     }
