@@ -238,6 +238,31 @@ class Calib:
         return 4 * 64 * 4 * cus / (3 * t_perm + t_bitop3 + t_xor)
 
 
+def device_ident(torch, dev, local_dev: int) -> str:
+    """host:PCI location of this rank's GPU (falls back to the device index): distinct GPUs of a job are the
+    distinct idents over its ranks, on one node or many."""
+    import socket
+    p = torch.cuda.get_device_properties(dev)
+    bus = getattr(p, "pci_bus_id", None)
+    loc = f"{getattr(p, 'pci_domain_id', 0):04x}:{bus:02x}:{getattr(p, 'pci_device_id', 0):02x}" if bus is not None else f"dev{local_dev}"
+    return f"{socket.gethostname()}:{loc}"
+
+
+def per_rank_summary(records: list[dict], value: float, payload_per_rank_step: list[float]) -> dict:
+    """Evidence for a multi-GPU line, from every rank's own record (gathered after the timed region):
+    distinct devices, and value / (world x rank 0's single-rank-equivalent rate) -- rank 0's own payload per
+    step over its own wall time per step -- so a 1->N curve shows whether one GPU (or one host launch queue)
+    held the job back.  (This is within one run; the driver computes the cross-N scaling efficiency itself.)"""
+    world = len(records)
+    r0 = records[0]
+    rate0 = payload_per_rank_step[0] / (r0["wall_ms_per_step"] * 1e-3) / 2**30 if r0["wall_ms_per_step"] else None
+    slowest = max(records, key=lambda r: r["wall_ms_per_step"])
+    return {"devices": len({r["device"] for r in records}),
+            "rank0_equivalent_GiBps": round(rate0, 2) if rate0 else None,
+            "scaling_efficiency": round(value / (world * rate0), 4) if rate0 else None,
+            "slowest_rank": slowest["rank"]}
+
+
 def rank_groups(groups_per_gpu: int, world: int, rank: int) -> tuple[int, int, int]:
     """(g0, g1, total): this rank's contiguous slice of the global group space (weak scaling:
     total = groups_per_gpu * world, split by kcptube_amd.partition.group_range)."""
@@ -303,14 +328,16 @@ def main():
     import torch
     import torch.distributed as dist
 
-    # (device_count does not initialise the GPU; refuse before the rendezvous and before any device work)
+    # (device_count does not initialise the GPU; refuse before the rendezvous and before any device work).
+    # Ranks per node (LOCAL_WORLD_SIZE, as torch.distributed.run sets it) against this node's GPUs: a multi-node
+    # world of 2 x 4 GPUs is 4 ranks per node on 4 devices, not 8 ranks on 4.
     n_dev = torch.cuda.device_count()
     rehearsal = rehearsal_allowed(args)
-    why = check_devices(world, n_dev, rehearsal)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)) or world)
+    why = check_devices(local_world, n_dev, rehearsal)
     if why:
         print(f"bench.py: {why}", file=sys.stderr)
         sys.exit(2)
-    devices = min(world, n_dev)  # distinct devices the ranks run on
 
     from kcptube_amd import FecCode
     from kcptube_amd.partition import combine_digests, group_range
@@ -372,6 +399,7 @@ def main():
     for i in range(args.steps):
         step(i)
     torch.cuda.synchronize()
+    local_elapsed = time.perf_counter() - t0  # this rank's own steps, before waiting for the others
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
@@ -383,6 +411,15 @@ def main():
 
     enc_ms = sum(ev[i][0].elapsed_time(ev[i][1]) for i in range(n_ev)) / n_ev
     dec_ms = sum(ev[i][1].elapsed_time(ev[i][2]) for i in range(n_ev)) / n_ev
+    # every rank's own timing and device, gathered after the timed region (per_rank in the JSON line)
+    my_rec = {"rank": rank, "device": device_ident(torch, dev, local_dev), "name": torch.cuda.get_device_name(dev),
+              "groups": G, "encode_ms": round(enc_ms, 4) if do_enc else None, "decode_ms": round(dec_ms, 4),
+              "wall_ms_per_step": round(local_elapsed / args.steps * 1e3, 4)}
+    records = [my_rec]
+    if world > 1:
+        records = [None] * world
+        dist.all_gather_object(records, my_rec)
+    devices = len({r["device"] for r in records})  # distinct GPUs over every rank (and node)
 
     # correctness of what was timed (untimed): every erased data shard recovered bit-exact
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -520,6 +557,9 @@ def main():
         "verified_bit_exact": ok,
         "cpu_baseline": None,
     }
+    if world > 1:
+        result["per_rank"] = records
+        result["multi_rank"] = per_rank_summary(records, value, [K * B * r["groups"] for r in records])
     if parts:
         result["combined_digest"] = combine_digests([d for ds in all_digs for d in ds])
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -52,7 +52,9 @@ int kfec_create(size_t K, size_t N, kfec_ctx **out);
  * locking either; kcptube re-targets a coder from the thread that uses it (client.cpp:1755, relay.cpp:947).
  * Matrices are shared per (device, K, N) and immutable: create and reset build one on the first use of a shape
  * and are a lookup afterwards (no allocation, launch or synchronisation); the old matrix stays valid for
- * batched launches still in flight.  The cached matrices are released with the device's last coder. */
+ * batched launches still in flight.  Matrices no coder uses stay cached up to 8 shapes / 4 MiB per device (the
+ * least recently released beyond that are freed; that free waits for the device's in-flight work); the rest
+ * are released with the device's last coder. */
 int kfec_reset(kfec_ctx *ctx, size_t K, size_t N);
 void kfec_destroy(kfec_ctx *ctx);
 size_t kfec_get_K(const kfec_ctx *ctx);
@@ -139,6 +141,12 @@ int kfec_device(const kfec_ctx *ctx);
  * its device is destroyed; it is relaunched on demand.  KFEC_WORKER=0 turns the workers off; KFEC_WORKER=1 makes a worker failure an error instead of a
  * switch to the launch path; KFEC_WORKER_SLOTS (1-8, default 2) sets the workers per device. */
 uint64_t kfec_worker_requests(void);
+/* Batch requests served so far by the resident workers (process-wide; diagnostics): the small flushes of the
+ * batched queues (kfec_pipeline.h) that took the worker instead of kernel launches. */
+uint64_t kfec_worker_batches(void);
+/* Matrices cached on the coder's device (diagnostics): their count, and in *bytes (if not NULL) their device
+ * allocation.  Bounded by the coders' distinct shapes plus the unused-shape cache of kfec_reset. */
+size_t kfec_cached_matrices(const kfec_ctx *ctx, size_t *bytes);
 /* One empty request through a resident worker of the coder's device (diagnostics: the communication floor of
  * the per-call path).  KFEC_OK, or KFEC_ENODEV when the workers are off. */
 int kfec_worker_ping(const kfec_ctx *ctx);

@@ -26,20 +26,29 @@ namespace {
 // immutable device allocation (the N x K matrix, then its perm tables) and its host copy.  kcptube builds a
 // coder per connection and direction and re-targets it with reset_martix (client.cpp:1755, relay.cpp:947,
 // server.cpp:438): after the first coder of a shape, create / reset are a table lookup -- no allocation, no
-// launch, no synchronisation.  Matrices are never freed while a coder of their device lives (so a batched
-// launch still reading the old matrix after a reset stays valid, and no hipFree -- which waits for every stream
-// of the device, the resident worker's included -- runs on a coder's lifecycle); they are released with the
-// device's last coder, after its workers have stopped.
+// launch, no synchronisation.  Each matrix counts the coders pointing at it.  A matrix no coder points at stays
+// cached (a reset back to its shape is a lookup again, and a batched launch still reading it stays valid) until
+// more than kKeepUnused such matrices -- or more than kKeepUnusedBytes of them -- exist on the device: then the
+// least recently released ones are freed.  hipFree waits for every stream of the device (in-flight launches that
+// still read the matrix finish first; the resident worker's lease bounds that wait), so eviction only runs on
+// the rare reset that leaves the cache over its bound, never on the common lookup.  What is left goes with the
+// device's last coder, after its workers have stopped.  Matrix ids are never reused, so the worker's LDS table
+// cache (keyed by id) cannot mistake a new matrix at a freed address for the old one.
+constexpr size_t kKeepUnused = 8;
+constexpr size_t kKeepUnusedBytes = size_t(4) << 20;
 struct Matrix {
     size_t K = 0, N = 0;
     uint8_t *d = nullptr;     // N x K matrix, then the perm tables (enc_alloc_bytes)
     std::vector<uint8_t> h;   // host copy of the N x K matrix
     uint64_t id = 0;          // unique per built matrix: the resident worker's LDS table-cache key
+    size_t refs = 0;          // coders whose d_enc is this matrix
+    uint64_t released = 0;    // release clock when refs last dropped to 0 (eviction order)
 };
 struct DevMatrices {
     std::mutex mu;
     hipStream_t stream = nullptr;  // builds run here
     std::vector<Matrix *> all;
+    uint64_t clock = 0;
 };
 DevMatrices g_mats[64];
 std::atomic<uint64_t> g_mat_ids{0};
@@ -52,6 +61,7 @@ struct kfec_ctx {
     const uint8_t *d_enc = nullptr;  // the shared matrix of (K, N) on the device (Matrix::d)
     const uint8_t *h_enc = nullptr;  // its host copy (Matrix::h)
     uint64_t mat_id = 0;             // Matrix::id
+    Matrix *mat = nullptr;           // the shared matrix this coder holds a reference on
     hipStream_t stream = nullptr;    // private stream of the single-group launch path (created on first use)
     std::mutex mu;                   // single-group staging is shared by encode and decode callers
     uint8_t *d_stage = nullptr;
@@ -60,6 +70,10 @@ struct kfec_ctx {
     size_t h_stage_cap = 0;
     bool counted = false;        // kfec_create returned it (counted in g_live)
 };
+
+const uint8_t *kfec::ctx_enc(const kfec_ctx *c) { return c->d_enc; }
+const uint8_t *kfec::ctx_h_enc(const kfec_ctx *c) { return c->h_enc; }
+uint64_t kfec::ctx_mat_id(const kfec_ctx *c) { return c->mat_id; }
 
 int kfec::current_device_cus()
 {
@@ -98,13 +112,46 @@ int probe_device(kfec::DeviceInfo &di)
     return KFEC_OK;
 }
 
-// The shared matrix of (K, N) on the current device, built on first use.  nullptr + rc on failure.
-const Matrix *get_matrix(int dev, size_t K, size_t N, int &rc)
+// Free the least recently released unreferenced matrices while more than kKeepUnused (or kKeepUnusedBytes) of
+// them are cached.  Called with dm.mu held.
+void evict_unused(DevMatrices &dm)
+{
+    for (;;) {
+        size_t n = 0, bytes = 0;
+        Matrix *oldest = nullptr;
+        for (Matrix *m : dm.all) {
+            if (m->refs) continue;
+            ++n;
+            bytes += kfec::enc_alloc_bytes(m->K, m->N);
+            if (!oldest || m->released < oldest->released) oldest = m;
+        }
+        if (!oldest || (n <= kKeepUnused && bytes <= kKeepUnusedBytes)) return;
+        (void)hipFree(oldest->d);  // (waits for the device's in-flight work, which may still read it)
+        dm.all.erase(std::remove(dm.all.begin(), dm.all.end(), oldest), dm.all.end());
+        delete oldest;
+    }
+}
+
+void unref_matrix(int dev, Matrix *m)
+{
+    if (!m) return;
+    DevMatrices &dm = g_mats[dev];
+    std::lock_guard<std::mutex> lk(dm.mu);
+    if (m->refs && --m->refs == 0) {
+        m->released = ++dm.clock;
+        evict_unused(dm);
+    }
+}
+
+// The shared matrix of (K, N) on the current device, built on first use, with one more reference counted on
+// it.  nullptr + rc on failure.
+Matrix *get_matrix(int dev, size_t K, size_t N, int &rc)
 {
     DevMatrices &dm = g_mats[dev];
     std::lock_guard<std::mutex> lk(dm.mu);
-    for (const Matrix *m : dm.all)
+    for (Matrix *m : dm.all)
         if (m->K == K && m->N == N) {
+            ++m->refs;
             rc = KFEC_OK;
             return m;
         }
@@ -144,6 +191,7 @@ const Matrix *get_matrix(int dev, size_t K, size_t N, int &rc)
     m->K = K;
     m->N = N;
     m->id = g_mat_ids.fetch_add(1) + 1;
+    m->refs = 1;
     dm.all.push_back(m);
     rc = KFEC_OK;
     return m;
@@ -153,13 +201,16 @@ const Matrix *get_matrix(int dev, size_t K, size_t N, int &rc)
 int set_matrix(kfec_ctx *c, size_t K, size_t N)
 {
     int rc = KFEC_OK;
-    const Matrix *m = get_matrix(c->di.device, K, N, rc);
+    Matrix *m = get_matrix(c->di.device, K, N, rc);
     if (!m) return rc;
+    Matrix *old = c->mat;
+    c->mat = m;
     c->d_enc = m->d;
     c->h_enc = m->h.data();
     c->K = K;
     c->N = N;
     c->mat_id = m->id;
+    unref_matrix(c->di.device, old);  // (after the new one is referenced: a reset to the same shape keeps it)
     return KFEC_OK;
 }
 
@@ -240,6 +291,20 @@ int kfec_device(const kfec_ctx *ctx) { return ctx ? ctx->di.device : -1; }
 
 uint64_t kfec_worker_requests(void) { return kfec::worker_served(); }
 
+uint64_t kfec_worker_batches(void) { return kfec::worker_batches(); }
+
+size_t kfec_cached_matrices(const kfec_ctx *ctx, size_t *bytes)
+{
+    if (bytes) *bytes = 0;
+    if (!ctx) return 0;
+    DevMatrices &dm = g_mats[ctx->di.device];
+    std::lock_guard<std::mutex> lk(dm.mu);
+    size_t b = 0;
+    for (const Matrix *m : dm.all) b += kfec::enc_alloc_bytes(m->K, m->N);
+    if (bytes) *bytes = b;
+    return dm.all.size();
+}
+
 int kfec_worker_ping(const kfec_ctx *ctx)
 {
     if (!ctx) return KFEC_EINVAL;
@@ -300,6 +365,7 @@ void kfec_destroy(kfec_ctx *ctx)
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    unref_matrix(dev, ctx->mat);  // (the device's last coder then releases every cached matrix below)
     delete ctx;
     if (last) {
         std::lock_guard<std::mutex> lk(g_live_mu);

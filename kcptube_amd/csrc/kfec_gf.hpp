@@ -13,7 +13,9 @@ namespace kfec {
 
 struct GfTables {
     uint8_t exp[512];  // exp[i] = alpha^(i mod 255), doubled so log a + log b needs no reduction
-    uint8_t log[256];  // log[0] = 0xFF sentinel (never used: callers test for zero first)
+    uint8_t log[256];  // log[0] = 0xFF = 255: callers that multiply test for zero first, but the fused
+                       // Lagrange prep (kfec_kernels.hip decode_prep_lagrange) relies on 255 = 0 mod 255
+                       // (static_assert there); do not change the sentinel
 };
 
 constexpr GfTables make_gf_tables()

@@ -4,6 +4,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "../../include/kfec.h"
 #include "../../include/kfec_frame.h"
 #include "../../include/kfec_aead.h"
 
@@ -23,13 +24,14 @@ inline size_t record_stride(size_t K, size_t R)
     const size_t coef = (4 + rec_k4(K) + R * rec_k4(K) + 15) & ~size_t(15);
     return coef > 112 ? coef : 112;
 }
-// after the G records (256-aligned): the syndrome decode's active-group list -- a count (+ 252 bytes of
-// padding), per-1024-group chunk counts / offsets, then the list of up to G group ids (uint32 each)
+// after the G records (256-aligned): the syndrome decode's active-group list -- a count and the bucketed
+// decode's per-mask counts / first slots (256 bytes), per-1024-group chunk counts / offsets (8 per chunk: one
+// per used-row mask), then the list of up to G group ids (uint32 each)
 inline size_t decode_list_offset(size_t G, size_t K, size_t R) { return (G * record_stride(K, R) + 255) & ~size_t(255); }
 inline size_t decode_list_chunks(size_t G) { return (G + 1023) / 1024; }
 inline size_t decode_workspace_bytes(size_t G, size_t K, size_t R)
 {
-    return decode_list_offset(G, K, R) + 256 + 4 * decode_list_chunks(G) + 4 * G;
+    return decode_list_offset(G, K, R) + 256 + 32 * decode_list_chunks(G) + 4 * G;
 }
 
 // The encoding matrix allocation also holds the perm-MAC tables of its parity rows (gf_perm_tables, 5 dwords
@@ -46,6 +48,11 @@ struct DeviceInfo {
 
 // multiprocessor count of the current device, cached per device id (grids of the persistent kernels)
 int current_device_cus();
+
+// the coder's shared matrix (kfec_api.cpp): device allocation, host copy, worker table-cache id
+const uint8_t *ctx_enc(const kfec_ctx *c);
+const uint8_t *ctx_h_enc(const kfec_ctx *c);
+uint64_t ctx_mat_id(const kfec_ctx *c);
 
 // every launcher returns 0 or a negative KFEC_E* code
 int launch_build_matrix(uint8_t *d_enc, int K, int N, hipStream_t s);
@@ -72,6 +79,39 @@ int worker_decode(int device, const uint8_t *d_enc, const uint8_t *h_enc, uint64
                   const uint8_t *const *row_ptr, int m, const uint8_t *M, const uint8_t *P, uint8_t *out);
 void worker_stop(int device);
 int worker_ping(int device);  // 0, 1 workers off, < 0 KFEC_E*
+
+// Batch requests through the resident worker (the queues' small flushes, kfec_pipeline.cpp): n groups whose
+// shards sit in a device staging arena.  kBatchEncode: the R parity rows of each group's K framed data
+// shards; kBatchDecode: the m recovered rows of each group from its K selected shares and the host-solved
+// coefficients.  Output row (g, r) at out + (g * R + r) * opitch + ooff (host memory, coherent pinned).
+enum { kBatchEncode = 1, kBatchDecode = 2 };
+struct BatchSpec {
+    int op = kBatchEncode;
+    const uint8_t *enc = nullptr;  // encode: the coder's matrix allocation
+    uint64_t mat_id = 0;
+    const void *arena = nullptr;   // device address (64 bytes of readable headroom before and after)
+    uint8_t *out = nullptr;
+    size_t opitch = 0, ooff = 0;
+    int n = 0, K = 0, N = 0, B = 0;
+    const uint64_t *desc = nullptr;  // [n][K] shard descriptors (kfec_worker.hip bdesc_pack)
+    const uint8_t *rec = nullptr;    // decode: [n] records of rec_stride bytes: [0] m, [16 + u * K + j] D[u][j]
+    size_t rec_stride = 0;
+};
+// shard descriptor: byte offset in the arena, payload length, raw (parity share) or framed (data shard)
+inline uint64_t batch_desc(uint64_t off, uint32_t len, bool raw)
+{
+    return (off & 0xFFFFFFFFFFull) | ((uint64_t)(len & 0xFFFFu) << 40) | ((uint64_t)raw << 56);
+}
+bool worker_batch_ok(const BatchSpec &b);
+int worker_batch(int device, const BatchSpec &b);  // 0 done, 1 not taken (launch path), < 0 KFEC_E*
+uint64_t worker_batches();                          // batch requests served (process-wide)
+// the single-group decode's host solve: D[u][j] (m x K) for shares selected as rows M_t <- parity P_t
+bool worker_solve(const uint8_t *h_enc, int K, int m, const uint8_t *M, const uint8_t *P, uint8_t *D);
+// large-BAR staging: whether the host may write this device's memory directly, the write-combined copy, and
+// the fence that orders those writes before a later doorbell / launch
+bool bar_writable(int device);
+void copy_to_bar(void *dst, const void *src, size_t n);
+void bar_fence();
 
 // framing and wire layer (kfec_frame.hip)
 int launch_frame(int K, int N, bool recv, size_t G, const void *src, size_t src_bytes, const uint64_t *off,

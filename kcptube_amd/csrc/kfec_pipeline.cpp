@@ -1,7 +1,17 @@
 // kfec_pipeline.cpp -- include/kfec_pipeline.h: kcptube's fec_maker / fec_unpack + fec_find_missings
 // bookkeeping on the host, feeding batched device coding through the public C ABI (kfec.h, kfec_frame.h).
-// Per-packet work here is bookkeeping and copies into pinned staging; every byte of parity, recovered data and
+// Per-packet work here is bookkeeping and copies into staging; every byte of parity, recovered data and
 // redundant packet is computed by the GPU kernels at flush time.
+//
+// Two flush paths, chosen per flush:
+//   * the resident worker (kfec_worker.hip batch requests) for small flushes -- a doorbell, no launch and no
+//     stream synchronisation -- when the staging arena lives in device memory the host writes through the PCIe
+//     BAR as each datagram / shard arrives (BAR mode: large-BAR devices), so no bulk bytes cross PCIe at the
+//     flush.  The reference codes a group inside fec_maker / fec_find_missings (client.cpp:797-840, 895-938):
+//     at low load a flush of a few groups is the product's latency.
+//   * kernel launches on the caller's stream (kfec_encode_framed_batch / kfec_decode_framed_batch + pack / seal)
+//     for large flushes and for sealed queues.
+// A flush that fails leaves the queue as it was (tables, staged bytes, iv counter): it can be retried.
 #include "../../include/kfec_pipeline.h"
 
 #include <hip/hip_runtime.h>
@@ -9,9 +19,12 @@
 #include "kfec_internal.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
+#include <string>
 #include <vector>
 
 namespace {
@@ -20,18 +33,88 @@ constexpr uint32_t kFecWaits = KFEC_FEC_WAITS;
 
 size_t round4(size_t x) { return (x + 3) & ~size_t(3); }
 size_t round8(size_t x) { return (x + 7) & ~size_t(7); }
+size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// KFEC_QUEUE_BAR: 1 (default where the device has a large BAR) = BAR-mode staging allowed; 0 = pinned staging
+// uploaded by DMA only.  BAR mode is in effect while the queue's flushes stay small (KFEC_QUEUE_BAR_MAX groups,
+// default 2048): it takes the bulk upload out of the flush (latency), but a write-combined copy through the BAR
+// costs the host more per datagram than a memcpy into pinned memory that DMA uploads while the host keeps
+// queueing (throughput).  KFEC_QUEUE_BAR_ALIGN: staging granule in BAR mode (default 64: whole write-combining
+// lines).  KFEC_QUEUE_WORKER_MAX: the largest flush (groups) sent to the resident worker (default 64; 0 = never).
+bool env_flag(const char *name, bool def)
+{
+    const char *e = getenv(name);
+    return e ? std::string(e) != "0" : def;
+}
+size_t env_size(const char *name, size_t def)
+{
+    const char *e = getenv(name);
+    return e ? (size_t)std::max(0L, atol(e)) : def;
+}
+size_t bar_flush_max()
+{
+    static const size_t v = env_size("KFEC_QUEUE_BAR_MAX", 2048);
+    return v;
+}
+size_t bar_align()
+{
+    static const size_t v = [] {
+        size_t a = env_size("KFEC_QUEUE_BAR_ALIGN", 64);
+        return (a >= 4 && (a & (a - 1)) == 0 && a <= 4096) ? a : (size_t)64;
+    }();
+    return v;
+}
+
+std::atomic<long> g_worker_max{-1};  // -1: the environment not read yet
+size_t worker_flush_max()
+{
+    long v = g_worker_max.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char *e = getenv("KFEC_QUEUE_WORKER_MAX");
+        const long x = e ? std::max(0L, atol(e)) : 64L;
+        g_worker_max.compare_exchange_strong(v, x);
+        v = g_worker_max.load();
+    }
+    return (size_t)v;
+}
+
+// Test knob: fail the n-th HIP step (copy, launch, worker request, synchronisation) of the next flush, once
+// (KFEC_TEST_FAIL_FLUSH=n in the environment, or kfec_test_fail_flush(n)); the step returns KFEC_EHIP without
+// running, as a failed HIP call would.
+std::atomic<int> g_fail_at{-1};  // -1: the environment not read yet; 0: off
+int fail_at()
+{
+    int v = g_fail_at.load();
+    if (v < 0) {
+        const char *e = getenv("KFEC_TEST_FAIL_FLUSH");
+        const int x = e ? std::max(0, atoi(e)) : 0;
+        g_fail_at.compare_exchange_strong(v, x);
+        v = g_fail_at.load();
+    }
+    return v;
+}
+struct Steps {
+    int k = 0;
+    bool fail()
+    {
+        ++k;
+        int f = fail_at();
+        return f > 0 && k == f && g_fail_at.compare_exchange_strong(f, 0);
+    }
+};
 
 // pinned host and device buffers, grown on demand
 struct Pinned {
     void *p = nullptr;
     size_t n = 0;
+    unsigned flags = hipHostMallocDefault;
     int ensure(size_t bytes)
     {
         if (bytes <= n) return KFEC_OK;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         n = 0;
-        if (hipHostMalloc(&p, std::max<size_t>(bytes, 256), hipHostMallocDefault) != hipSuccess) return KFEC_ENOMEM;
+        if (hipHostMalloc(&p, std::max<size_t>(bytes, 256), flags) != hipSuccess) return KFEC_ENOMEM;
         n = std::max<size_t>(bytes, 256);
         return KFEC_OK;
     }
@@ -39,26 +122,43 @@ struct Pinned {
     ~Pinned() { if (p) (void)hipHostFree(p); }
 };
 
+// Device buffer; `uncached` (BAR mode): written by the host through the BAR and read by kernels and the resident
+// worker, so no L2 line may outlive a host write.  64 bytes of readable headroom before and after the usable
+// range (the worker's 16-byte granule loads reach a few bytes past a payload on either side).
+constexpr size_t kDevPad = 64;
 struct Device {
+    void *alloc = nullptr;
     void *p = nullptr;
     size_t n = 0;
+    bool uncached = false;
     int ensure(size_t bytes)
     {
         if (bytes <= n) return KFEC_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        n = 0;
-        if (hipMalloc(&p, std::max<size_t>(bytes, 256)) != hipSuccess) return KFEC_ENOMEM;
-        n = std::max<size_t>(bytes, 256);
+        release();
+        const size_t want = std::max<size_t>(bytes, 256);
+        const hipError_t e = uncached ? hipExtMallocWithFlags(&alloc, want + 2 * kDevPad, hipDeviceMallocUncached)
+                                      : hipMalloc(&alloc, want + 2 * kDevPad);
+        if (e != hipSuccess) {
+            alloc = nullptr;
+            return KFEC_ENOMEM;
+        }
+        p = static_cast<uint8_t *>(alloc) + kDevPad;
+        n = want;
         return KFEC_OK;
     }
+    void release()
+    {
+        if (alloc) (void)hipFree(alloc);
+        alloc = p = nullptr;
+        n = 0;
+    }
     template <typename T> T *as() const { return static_cast<T *>(p); }
-    ~Device() { if (p) (void)hipFree(p); }
+    ~Device() { release(); }
 };
 
-// Append-only staging uploaded while the host is still filling it: every kUploadChunk bytes of finished
-// groups go H2D on the queue's own copy stream, so the PCIe transfer overlaps the per-packet host work and a
-// flush only copies the tail.  Bytes already queued for DMA are never written again before the flush has
+// Append-only staging uploaded while the host is still filling it (pinned mode): every kUploadChunk bytes of
+// finished groups go H2D on the queue's own copy stream, so the PCIe transfer overlaps the per-packet host work
+// and a flush only copies the tail.  Bytes already queued for DMA are never written again before the flush has
 // synchronised (the arena is append-only between flushes).
 struct Upload {
     static constexpr size_t kUploadChunk = size_t(8) << 20;
@@ -73,55 +173,153 @@ struct Upload {
         return KFEC_OK;
     }
     // called after the arena grew to `used` bytes: start the copy of the finished bytes once a chunk is ready
-    void grow(const Pinned &h, const Device &d, size_t used)
+    void grow(const uint8_t *h, uint8_t *d, size_t used)
     {
         if (used - issued < kUploadChunk) return;
-        if (hipMemcpyAsync(static_cast<uint8_t *>(d.p) + issued, static_cast<const uint8_t *>(h.p) + issued,
-                           used - issued, hipMemcpyHostToDevice, cs) == hipSuccess)
+        if (hipMemcpyAsync(d + issued, h + issued, used - issued, hipMemcpyHostToDevice, cs) == hipSuccess)
             issued = used;  // on failure the bytes are simply copied again by finish()
     }
     // copy the tail and make `s` wait for every upload
-    int finish(const Pinned &h, const Device &d, size_t used, hipStream_t s)
+    int finish(const uint8_t *h, uint8_t *d, size_t used, hipStream_t s)
     {
-        if (issued == 0) {  // nothing went up early (a small flush): one copy on s, no cross-stream event
-            return (used == 0 || hipMemcpyAsync(d.p, h.p, used, hipMemcpyHostToDevice, s) == hipSuccess) ? KFEC_OK
-                                                                                                        : KFEC_EHIP;
-        }
-        if (used > issued && hipMemcpyAsync(static_cast<uint8_t *>(d.p) + issued, static_cast<const uint8_t *>(h.p) + issued,
-                                            used - issued, hipMemcpyHostToDevice, cs) != hipSuccess)
+        if (issued == 0)  // nothing went up early (a small flush): one copy on s, no cross-stream event
+            return (used == 0 || hipMemcpyAsync(d, h, used, hipMemcpyHostToDevice, s) == hipSuccess) ? KFEC_OK : KFEC_EHIP;
+        if (used > issued && hipMemcpyAsync(d + issued, h + issued, used - issued, hipMemcpyHostToDevice, cs) != hipSuccess)
             return KFEC_EHIP;
-        issued = 0;
+        issued = 0;  // (a retried flush uploads everything again on s)
         if (hipEventRecord(ev, cs) != hipSuccess || hipStreamWaitEvent(s, ev, 0) != hipSuccess) return KFEC_EHIP;
         return KFEC_OK;
     }
+    int drain() { return (cs && hipStreamSynchronize(cs) != hipSuccess) ? KFEC_EHIP : KFEC_OK; }
     ~Upload()
     {
-        if (cs) (void)hipStreamSynchronize(cs);
+        (void)drain();
         if (ev) (void)hipEventDestroy(ev);
         if (cs) (void)hipStreamDestroy(cs);
     }
 };
 
-// Make room for `need` more bytes in a staging arena holding `used` bytes when nothing is queued (so a flush
-// cannot free anything): the partial / waiting groups of many connections can outgrow the initial
-// max_groups-sized arena.  Doubles the pinned and the device arena; the upload restarts from byte 0.
-int grow_arena(Pinned &h, Device &d, Upload &up, size_t used, size_t need, size_t &cap)
-{
-    size_t ncap = std::max<size_t>(cap, 4096);
-    while (used + need > ncap) ncap *= 2;
-    if (up.cs && hipStreamSynchronize(up.cs) != hipSuccess) return KFEC_EHIP;
-    Pinned nh;
-    Device nd;
-    if (nh.ensure(ncap) || nd.ensure(ncap)) return KFEC_ENOMEM;
-    if (used) std::memcpy(nh.p, h.p, used);
-    std::swap(h.p, nh.p);
-    std::swap(h.n, nh.n);
-    std::swap(d.p, nd.p);
-    std::swap(d.n, nd.n);
-    up.issued = 0;
-    cap = ncap;
-    return KFEC_OK;
-}
+// The staging arena of a queue: the bytes in pinned host memory (the queue's own copy: compaction, deferred
+// data packets) and their device image.  BAR mode: the image is uncached device memory written through the BAR
+// at staging time (no upload; the worker and the kernels read it in place).  Pinned mode: uploaded (Upload).
+struct Arena {
+    Pinned h;
+    Device d;
+    size_t cap = 0;
+    bool bar_ok = false;  // the device image is BAR-writable, uncached memory
+    bool bar = false;     // BAR mode in effect (decided at each compaction, see set_mode)
+    size_t align = 4;     // staging granule (offsets and lengths rounded up to it)
+    size_t reserve = 0;   // device image bytes past cap: the sealed small flush's redundant-packet rows
+    Upload up;            // (pinned mode)
+    int init(int device, size_t bytes, bool use_bar, size_t extra = 0)
+    {
+        bar_ok = bar = use_bar;
+        d.uncached = use_bar;
+        align = use_bar ? bar_align() : 4;
+        reserve = use_bar ? extra : 0;
+        if (h.ensure(bytes) || d.ensure(bytes + reserve)) return KFEC_ENOMEM;
+        cap = bytes;
+        return up.init(device);
+    }
+    size_t step(size_t n) const { return (n + align - 1) & ~(align - 1); }
+    // BAR mode while the flushes stay small: called between flushes (nothing staged for DMA in flight)
+    void set_mode(size_t last_flush_groups) { bar = bar_ok && last_flush_groups <= bar_flush_max(); }
+    uint8_t *host(size_t off = 0) const { return h.as<uint8_t>() + off; }
+    // n bytes at off: the host copy and, in BAR mode, the device image
+    void put(size_t off, const void *src, size_t n)
+    {
+        if (!n) return;
+        std::memcpy(host(off), src, n);
+        if (bar) kfec::copy_to_bar(d.as<uint8_t>() + off, src, n);
+    }
+    // bytes the host already wrote into its copy, to the device image (BAR mode)
+    void mirror(size_t off, size_t n)
+    {
+        if (bar && n) kfec::copy_to_bar(d.as<uint8_t>() + off, host(off), n);
+    }
+    void staged(size_t used)
+    {
+        if (!bar) up.grow(host(), d.as<uint8_t>(), used);
+    }
+    // the device image of [0, used) complete and ordered before work on s
+    int finish(size_t used, hipStream_t s)
+    {
+        if (bar) {
+            kfec::bar_fence();
+            return KFEC_OK;
+        }
+        return up.finish(host(), d.as<uint8_t>(), used, s);
+    }
+    // before the host copy is compacted: no upload may still be reading it
+    int quiesce() { return up.drain(); }
+    // after the host copy was compacted to [0, used): rewrite the image (BAR) / restart the upload
+    void restage(size_t used)
+    {
+        up.issued = 0;
+        mirror(0, used);
+    }
+    // room for `need` more bytes after `used` when nothing is queued: doubles both copies, keeps [0, used)
+    int grow(size_t used, size_t need)
+    {
+        size_t ncap = std::max<size_t>(cap, 4096);
+        while (used + need > ncap) ncap *= 2;
+        if (up.drain()) return KFEC_EHIP;
+        Pinned nh;
+        Device nd;
+        nd.uncached = bar_ok;
+        if (nh.ensure(ncap) || nd.ensure(ncap + reserve)) return KFEC_ENOMEM;
+        if (used) std::memcpy(nh.p, h.p, used);
+        std::swap(h.p, nh.p);
+        std::swap(h.n, nh.n);
+        std::swap(d.alloc, nd.alloc);
+        std::swap(d.p, nd.p);
+        std::swap(d.n, nd.n);
+        up.issued = 0;
+        cap = ncap;
+        mirror(0, used);
+        return KFEC_OK;
+    }
+    ~Arena() { (void)up.drain(); }  // (the copy stream is idle before the buffers go)
+};
+
+// The queue's own stream for a flush called with stream = NULL: HIP's null stream would also wait for the
+// device's other streams -- a resident worker's among them, for up to its lease -- at every flush.
+struct OwnStream {
+    hipStream_t s = nullptr;
+    int init() { return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? KFEC_OK : KFEC_EHIP; }
+    void *pick(void *stream) const { return stream ? stream : static_cast<void *>(s); }
+    ~OwnStream()
+    {
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    }
+};
+
+// A host table written to device memory: in BAR mode straight through the BAR (no copy call), otherwise packed
+// into `pack` and sent by one hipMemcpyAsync.  The sources are never moved (a failed flush can be retried).
+struct TableUpload {
+    bool bar;
+    uint8_t *dst;   // device
+    uint8_t *pack;  // pinned staging (pinned mode)
+    size_t used = 0;
+    void add(size_t off, const void *src, size_t n)
+    {
+        if (!n) return;
+        if (bar) kfec::copy_to_bar(dst + off, src, n);
+        else if (pack + off != src) std::memcpy(pack + off, src, n);
+        used = std::max(used, off + n);
+    }
+    int send(hipStream_t s)
+    {
+        if (bar) {
+            kfec::bar_fence();
+            return KFEC_OK;
+        }
+        return (used == 0 || hipMemcpyAsync(dst, pack, used, hipMemcpyHostToDevice, s) == hipSuccess) ? KFEC_OK : KFEC_EHIP;
+    }
+};
 
 inline void put_le32(uint8_t *p, uint32_t v)
 {
@@ -166,22 +364,31 @@ int seal_rows(int mode, const kfec_aead *aead, size_t P, const void *src, size_t
 
 }  // namespace
 
+// test-only hooks (not in the headers): arm the flush fault knob; override KFEC_QUEUE_WORKER_MAX (-1: env again)
+extern "C" void kfec_test_fail_flush(int n) { (void)fail_at(); g_fail_at.store(n > 0 ? n : 0); }
+extern "C" void kfec_test_queue_worker_max(long n) { g_worker_max.store(n < 0 ? -1 : n); }
+
 // ---- send ------------------------------------------------------------------------------------------------
 struct kfec_txq {
     const kfec_ctx *ctx = nullptr;
+    int device = 0;
     size_t K = 0, N = 0, R = 0, G = 0, mtu = 0, slot = 0;  // slot: datagram stride of a kfec_tx group cache
     size_t n = 0;                                          // complete groups queued
-    size_t used = 0;  // staged datagram bytes (packed back to back at 4-byte offsets: one H2D of these)
-    size_t cap = 0;   // staging arena bytes
+    size_t last_n = 0;                                     // groups of the last flush (the arena's mode)
+    size_t used = 0;  // staged bytes (packed back to back at Arena::step granules)
     std::vector<kfec_tx *> txs;  // the senders whose partial groups live in the arena
-    // h_meta: the per-group tables, filled at [0, GK*8) off, [m_len, +GK*2) len, [m_sn, +G*4) sn, [m_conv, +G*4)
-    // conv; a flush packs the used parts back to back and sends them in ONE copy (small flushes are
-    // latency-bound: each DMA costs microseconds to set up).  h_res: the redundant packets [n][R], then their
-    // lengths, again one copy back.
-    Pinned h_dg, h_meta, h_res;
-    size_t m_len = 0, m_sn = 0, m_conv = 0;
+    // per queued group g: the K datagrams' arena offsets and lengths, sn, conv (as kfec_tx_send wrote them; a
+    // flush never moves them)
+    std::vector<uint64_t> off;
+    std::vector<uint16_t> len;
+    std::vector<uint32_t> sn, conv;
     std::vector<uint64_t> tags;
-    Device d_dg, d_meta, d_par, d_align, d_res;
+    // launch path: h_pack (pinned mode: the tables packed for one copy up), h_res (the redundant packets [n][R],
+    // then their lengths, one copy back); worker path: wdesc (the batch's shard descriptors) and h_wout
+    // (coherent pinned: the worker writes parity rows there, each behind a 16-byte gap for its 13-byte header)
+    Pinned h_pack, h_res, h_wout;
+    std::vector<uint64_t> wdesc;
+    Device d_meta, d_par, d_align, d_res;
     // packet protection and deferred data packets (kfec_txq_seal)
     int seal_mode = KFEC_TXQ_SEAL_OFF;
     const kfec_aead *aead = nullptr;
@@ -198,11 +405,8 @@ struct kfec_txq {
     std::vector<DataPkt> dpk;  // staged since the last flush, in send order
     Pinned h_sdesc, h_sealed;  // seal descriptors (+ iv draws) up; sealed rows + lengths down
     Device d_sdesc, d_sealed;
-    uint64_t *h_off() const { return h_meta.as<uint64_t>(); }
-    uint16_t *h_len() const { return reinterpret_cast<uint16_t *>(h_meta.as<uint8_t>() + m_len); }
-    uint32_t *h_sn() const { return reinterpret_cast<uint32_t *>(h_meta.as<uint8_t>() + m_sn); }
-    uint32_t *h_conv() const { return reinterpret_cast<uint32_t *>(h_meta.as<uint8_t>() + m_conv); }
-    Upload up;  // declared after the buffers: destroyed (and drained) before them
+    OwnStream own;
+    Arena arena;  // declared last: destroyed (and its copy stream drained) first
 };
 
 struct kfec_tx {
@@ -226,28 +430,29 @@ bool kn_changed(const kfec_ctx *ctx, size_t K, size_t N) { return kfec_get_K(ctx
 // Move the live bytes (datagrams of every sender's partial group) to the front of the arena, in arena order
 // (every destination lies at or below its source, so memmove in that order never overwrites unread bytes).
 // Called with no group queued: after a flush, and before growing a full arena, so the bytes of destroyed
-// senders are reclaimed instead of doubling memory.  Any early upload is drained and restarted.
+// senders are reclaimed instead of doubling memory.
 int tx_compact(kfec_txq *q)
 {
-    if (q->up.cs && hipStreamSynchronize(q->up.cs) != hipSuccess) return KFEC_EHIP;
-    q->up.issued = 0;
     struct Part {
         uint64_t off;
         size_t len;
         uint64_t *rec;  // where the offset is recorded
         bool operator<(const Part &o) const { return off < o.off; }
     };
+    if (q->arena.quiesce()) return KFEC_EHIP;
     std::vector<Part> part;
     for (kfec_tx *tx : q->txs)
         for (size_t i = 0; i < tx->cached; ++i) part.push_back({tx->cache_off[i], tx->cache_len[i], &tx->cache_off[i]});
     std::sort(part.begin(), part.end());
     size_t at = 0;
     for (const Part &p : part) {
-        if (p.len && at != p.off) std::memmove(q->h_dg.as<uint8_t>() + at, q->h_dg.as<uint8_t>() + p.off, p.len);
+        if (p.len && at != p.off) std::memmove(q->arena.host(at), q->arena.host(p.off), p.len);
         *p.rec = at;
-        at += round4(p.len);
+        at += q->arena.step(p.len);
     }
     q->used = at;
+    q->arena.set_mode(q->last_n);
+    q->arena.restage(at);
     return KFEC_OK;
 }
 
@@ -255,7 +460,7 @@ int tx_compact(kfec_txq *q)
 
 extern "C" {
 
-size_t kfec_txq_capacity(const kfec_txq *q) { return q ? q->cap : 0; }
+size_t kfec_txq_capacity(const kfec_txq *q) { return q ? q->arena.cap : 0; }
 
 int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram, kfec_txq **out)
 {
@@ -265,32 +470,43 @@ int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram,
     kfec_txq *q = new (std::nothrow) kfec_txq;
     if (!q) return KFEC_ENOMEM;
     q->ctx = ctx;
+    q->device = kfec_device(ctx);
     q->K = kfec_get_K(ctx);
     q->N = kfec_get_N(ctx);
     q->R = q->N - q->K;
     q->G = max_groups;
     q->mtu = max_datagram;
-    q->slot = std::max<size_t>(round4(max_datagram), 4);
+    const bool bar = env_flag("KFEC_QUEUE_BAR", true) && kfec::bar_writable(q->device);
+    q->slot = (std::max<size_t>(max_datagram, 4) + (bar ? bar_align() : 4) - 1) & ~((bar ? bar_align() : 4) - 1);
     const size_t G = q->G, K = q->K, GK = G * K, R1 = std::max<size_t>(q->R, 1);
     const size_t pitch = round4(max_datagram + KFEC_FEC_CONTAINER_HEADER);
     const size_t pkt_pitch = round4(KFEC_PKT_REDUNDANT_HEADER + max_datagram + KFEC_FEC_CONTAINER_HEADER);
     // every buffer up front: a flush then costs copies and kernels only (pinning memory takes milliseconds)
-    q->m_len = GK * 8;
-    q->m_sn = round8(GK * 10);
-    q->m_conv = q->m_sn + G * 4;
-    const size_t meta = q->m_conv + G * 4, res = G * R1 * (pkt_pitch + 2);
-    if (q->h_dg.ensure(GK * q->slot) || q->h_meta.ensure(meta) || q->h_res.ensure(res) ||
-        q->d_dg.ensure(GK * q->slot) || q->d_meta.ensure(meta) || q->d_res.ensure(res) ||
-        q->d_par.ensure(G * R1 * pitch) || q->d_align.ensure(G * 2)) {
+    const size_t meta = round8(GK * 10) + G * 8, res = G * R1 * (pkt_pitch + 2);
+    q->d_meta.uncached = bar;
+    q->h_wout.flags = hipHostMallocCoherent;
+    try {
+        q->off.resize(GK);
+        q->len.resize(GK);
+        q->sn.resize(G);
+        q->conv.resize(G);
+        q->tags.resize(G);
+    } catch (...) {
         delete q;
         return KFEC_ENOMEM;
     }
-    if (q->up.init(kfec_device(ctx))) {
+    if (hipSetDevice(q->device) != hipSuccess) {
         delete q;
         return KFEC_EHIP;
     }
-    q->cap = GK * q->slot;
-    q->tags.resize(q->G);
+    const size_t red_rows = std::min(G, worker_flush_max()) * R1 * (16 + round16(max_datagram + KFEC_FEC_CONTAINER_HEADER));
+    // (BAR mode stages at whole write-combining lines: one group's worth more, so that partial groups of small
+    //  datagrams still fit beside a full queue as with 4-byte staging)
+    if (q->own.init() || q->arena.init(q->device, (GK + (bar ? K : 0)) * q->slot, bar, red_rows + 64) || q->h_pack.ensure(meta) || q->h_res.ensure(res) ||
+        q->d_meta.ensure(meta) || q->d_res.ensure(res) || q->d_par.ensure(G * R1 * pitch) || q->d_align.ensure(G * 2)) {
+        delete q;
+        return KFEC_ENOMEM;
+    }
     *out = q;
     return KFEC_OK;
 }
@@ -338,11 +554,11 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
     const bool completes = tx->conv != 0 && tx->cached + 1 == q->K;
     if (completes && q->n == q->G) return KFEC_ENOMEM;
     // staged bytes: the datagram (group cache) and, deferred, the data packet around it
-    const size_t need = round4(len + (defer ? KFEC_PKT_DATA_HEADER : 0));
-    if ((tx->conv != 0 || defer) && q->used + need > q->cap) {
+    const size_t need = q->arena.step(len + (defer ? KFEC_PKT_DATA_HEADER : 0));
+    if ((tx->conv != 0 || defer) && q->used + need > q->arena.cap) {
         if (q->n || !q->dpk.empty()) return KFEC_ENOMEM;  // a flush frees the queued bytes
         int rc = tx_compact(q);                            // first reclaim what no partial group holds any more
-        if (!rc && q->used + need > q->cap) rc = grow_arena(q->h_dg, q->d_dg, q->up, q->used, need, q->cap);
+        if (!rc && q->used + need > q->arena.cap) rc = q->arena.grow(q->used, need);
         if (rc) return rc;
     }
     if (defer) {
@@ -356,7 +572,7 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
     }
     // create_fec_data_packet (connections.cpp:395-411), sub_sn = fec_snd_sub_sn++ (client.cpp:805-806)
     const uint8_t sub = tx->sub_sn++;
-    uint8_t *dst = defer ? q->h_dg.as<uint8_t>() + q->used : pkt;  // deferred: staged for the flush
+    uint8_t *dst = defer ? q->arena.host(q->used) : pkt;  // deferred: staged for the flush
     put_le32(dst, timestamp);
     put_be32(dst + 4, tx->sn);
     dst[8] = sub;
@@ -364,33 +580,31 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
     if (pkt_len) *pkt_len = defer ? 0 : KFEC_PKT_DATA_HEADER + len;
     const int32_t slot = completes ? (int32_t)q->n : -1;
     if (defer) {
+        q->arena.mirror(q->used, KFEC_PKT_DATA_HEADER + len);
         q->dpk.push_back({q->used, (uint32_t)(KFEC_PKT_DATA_HEADER + len), tx->sn, sub, slot, tx->tag});
         if (tx->conv == 0) {
             q->used += need;
-            q->up.grow(q->h_dg, q->d_dg, q->used);
+            q->arena.staged(q->used);
         }
     }
     if (tx->conv == 0) {  // client.cpp:811-815
         tx->sub_sn = 0;
         return KFEC_OK;
     }
-    if (!defer && len) std::memcpy(q->h_dg.as<uint8_t>() + q->used, datagram, len);
+    if (!defer) q->arena.put(q->used, datagram, len);
     tx->cache_off[tx->cached] = q->used + (defer ? KFEC_PKT_DATA_HEADER : 0);
     tx->cache_len[tx->cached++] = (uint16_t)len;
     q->used += need;
-    if (!completes) {
-        if (defer) q->up.grow(q->h_dg, q->d_dg, q->used);
-        return KFEC_OK;
-    }
+    q->arena.staged(q->used);
+    if (!completes) return KFEC_OK;
     // the group is complete: it takes queue slot n (compact_into_container + encode run at the flush)
     const size_t g = q->n;
     for (size_t i = 0; i < q->K; ++i) {
-        q->h_off()[g * q->K + i] = tx->cache_off[i];
-        q->h_len()[g * q->K + i] = tx->cache_len[i];
+        q->off[g * q->K + i] = tx->cache_off[i];
+        q->len[g * q->K + i] = tx->cache_len[i];
     }
-    q->up.grow(q->h_dg, q->d_dg, q->used);
-    q->h_sn()[g] = tx->sn;
-    q->h_conv()[g] = tx->conv;
+    q->sn[g] = tx->sn;
+    q->conv[g] = tx->conv;
     q->tags[g] = tx->tag;
     q->n = g + 1;
     tx->cached = 0;  // fec_snd_cache.clear(), client.cpp:830-832
@@ -399,25 +613,210 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
     return KFEC_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// The flush's packets in emission order: the redundant ones in queue order or, with deferred data packets,
+// every packet in send order with a group's redundant packets right after the data packet completing it.
+template <typename Data, typename Red>
+void emit(const kfec_txq *q, size_t n, Data &&data, Red &&red)
+{
+    if (q->defer) {
+        for (size_t i = 0; i < q->dpk.size(); ++i) {
+            data(i);
+            if (q->dpk[i].group >= 0) red((size_t)q->dpk[i].group);
+        }
+    } else {
+        for (size_t g = 0; g < n; ++g) red(g);
+    }
+}
+
+// Small, unsealed flush through the resident worker: the groups' framed shards are read from the arena's
+// device image (BAR mode), the parity rows land in h_wout behind a 16-byte gap each, and the 13-byte redundant
+// headers (create_fec_redundant_packet, connections.cpp:413-430) are written into the gap here.  1: not taken.
+int txq_flush_worker(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *user, Steps &st)
+{
+    const size_t n = q->n, K = q->K, R = q->R;
+    if (!q->arena.bar || R == 0 || n == 0 || n > worker_flush_max()) return 1;
+    const size_t B = q->mtu + KFEC_FEC_CONTAINER_HEADER, opitch = 16 + round16(B);
+    kfec::BatchSpec b;
+    b.op = kfec::kBatchEncode;
+    b.enc = kfec::ctx_enc(q->ctx);
+    b.mat_id = kfec::ctx_mat_id(q->ctx);
+    b.arena = q->arena.d.p;
+    b.opitch = opitch;
+    b.ooff = 16;
+    b.n = (int)n;
+    b.K = (int)K;
+    b.N = (int)q->N;
+    b.B = (int)B;
+    if (!kfec::worker_batch_ok(b)) return 1;
+    if (q->h_wout.ensure(n * R * opitch)) return KFEC_ENOMEM;
+    try {
+        q->wdesc.resize(n * K);
+    } catch (...) {
+        return KFEC_ENOMEM;
+    }
+    for (size_t i = 0; i < n * K; ++i) q->wdesc[i] = kfec::batch_desc(q->off[i], q->len[i], false);
+    b.desc = q->wdesc.data();
+    b.out = q->h_wout.as<uint8_t>();
+    kfec::bar_fence();  // the staged datagrams before the doorbell
+    if (st.fail()) return KFEC_EHIP;
+    const int rc = kfec::worker_batch(q->device, b);
+    if (rc) return rc;  // (1: the worker is off or gone -> the launch path)
+    uint8_t *wo = q->h_wout.as<uint8_t>();
+    auto red = [&](size_t g) {
+        uint16_t mx = 0;  // align = max datagram length + 2 (data_operations.cpp:613-616)
+        for (size_t i = 0; i < K; ++i) mx = std::max(mx, q->len[g * K + i]);
+        const size_t align = (size_t)mx + KFEC_FEC_CONTAINER_HEADER;
+        for (size_t r = 0; r < R; ++r) {
+            uint8_t *p = wo + (g * R + r) * opitch + 16 - KFEC_PKT_REDUNDANT_HEADER;
+            put_le32(p, timestamp);  // host_to_little_endian
+            put_be32(p + 4, q->sn[g]);
+            p[8] = (uint8_t)(K + r);
+            put_be32(p + 9, q->conv[g]);
+            if (cb) cb(user, q->tags[g], q->sn[g], (uint8_t)(K + r), p, KFEC_PKT_REDUNDANT_HEADER + align);
+        }
+    };
+    auto data = [&](size_t i) {
+        const kfec_txq::DataPkt &d = q->dpk[i];
+        if (cb && d.len) cb(user, d.tag, d.sn, d.sub, q->arena.host(d.off), d.len);
+    };
+    emit(q, n, data, red);
+    q->last_n = n;
+    q->n = 0;
+    q->dpk.clear();
+    return tx_compact(q);  // keep the partial groups, at the front of the arena
+}
+
+// Small sealed flush (BAR mode): the resident worker writes the parity rows into the arena's reserve behind a
+// 16-byte gap each, the host writes each redundant header into its gap through the BAR, and ONE seal launch
+// protects every packet -- the staged data packets and the redundant ones, in emission order -- straight into
+// pinned host rows (no pack or descriptor kernels, no copy calls).  1: not taken.
+int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *user, void *stream, Steps &st)
+{
+    const size_t n = q->n, nd = q->dpk.size(), K = q->K, R = q->R;
+    if (!q->arena.bar || n > worker_flush_max() || (n && R == 0)) return 1;
+    const size_t B = q->mtu + KFEC_FEC_CONTAINER_HEADER, opitch = 16 + round16(B);
+    const size_t red_base = (q->used + 63) & ~size_t(63), nr = n * R;
+    if (red_base + nr * opitch > q->arena.cap + q->arena.reserve) return 1;
+    uint8_t *dimg = q->arena.d.as<uint8_t>();
+    kfec::BatchSpec b;
+    b.op = kfec::kBatchEncode;
+    b.enc = kfec::ctx_enc(q->ctx);
+    b.mat_id = kfec::ctx_mat_id(q->ctx);
+    b.arena = dimg;
+    b.out = dimg + red_base;  // (device memory: the seal launch reads the rows in place)
+    b.opitch = opitch;
+    b.ooff = 16;
+    b.n = (int)n;
+    b.K = (int)K;
+    b.N = (int)q->N;
+    b.B = (int)B;
+    if (n && !kfec::worker_batch_ok(b)) return 1;
+    const size_t rows = nd + nr;
+    const size_t spitch = round4(KFEC_PKT_REDUNDANT_HEADER + B + seal_overhead(q->seal_mode));
+    const size_t dL = rows * 8, dI = round8(dL + rows * 4), dT = dI + rows * 2;
+    const size_t sO = rows * spitch, sT = sO + rows * 4;
+    q->d_sdesc.uncached = true;
+    if (q->h_sdesc.ensure(dT) || q->d_sdesc.ensure(dT) || q->h_sealed.ensure(sT)) return KFEC_ENOMEM;
+    try {
+        q->wdesc.resize(n * K);
+    } catch (...) {
+        return KFEC_ENOMEM;
+    }
+    // descriptors (data rows, then redundant rows) and iv draws in emission order, built in h_sdesc and written
+    // through the BAR; the redundant headers into the rows' gaps
+    uint8_t *hd = q->h_sdesc.as<uint8_t>();
+    uint64_t *off = reinterpret_cast<uint64_t *>(hd);
+    uint32_t *len = reinterpret_cast<uint32_t *>(hd + dL);
+    uint16_t *iv = reinterpret_cast<uint16_t *>(hd + dI);
+    for (size_t i = 0; i < nd; ++i) {
+        off[i] = q->dpk[i].off;
+        len[i] = q->dpk[i].len;
+    }
+    uint8_t hdr[KFEC_PKT_REDUNDANT_HEADER];
+    for (size_t g = 0; g < n; ++g) {
+        uint16_t mx = 0;  // align = max datagram length + 2 (data_operations.cpp:613-616)
+        for (size_t i = 0; i < K; ++i) mx = std::max(mx, q->len[g * K + i]);
+        put_le32(hdr, timestamp);
+        put_be32(hdr + 4, q->sn[g]);
+        put_be32(hdr + 9, q->conv[g]);
+        for (size_t r = 0; r < R; ++r) {
+            const size_t row = red_base + (g * R + r) * opitch + 16 - KFEC_PKT_REDUNDANT_HEADER;
+            hdr[8] = (uint8_t)(K + r);
+            kfec::copy_to_bar(dimg + row, hdr, sizeof(hdr));
+            off[nd + g * R + r] = row;
+            len[nd + g * R + r] = (uint32_t)(KFEC_PKT_REDUNDANT_HEADER + mx + KFEC_FEC_CONTAINER_HEADER);
+        }
+    }
+    uint64_t iv_ctr = q->iv_ctr;  // committed only when the flush succeeds
+    emit(q, n, [&](size_t i) { iv[i] = iv_draw(q->iv_seed, iv_ctr++); },
+         [&](size_t g) { for (size_t r = 0; r < R; ++r) iv[nd + g * R + r] = iv_draw(q->iv_seed, iv_ctr++); });
+    kfec::copy_to_bar(q->d_sdesc.p, hd, dT);
+    kfec::bar_fence();  // staged packets, headers and descriptors before the doorbell / the launch
+    if (n) {
+        for (size_t i = 0; i < n * K; ++i) q->wdesc[i] = kfec::batch_desc(q->off[i], q->len[i], false);
+        b.desc = q->wdesc.data();
+        if (st.fail()) return KFEC_EHIP;
+        const int rc = kfec::worker_batch(q->device, b);
+        if (rc) return rc;  // (1: the worker is off or gone -> the launch path)
+    }
+    uint8_t *hs = q->h_sealed.as<uint8_t>();
+    uint32_t *s_len = reinterpret_cast<uint32_t *>(hs + sO);
+    const uint8_t *ds = q->d_sdesc.as<uint8_t>();
+    if (st.fail()) return KFEC_EHIP;
+    int rc = seal_rows(q->seal_mode, q->aead, rows, dimg, red_base + nr * opitch, reinterpret_cast<const uint64_t *>(ds),
+                       reinterpret_cast<const uint32_t *>(ds + dL), reinterpret_cast<const uint16_t *>(ds + dI), hs, spitch,
+                       s_len, stream);
+    if (rc) return rc;
+    if (st.fail() || hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) return KFEC_EHIP;
+    auto red = [&](size_t g) {
+        for (size_t r = 0; r < R; ++r) {
+            const size_t i = nd + g * R + r;
+            if (s_len[i] && cb) cb(user, q->tags[g], q->sn[g], (uint8_t)(K + r), hs + i * spitch, s_len[i]);
+        }
+    };
+    auto data = [&](size_t i) {
+        const kfec_txq::DataPkt &d = q->dpk[i];
+        if (s_len[i] && cb) cb(user, d.tag, d.sn, d.sub, hs + i * spitch, s_len[i]);
+    };
+    emit(q, n, data, red);
+    q->iv_ctr = iv_ctr;
+    q->last_n = n;
+    q->n = 0;
+    q->dpk.clear();
+    return tx_compact(q);
+}
+
+}  // namespace
+
+extern "C" {
+
 int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *user, void *stream)
 {
     if (!q) return KFEC_EINVAL;
     const size_t n = q->n, nd = q->dpk.size();
     if (n == 0 && nd == 0) return KFEC_OK;
     if (kn_changed(q->ctx, q->K, q->N)) return KFEC_EINVAL;  // the coder was reset: recreate the queue
+    const bool seal = q->seal_mode != KFEC_TXQ_SEAL_OFF;
+    stream = q->own.pick(stream);
+    Steps st;
+    if (!seal && n) {
+        const int rc = txq_flush_worker(q, timestamp, cb, user, st);
+        if (rc <= 0) return rc;
+    } else if (seal) {
+        const int rc = txq_flush_sealed_small(q, timestamp, cb, user, stream, st);
+        if (rc <= 0) return rc;
+    }
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t K = q->K, R = q->R;
     const size_t B = q->mtu + KFEC_FEC_CONTAINER_HEADER, pitch = round4(B);
     const size_t pkt_pitch = round4(KFEC_PKT_REDUNDANT_HEADER + B);
     const size_t nk = n * K, nr = n * R;
-    const bool seal = q->seal_mode != KFEC_TXQ_SEAL_OFF;
-    // pack the used tables back to back (each destination lies below its source, and below the sources still
-    // to be moved): [off nk*8][len nk*2][pad][sn n*4][conv n*4]
-    uint8_t *hm = q->h_meta.as<uint8_t>();
-    const size_t L = nk * 8, S = round8(L + nk * 2), C = S + n * 4, T = C + n * 4;
-    std::memmove(hm + L, hm + q->m_len, nk * 2);
-    std::memmove(hm + S, hm + q->m_sn, n * 4);
-    std::memmove(hm + C, hm + q->m_conv, n * 4);
+    // device tables [off nk*8][len nk*2][pad][sn n*4][conv n*4], from the queue's tables (never moved)
+    const size_t L = nk * 8, S = round8(L + nk * 2), C = S + n * 4;
     uint8_t *dm = q->d_meta.as<uint8_t>();
     const uint64_t *d_off = reinterpret_cast<const uint64_t *>(dm);
     const uint16_t *d_len = reinterpret_cast<const uint16_t *>(dm + L);
@@ -427,7 +826,9 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
     const size_t spitch = round4(KFEC_PKT_REDUNDANT_HEADER + B + seal_overhead(q->seal_mode));
     const size_t dL = nd * 8, dI = round8(dL + nd * 4), dT = dI + rows * 2;
     const size_t sO = rows * spitch, sT = sO + rows * 4;
+    uint64_t iv_ctr = q->iv_ctr;  // committed only when the flush succeeds
     if (seal) {
+        q->d_sdesc.uncached = q->arena.bar_ok;
         if (q->h_sdesc.ensure(dT) || q->d_sdesc.ensure(dT + nr * 12 + 8) || q->h_sealed.ensure(sT) || q->d_sealed.ensure(sT))
             return KFEC_ENOMEM;
         uint8_t *hd = q->h_sdesc.as<uint8_t>();
@@ -436,33 +837,37 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
             reinterpret_cast<uint64_t *>(hd)[i] = q->dpk[i].off;
             reinterpret_cast<uint32_t *>(hd + dL)[i] = q->dpk[i].len;
         }
-        // iv draws in emission order (see kfec_txq_flush): data packet i, then its group's redundant packets
+        // iv draws in emission order: data packet i, then its group's redundant packets
         auto red_ivs = [&](size_t g) {
-            for (size_t r = 0; r < R; ++r) iv[nd + g * R + r] = iv_draw(q->iv_seed, q->iv_ctr++);
+            for (size_t r = 0; r < R; ++r) iv[nd + g * R + r] = iv_draw(q->iv_seed, iv_ctr++);
         };
-        if (q->defer) {
-            for (size_t i = 0; i < nd; ++i) {
-                iv[i] = iv_draw(q->iv_seed, q->iv_ctr++);
-                if (q->dpk[i].group >= 0) red_ivs((size_t)q->dpk[i].group);
-            }
-        } else {
-            for (size_t g = 0; g < n; ++g) red_ivs(g);
-        }
-        if (hipMemcpyAsync(q->d_sdesc.p, hd, dT, hipMemcpyHostToDevice, s) != hipSuccess) return KFEC_EHIP;
+        emit(q, n, [&](size_t i) { iv[i] = iv_draw(q->iv_seed, iv_ctr++); }, red_ivs);
+        if (st.fail()) return KFEC_EHIP;
+        TableUpload tu{q->arena.bar, q->d_sdesc.as<uint8_t>(), hd};
+        tu.add(0, hd, dT);
+        if (tu.send(s)) return KFEC_EHIP;
     }
-    if (q->up.finish(q->h_dg, q->d_dg, q->used, s) ||
-        (n && hipMemcpyAsync(dm, hm, T, hipMemcpyHostToDevice, s) != hipSuccess))
-        return KFEC_EHIP;
+    if (st.fail() || q->arena.finish(q->used, s)) return KFEC_EHIP;
+    if (n) {
+        TableUpload tu{q->arena.bar, dm, q->h_pack.as<uint8_t>()};
+        tu.add(0, q->off.data(), L);
+        tu.add(L, q->len.data(), nk * 2);
+        tu.add(S, q->sn.data(), n * 4);
+        tu.add(C, q->conv.data(), n * 4);
+        if (st.fail() || tu.send(s)) return KFEC_EHIP;
+    }
     const size_t arena = std::max<size_t>(q->used, 4);
     const size_t P = nr * pkt_pitch;  // [n][R] compact redundant packets, then their lengths
     uint8_t *dr = q->d_res.as<uint8_t>();
     int rc = KFEC_OK;
     if (n) {
-        rc = kfec_encode_framed_batch(q->ctx, n, q->d_dg.p, arena, d_off, d_len, B, pitch, q->d_par.p,
+        if (st.fail()) return KFEC_EHIP;
+        rc = kfec_encode_framed_batch(q->ctx, n, q->arena.d.p, arena, d_off, d_len, B, pitch, q->d_par.p,
                                       q->d_align.as<uint16_t>(), stream);
         if (rc) return rc;
         if (R) {
-            rc = kfec_pack_batch(q->ctx, n, KFEC_PACK_REDUNDANT | KFEC_PACK_COMPACT, q->d_dg.p, arena, d_off, d_len,
+            if (st.fail()) return KFEC_EHIP;
+            rc = kfec_pack_batch(q->ctx, n, KFEC_PACK_REDUNDANT | KFEC_PACK_COMPACT, q->arena.d.p, arena, d_off, d_len,
                                  pitch, q->d_par.p, q->d_align.as<uint16_t>(), reinterpret_cast<const uint32_t *>(dm + S),
                                  reinterpret_cast<const uint32_t *>(dm + C), timestamp, dr, pkt_pitch,
                                  reinterpret_cast<uint16_t *>(dr + P), stream);
@@ -476,49 +881,46 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
         uint32_t *out_len = reinterpret_cast<uint32_t *>(sealed + sO);
         const kfec_aead *a = q->aead;
         // the staged data packets, straight from the arena
-        rc = seal_rows(q->seal_mode, a, nd, q->d_dg.p, arena, reinterpret_cast<const uint64_t *>(ds),
+        if (st.fail()) return KFEC_EHIP;
+        rc = seal_rows(q->seal_mode, a, nd, q->arena.d.p, arena, reinterpret_cast<const uint64_t *>(ds),
                        reinterpret_cast<const uint32_t *>(ds + dL), d_iv, sealed, spitch, out_len, stream);
         if (rc) return rc;
         if (nr) {  // the redundant packets the pack just wrote
             uint64_t *r_off = reinterpret_cast<uint64_t *>(ds + round8(dT));
             uint32_t *r_len = reinterpret_cast<uint32_t *>(r_off + nr);
-            if (kfec::launch_pkt_desc(nr, pkt_pitch, reinterpret_cast<const uint16_t *>(dr + P), r_off, r_len, s))
+            if (st.fail() || kfec::launch_pkt_desc(nr, pkt_pitch, reinterpret_cast<const uint16_t *>(dr + P), r_off, r_len, s))
                 return KFEC_EHIP;
+            if (st.fail()) return KFEC_EHIP;
             rc = seal_rows(q->seal_mode, a, nr, dr, std::max<size_t>(P, 4), r_off, r_len, d_iv + nd,
                            sealed + nd * spitch, spitch, out_len + nd, stream);
             if (rc) return rc;
         }
-        if (hipMemcpyAsync(q->h_sealed.p, sealed, sT, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
+        if (st.fail() || hipMemcpyAsync(q->h_sealed.p, sealed, sT, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
     } else if (nr) {
-        if (hipMemcpyAsync(q->h_res.p, dr, P + nr * 2, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
+        if (st.fail() || hipMemcpyAsync(q->h_res.p, dr, P + nr * 2, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
     }
-    if (hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
-    const uint32_t *sn = reinterpret_cast<const uint32_t *>(hm + S);
+    if (st.fail() || hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
     const uint8_t *pk = q->h_res.as<uint8_t>();
     const uint16_t *pk_len = reinterpret_cast<const uint16_t *>(pk + P);
     const uint8_t *hs = q->h_sealed.as<uint8_t>();
     const uint32_t *s_len = reinterpret_cast<const uint32_t *>(hs + sO);
-    auto emit_red = [&](size_t g) {
+    auto red = [&](size_t g) {
         for (size_t r = 0; r < R; ++r) {
             const size_t i = g * R + r;
             const uint8_t *p = seal ? hs + (nd + i) * spitch : pk + i * pkt_pitch;
-            const size_t len = seal ? s_len[nd + i] : pk_len[i];
-            if (len) cb(user, q->tags[g], sn[g], (uint8_t)(K + r), p, len);
+            const size_t plen = seal ? s_len[nd + i] : pk_len[i];
+            if (plen && cb) cb(user, q->tags[g], q->sn[g], (uint8_t)(K + r), p, plen);
         }
     };
-    if (cb) {
-        if (q->defer) {  // send order; a group's redundant packets right after the data packet completing it
-            for (size_t i = 0; i < nd; ++i) {
-                const kfec_txq::DataPkt &d = q->dpk[i];
-                const uint8_t *p = seal ? hs + i * spitch : q->h_dg.as<uint8_t>() + d.off;
-                const size_t len = seal ? s_len[i] : d.len;
-                if (len) cb(user, d.tag, d.sn, d.sub, p, len);
-                if (d.group >= 0) emit_red((size_t)d.group);
-            }
-        } else {
-            for (size_t g = 0; g < n; ++g) emit_red(g);
-        }
-    }
+    auto data = [&](size_t i) {
+        const kfec_txq::DataPkt &d = q->dpk[i];
+        const uint8_t *p = seal ? hs + i * spitch : q->arena.host(d.off);
+        const size_t plen = seal ? s_len[i] : d.len;
+        if (plen && cb) cb(user, d.tag, d.sn, d.sub, p, plen);
+    };
+    emit(q, n, data, red);
+    q->iv_ctr = iv_ctr;
+    q->last_n = n;
     q->n = 0;
     q->dpk.clear();
     return tx_compact(q);  // keep the partial groups, at the front of the arena
@@ -530,17 +932,14 @@ int kfec_txq_seal(kfec_txq *q, int mode, const kfec_aead *aead, uint64_t iv_seed
 {
     if (!q || (flags & ~KFEC_TXQ_DEFER_DATA) || q->n || !q->dpk.empty()) return KFEC_EINVAL;
     if (mode != KFEC_TXQ_SEAL_OFF) {
-        if (!seal_mode_ok(mode, aead) || (aead && aead->device != kfec_device(q->ctx))) return KFEC_EINVAL;
+        if (!seal_mode_ok(mode, aead) || (aead && aead->device != q->device)) return KFEC_EINVAL;
     } else if (aead) {
         return KFEC_EINVAL;
     }
     const bool defer = (flags & KFEC_TXQ_DEFER_DATA) != 0;
     if (defer && !q->defer) {  // every data packet now takes its 9-byte header in the arena too
-        const size_t slot = std::max<size_t>(round4(q->mtu + KFEC_PKT_DATA_HEADER), 4);
-        if (slot * q->G * q->K > q->cap) {
-            if (q->up.cs && hipStreamSynchronize(q->up.cs) != hipSuccess) return KFEC_EHIP;
-            if (grow_arena(q->h_dg, q->d_dg, q->up, q->used, slot * q->G * q->K - q->used, q->cap)) return KFEC_ENOMEM;
-        }
+        const size_t slot = q->arena.step(std::max<size_t>(q->mtu + KFEC_PKT_DATA_HEADER, 4));
+        if (slot * q->G * q->K > q->arena.cap && q->arena.grow(q->used, slot * q->G * q->K - q->used)) return KFEC_ENOMEM;
     }
     q->seal_mode = mode;
     q->aead = mode == KFEC_TXQ_SEAL_OFF ? nullptr : aead;
@@ -555,22 +954,36 @@ int kfec_txq_seal(kfec_txq *q, int mode, const kfec_aead *aead, uint64_t iv_seed
 // ---- receive ---------------------------------------------------------------------------------------------
 struct kfec_rxq {
     const kfec_ctx *ctx = nullptr;
+    int device = 0;
     size_t K = 0, N = 0, R = 0, G = 0, max_shard = 0, slot = 0;
-    size_t n = 0;     // groups queued for decoding
-    size_t used = 0;  // arena bytes staged (shards packed back to back at 4-byte offsets: one H2D of these)
-    size_t cap = 0;   // staging arena bytes
+    size_t n = 0;       // groups queued for decoding
+    size_t last_n = 0;  // groups of the last flush (the arena's mode)
+    size_t used = 0;    // arena bytes staged (shards packed back to back at Arena::step granules)
     std::vector<kfec_rx *> rxs;  // the receivers whose cached shards live in the arena
-    // h_meta: [0, GN*8) off, [m_len, +GN*2) len, [m_pres, +G*32) present, packed back to back at a flush and
-    // sent in one copy; h_res: recovered framed shards [n][R], then their data indices (one copy)
-    Pinned h_arena, h_meta, h_res;
-    size_t m_len = 0, m_pres = 0;
-    uint64_t *h_off() const { return h_meta.as<uint64_t>(); }
-    uint16_t *h_len() const { return reinterpret_cast<uint16_t *>(h_meta.as<uint8_t>() + m_len); }
-    uint64_t *h_present() const { return reinterpret_cast<uint64_t *>(h_meta.as<uint8_t>() + m_pres); }
+    // per queued group g: the N shard slots' arena offsets and lengths, the present bits (never moved by a flush)
+    std::vector<uint64_t> off;
+    std::vector<uint16_t> len;
+    std::vector<uint64_t> present;
     std::vector<uint64_t> tags;
     std::vector<uint32_t> sns;
-    Device d_arena, d_meta, d_align, d_st, d_ws, d_res;
-    Upload up;
+    // launch path: h_pack (pinned mode: the tables packed for one copy up), h_res (recovered framed shards
+    // [n][R], then their data indices; one copy back).  Worker path: wdesc / wrec (the batch's descriptors and
+    // per-group records), wmap (batch entry -> queue group), h_wout (coherent pinned recovered rows).
+    Pinned h_pack, h_res, h_wout;
+    std::vector<uint64_t> wdesc;
+    std::vector<uint8_t> wrec;
+    std::vector<uint32_t> wmap;
+    // host-solved decode coefficients by erasure pattern (m, missing ids, parity ids): live links repeat few
+    // patterns (at 1% loss most groups lose one shard)
+    struct Solved {
+        uint8_t m = 0;
+        uint8_t M[8] = {}, P[8] = {};
+        std::vector<uint8_t> D;
+    };
+    std::vector<Solved> solved;
+    Device d_meta, d_align, d_st, d_ws, d_res;
+    OwnStream own;
+    Arena arena;  // declared last: destroyed (and its copy stream drained) first
 };
 
 // fec_rcv_cache[sn]: the shards of one group, by sub_sn.  The bytes live in the queue's staging arena (stored
@@ -618,13 +1031,12 @@ bool kn_changed_rx(const kfec_rxq *q) { return kfec_get_K(q->ctx) != q->K || kfe
 // traffic (groups that never reach K shares) must not grow memory without bound.
 int rx_compact(kfec_rxq *q)
 {
-    if (q->up.cs && hipStreamSynchronize(q->up.cs) != hipSuccess) return KFEC_EHIP;
-    q->up.issued = 0;
     struct Part {
         uint64_t *off;
         size_t len;
         bool operator<(const Part &o) const { return *off < *o.off; }
     };
+    if (q->arena.quiesce()) return KFEC_EHIP;
     std::vector<Part> part;
     for (kfec_rx *rx : q->rxs)
         for (auto &kv : rx->cache) {
@@ -639,11 +1051,13 @@ int rx_compact(kfec_rxq *q)
     std::sort(part.begin(), part.end());
     size_t at = 0;
     for (const Part &p : part) {
-        if (p.len && at != *p.off) std::memmove(q->h_arena.as<uint8_t>() + at, q->h_arena.as<uint8_t>() + *p.off, p.len);
+        if (p.len && at != *p.off) std::memmove(q->arena.host(at), q->arena.host(*p.off), p.len);
         *p.off = at;
-        at += round4(p.len);
+        at += q->arena.step(p.len);
     }
     q->used = at;
+    q->arena.set_mode(q->last_n);
+    q->arena.restage(at);
     return KFEC_OK;
 }
 
@@ -651,14 +1065,14 @@ int rx_compact(kfec_rxq *q)
 void rx_enqueue(kfec_rxq *q, uint64_t tag, uint32_t sn, const RxGroup &grp)
 {
     const size_t g = q->n;
-    uint64_t *present = q->h_present() + g * 4;
+    uint64_t *present = &q->present[g * 4];
     present[0] = present[1] = present[2] = present[3] = 0;
     // a sub_sn beyond N is cached by the reference (it counts towards size()) but never selected usefully
     for (unsigned s = 0; s < q->N; ++s) {
         if (!grp.test(s)) continue;
         const size_t e = g * q->N + s;
-        q->h_off()[e] = grp.off[s];
-        q->h_len()[e] = grp.len[s];
+        q->off[e] = grp.off[s];
+        q->len[e] = grp.len[s];
         present[s >> 6] |= 1ull << (s & 63);
     }
     q->tags[g] = tag;
@@ -678,31 +1092,40 @@ int kfec_rxq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_shard, kf
     kfec_rxq *q = new (std::nothrow) kfec_rxq;
     if (!q) return KFEC_ENOMEM;
     q->ctx = ctx;
+    q->device = kfec_device(ctx);
     q->K = kfec_get_K(ctx);
     q->N = kfec_get_N(ctx);
     q->R = q->N - q->K;
     q->G = max_groups;
     q->max_shard = max_shard;
-    q->slot = round4(max_shard);
+    const bool bar = env_flag("KFEC_QUEUE_BAR", true) && kfec::bar_writable(q->device);
+    q->slot = (max_shard + (bar ? bar_align() : 4) - 1) & ~((bar ? bar_align() : 4) - 1);
     const size_t G = q->G, GN = G * q->N, R1 = std::max<size_t>(q->R, 1);
     const size_t pitch = round4(max_shard);
-    q->m_len = GN * 8;
-    q->m_pres = round8(GN * 10);
-    const size_t meta = q->m_pres + G * 32, res = G * R1 * (pitch + 3);
-    if (q->h_arena.ensure(GN * q->slot) || q->h_meta.ensure(meta) || q->h_res.ensure(res) ||
-        q->d_arena.ensure(GN * q->slot) || q->d_meta.ensure(meta) || q->d_res.ensure(res) ||
-        q->d_align.ensure(G * 2) || q->d_st.ensure(G) ||
+    const size_t meta = round8(GN * 10) + G * 32, res = G * R1 * (pitch + 3);
+    q->d_meta.uncached = bar;
+    q->h_wout.flags = hipHostMallocCoherent;
+    try {
+        q->off.resize(GN);
+        q->len.resize(GN);
+        q->present.resize(G * 4);
+        q->tags.resize(G);
+        q->sns.resize(G);
+        q->solved.resize(256);
+    } catch (...) {
+        delete q;
+        return KFEC_ENOMEM;
+    }
+    if (hipSetDevice(q->device) != hipSuccess) {
+        delete q;
+        return KFEC_EHIP;
+    }
+    if (q->own.init() || q->arena.init(q->device, (GN + (bar ? q->N : 0)) * q->slot, bar) || q->h_pack.ensure(meta) || q->h_res.ensure(res) ||
+        q->d_meta.ensure(meta) || q->d_res.ensure(res) || q->d_align.ensure(G * 2) || q->d_st.ensure(G) ||
         q->d_ws.ensure(kfec_decode_workspace_size(ctx, G))) {
         delete q;
         return KFEC_ENOMEM;
     }
-    if (q->up.init(kfec_device(ctx))) {
-        delete q;
-        return KFEC_EHIP;
-    }
-    q->cap = GN * q->slot;
-    q->tags.resize(q->G);
-    q->sns.resize(q->G);
     *out = q;
     return KFEC_OK;
 }
@@ -711,7 +1134,7 @@ void kfec_rxq_destroy(kfec_rxq *q) { delete q; }
 
 size_t kfec_rxq_pending(const kfec_rxq *q) { return q ? q->n : 0; }
 
-size_t kfec_rxq_capacity(const kfec_rxq *q) { return q ? q->cap : 0; }
+size_t kfec_rxq_capacity(const kfec_rxq *q) { return q ? q->arena.cap : 0; }
 
 int kfec_rx_create(kfec_rxq *q, uint64_t tag, kfec_rx **out)
 {
@@ -767,11 +1190,11 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
     const uint32_t have = fresh ? 0u : found->second->count + (found->second->test(sub) ? 0u : 1u);
     const bool completes = store && (fresh ? 1u : have) >= q->K;
     if (completes && q->n >= q->G) return KFEC_ENOMEM;
-    if (store && q->used + round4(plen) > q->cap) {
+    const size_t need = q->arena.step(plen);
+    if (store && q->used + need > q->arena.cap) {
         if (q->n) return KFEC_ENOMEM;  // a flush frees the queued groups' bytes
         int rc = rx_compact(q);        // first reclaim restored / evicted groups' bytes and overwritten duplicates
-        if (!rc && q->used + round4(plen) > q->cap)
-            rc = grow_arena(q->h_arena, q->d_arena, q->up, q->used, round4(plen), q->cap);
+        if (!rc && q->used + need > q->arena.cap) rc = q->arena.grow(q->used, need);
         if (rc) return rc;
     }
     // fec_rcv_cache[sn][sub_sn] = ... (client.cpp:869,887): a duplicate overwrites
@@ -787,11 +1210,11 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
         grp->count++;
     }
     if (store) {
-        if (plen) std::memcpy(q->h_arena.as<uint8_t>() + q->used, payload, plen);
+        q->arena.put(q->used, payload, plen);
         grp->off[sub] = q->used;
         grp->len[sub] = (uint16_t)plen;
-        q->used += round4(plen);
-        q->up.grow(q->h_arena, q->d_arena, q->used);
+        q->used += need;
+        q->arena.staged(q->used);
     }
     if (!red) {
         if (datagram) *datagram = payload;
@@ -820,25 +1243,147 @@ int kfec_rx_push(kfec_rx *rx, const uint8_t *pkt, size_t len, const uint8_t **da
     return queued;
 }
 
+}  // extern "C"
+
+namespace {
+
+// The decode coefficients of one erasure pattern (host_solve of the single-group decode), cached per queue.
+const uint8_t *rx_solve(kfec_rxq *q, int m, const uint8_t *M, const uint8_t *P)
+{
+    uint32_t h = (uint32_t)m * 0x9E3779B1u;
+    for (int t = 0; t < m; ++t) h = (h ^ M[t] ^ ((uint32_t)P[t] << 8)) * 0x01000193u;
+    kfec_rxq::Solved &e = q->solved[(h >> 8) & 255];
+    if (e.m == m && std::memcmp(e.M, M, m) == 0 && std::memcmp(e.P, P, m) == 0) return e.D.data();
+    try {
+        e.D.resize((size_t)m * q->K);
+    } catch (...) {
+        return nullptr;
+    }
+    e.m = 0;
+    if (!kfec::worker_solve(kfec::ctx_h_enc(q->ctx), (int)q->K, m, M, P, e.D.data())) return nullptr;
+    e.m = (uint8_t)m;
+    std::memcpy(e.M, M, m);
+    std::memcpy(e.P, P, m);
+    return e.D.data();
+}
+
+// Small flush through the resident worker.  Per queued group, on the host (bookkeeping): the reference's share
+// selection (fecpp.cpp:528-548: data share i fills row i, each missing row takes the highest unused id) and the
+// coefficients of the missing rows (cached by erasure pattern); on the device: the recovered framed shards,
+// straight into h_wout.  Groups with fewer than K shares recover nothing (the reference's {}), groups with every
+// data shard present need no device work.  1: not taken.
+int rxq_flush_worker(kfec_rxq *q, kfec_datagram_cb cb, void *user, Steps &st)
+{
+    const size_t n = q->n, K = q->K, N = q->N, R = q->R, B = q->max_shard;
+    if (!q->arena.bar || R == 0 || R > 8 || n == 0 || n > worker_flush_max()) return 1;
+    const size_t G16 = (B + 15) / 16, opitch = 16 * G16, rs = round16(16 + R * K);
+    try {
+        q->wdesc.resize(n * K);
+        q->wrec.assign(n * rs, 0);
+        q->wmap.resize(n);
+    } catch (...) {
+        return KFEC_ENOMEM;
+    }
+    size_t nb = 0;
+    for (size_t g = 0; g < n; ++g) {
+        const uint64_t *pr = &q->present[g * 4];
+        const int have = __builtin_popcountll(pr[0]) + __builtin_popcountll(pr[1]) + __builtin_popcountll(pr[2]) +
+                         __builtin_popcountll(pr[3]);
+        if ((size_t)have < K) continue;  // KFEC_GROUP_EMPTY: nothing recovered
+        auto bit = [&](size_t s_) { return (pr[s_ >> 6] >> (s_ & 63)) & 1; };
+        uint8_t M[8], P[8];
+        int m = 0;
+        size_t hi = N;  // parity picks: the highest present ids, descending
+        uint64_t *d = &q->wdesc[nb * K];
+        for (size_t i = 0; i < K; ++i) {
+            if (bit(i)) {
+                d[i] = kfec::batch_desc(q->off[g * N + i], q->len[g * N + i], false);
+                continue;
+            }
+            do --hi; while (!bit(hi));
+            if (m == 8) return 1;  // (R <= 8: unreachable)
+            M[m] = (uint8_t)i;
+            P[m] = (uint8_t)hi;
+            ++m;
+            d[i] = kfec::batch_desc(q->off[g * N + hi], q->len[g * N + hi], true);
+        }
+        if (m == 0) continue;  // every data shard present: nothing to recover
+        const uint8_t *D = rx_solve(q, m, M, P);
+        if (!D) return 1;  // a singular pattern (unreachable for an MDS code): the launch path reports it
+        uint8_t *rec = &q->wrec[nb * rs];
+        rec[0] = (uint8_t)m;
+        std::memcpy(rec + 1, M, m);  // (bytes 1..8: the recovered data ids, read back here below)
+        std::memcpy(rec + 16, D, (size_t)m * K);
+        q->wmap[nb++] = (uint32_t)g;
+    }
+    if (nb) {
+        kfec::BatchSpec b;
+        b.op = kfec::kBatchDecode;
+        b.arena = q->arena.d.p;
+        b.opitch = opitch;
+        b.ooff = 0;
+        b.n = (int)nb;
+        b.K = (int)K;
+        b.N = (int)N;
+        b.B = (int)B;
+        b.desc = q->wdesc.data();
+        b.rec = q->wrec.data();
+        b.rec_stride = rs;
+        if (!kfec::worker_batch_ok(b)) return 1;
+        if (q->h_wout.ensure(nb * R * opitch)) return KFEC_ENOMEM;
+        b.out = q->h_wout.as<uint8_t>();
+        kfec::bar_fence();  // the staged shards before the doorbell
+        if (st.fail()) return KFEC_EHIP;
+        const int rc = kfec::worker_batch(q->device, b);
+        if (rc) return rc;  // (1: the worker is off or gone -> the launch path)
+    }
+    const uint8_t *wo = q->h_wout.as<uint8_t>();
+    for (size_t e = 0; e < nb && cb; ++e) {
+        const uint8_t *rec = &q->wrec[e * rs];
+        const size_t g = q->wmap[e];
+        for (int u = 0; u < rec[0]; ++u) {
+            const uint8_t *shard = wo + (e * R + u) * opitch;
+            const size_t dlen = ((size_t)shard[0] << 8) | shard[1];  // ntohs(data_length)
+            if (dlen + KFEC_FEC_CONTAINER_HEADER > B) continue;     // inconsistent group (kfec_unframe_batch's 0xFFFF)
+            cb(user, q->tags[g], q->sns[g], rec[1 + u], shard + KFEC_FEC_CONTAINER_HEADER, dlen);
+        }
+    }
+    q->last_n = n;
+    q->n = 0;
+    return rx_compact(q);  // keep the shards of the groups still waiting for K shares
+}
+
+}  // namespace
+
+extern "C" {
+
 int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
 {
     if (!q) return KFEC_EINVAL;
     const size_t n = q->n;
     if (n == 0) return KFEC_OK;
     if (kn_changed_rx(q)) return KFEC_EINVAL;  // the coder was reset: recreate the queue
+    stream = q->own.pick(stream);
+    Steps st;
+    {
+        const int rc = rxq_flush_worker(q, cb, user, st);
+        if (rc <= 0) return rc;
+    }
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t N = q->N, R = q->R;
     const size_t B = q->max_shard, pitch = round4(B);
     const size_t nn = n * N;
-    // pack the used tables back to back: [off nn*8][len nn*2][pad][present n*32]
-    uint8_t *hm = q->h_meta.as<uint8_t>();
-    const size_t L = nn * 8, P = round8(L + nn * 2), T = P + n * 32;
-    std::memmove(hm + L, hm + q->m_len, nn * 2);
-    std::memmove(hm + P, hm + q->m_pres, n * 32);
+    // device tables [off nn*8][len nn*2][pad][present n*32], from the queue's tables (never moved)
+    const size_t L = nn * 8, P = round8(L + nn * 2);
     uint8_t *dm = q->d_meta.as<uint8_t>();
-    if (q->up.finish(q->h_arena, q->d_arena, q->used, s) ||
-        hipMemcpyAsync(dm, hm, T, hipMemcpyHostToDevice, s) != hipSuccess)
-        return KFEC_EHIP;
+    if (st.fail() || q->arena.finish(q->used, s)) return KFEC_EHIP;
+    {
+        TableUpload tu{q->arena.bar, dm, q->h_pack.as<uint8_t>()};
+        tu.add(0, q->off.data(), L);
+        tu.add(L, q->len.data(), nn * 2);
+        tu.add(P, q->present.data(), n * 32);
+        if (st.fail() || tu.send(s)) return KFEC_EHIP;
+    }
     // results: [n][R] recovered framed shards, then their data indices (one copy back).  extract_from_container
     // (data_operations.cpp:697-704) is only "skip the BE16 length": done here on the host at the callback, so
     // no unframe pass and no second copy of the recovered bytes
@@ -846,13 +1391,15 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
     uint8_t *dr = q->d_res.as<uint8_t>();
     uint8_t *d_idx = dr + D;
     // recv compact_into_container + decode fused: the chosen shares are framed on the fly from the arena
-    int rc = kfec_decode_framed_batch(q->ctx, n, q->d_arena.p, std::max<size_t>(q->used, 4),
+    if (st.fail()) return KFEC_EHIP;
+    int rc = kfec_decode_framed_batch(q->ctx, n, q->arena.d.p, std::max<size_t>(q->used, 4),
                                       reinterpret_cast<const uint64_t *>(dm), reinterpret_cast<const uint16_t *>(dm + L),
                                       reinterpret_cast<const uint64_t *>(dm + P), B, pitch, dr, d_idx,
                                       q->d_st.as<uint8_t>(), q->d_align.as<uint16_t>(), q->d_ws.p, stream);
     if (rc) return rc;
-    if (R && hipMemcpyAsync(q->h_res.p, dr, D + n * R, hipMemcpyDeviceToHost, s) != hipSuccess) return KFEC_EHIP;
-    if (hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
+    if (R && (st.fail() || hipMemcpyAsync(q->h_res.p, dr, D + n * R, hipMemcpyDeviceToHost, s) != hipSuccess))
+        return KFEC_EHIP;
+    if (st.fail() || hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
     const uint8_t *hr = q->h_res.as<uint8_t>();
     const uint8_t *rec_idx = hr + D;
     for (size_t g = 0; g < n && cb && R; ++g)
@@ -860,10 +1407,11 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
             const uint8_t idx = rec_idx[g * R + t];
             if (idx == 0xFF) continue;
             const uint8_t *shard = hr + (g * R + t) * pitch;
-            const size_t len = ((size_t)shard[0] << 8) | shard[1];  // ntohs(data_length)
-            if (len + KFEC_FEC_CONTAINER_HEADER > B) continue;     // inconsistent group (kfec_unframe_batch's 0xFFFF)
-            cb(user, q->tags[g], q->sns[g], idx, shard + KFEC_FEC_CONTAINER_HEADER, len);
+            const size_t dlen = ((size_t)shard[0] << 8) | shard[1];  // ntohs(data_length)
+            if (dlen + KFEC_FEC_CONTAINER_HEADER > B) continue;     // inconsistent group (kfec_unframe_batch's 0xFFFF)
+            cb(user, q->tags[g], q->sns[g], idx, shard + KFEC_FEC_CONTAINER_HEADER, dlen);
         }
+    q->last_n = n;
     q->n = 0;
     return rx_compact(q);  // keep the shards of the groups still waiting for K shares
 }
@@ -882,6 +1430,7 @@ struct kfec_opener {
     Pinned h_arena, h_desc, h_out;
     Device d_arena, d_desc, d_out;
     std::vector<uint64_t> tags;
+    OwnStream own;
 };
 
 extern "C" {
@@ -910,8 +1459,8 @@ int kfec_opener_create(int mode, const kfec_aead *aead, size_t max_packets, size
         delete o;
         return KFEC_ENOMEM;
     }
-    if (o->h_arena.ensure(arena) || o->h_desc.ensure(desc) || o->h_out.ensure(res) || o->d_arena.ensure(arena) ||
-        o->d_desc.ensure(desc) || o->d_out.ensure(res)) {
+    if (o->own.init() || o->h_arena.ensure(arena) || o->h_desc.ensure(desc) || o->h_out.ensure(res) ||
+        o->d_arena.ensure(arena) || o->d_desc.ensure(desc) || o->d_out.ensure(res)) {
         delete o;
         return KFEC_ENOMEM;
     }
@@ -948,6 +1497,7 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
     const size_t n = o->n;
     if (n == 0) return KFEC_OK;
     if (hipSetDevice(o->device) != hipSuccess) return KFEC_EHIP;
+    stream = o->own.pick(stream);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     // the host table stays as kfec_opener_add wrote it ([off max*8][len max*4]), so a flush that fails can be
     // retried: its first n offsets and first n lengths go up as two copies into [off n*8][len n*4]

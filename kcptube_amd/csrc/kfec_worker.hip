@@ -97,6 +97,38 @@ constexpr int kHostSolveWork = 1024;
 constexpr int kCinvLoads = 512 / 16;  // 16-byte loads of D (m * K <= 512: shape_ok's R * K bound)
 static_assert(kOffExited + 8 * kLineW <= kOffCinv && kOffCinv + kCinvLoads * 16 <= kOffShares, "slot layout");
 
+// ---- batch requests (the queues' small flushes, kfec_pipeline.cpp) -------------------------------------
+// A doorbell with B = 0 is a batch request: its K / N fields carry the request's length in 16-byte units, and
+// the request -- a BatchBody, then the shard descriptors, then (decode) one record per group -- sits at
+// kOffShares of the request side.  Every workgroup copies the whole request into LDS in one burst (one
+// dependent round trip, however many groups), then takes a contiguous range of the batch's (group, 16-byte
+// column) items.  The shards themselves are read from the queue's staging arena: device memory the host
+// wrote through the BAR as each datagram / shard arrived, so a flush moves no bulk bytes across PCIe before
+// the doorbell.  Outputs go straight to the queue's coherent pinned output rows.
+//   encode (kOpEncode): framed shards ([BE16 len][payload][zeros], compact_into_container, data_operations.cpp
+//     :610-631) -> the R parity rows of each group (the coder's matrix tables, as the single-group encode);
+//   decode (kOpDecode): the K selected shares of each group (data shards framed, parity shares raw, zero
+//     padded; data_operations.cpp:633-667) -> out_u = XOR_j D[u][j] * row_j with D = S^-1 [E | I] solved by
+//     the host per group (host_solve, the single-group decode's coefficients), rows u < m of the group.
+constexpr size_t kBatchReqMax = 16 * 1024;  // request bytes (body + descriptors + records): copied into LDS
+constexpr int kBatchMaxR = 8;               // parity rows (encode) / decode rows (m <= R) per group
+constexpr int kBatchMaxKS = 32;             // shards per lane (K / share split): bounds the loads in flight
+struct BatchBody {             // 128 bytes
+    uint64_t enc;              // encode: the coder's matrix allocation (N x K bytes, then its tables)
+    uint64_t mat_id;           // encode: LDS table-cache key
+    uint64_t arena;            // device address of the staging arena (64 bytes of headroom before and after)
+    uint64_t out;              // host address of the output rows: row (g, r) at out + (g * R + r) * opitch + ooff
+    uint32_t n, K, N, B;       // groups, shape, shard bytes (framed: datagram + 2)
+    uint32_t opitch, ooff;     // output row stride and the data's offset inside a row
+    uint32_t rec_off;          // decode: byte offset (from the body) of the group records
+    uint32_t rec_stride;       // decode: bytes per group record: [0] m, [16, 16 + R * K) D row-major (rows >= m zero)
+    uint8_t pad[128 - 64];
+};
+static_assert(sizeof(BatchBody) == 128, "batch body is one 128-byte block");
+// shard descriptor (u64, kfec_internal.hpp batch_desc): bits 0-39 byte offset in the arena, 40-55 payload
+// length, 56 raw (1: a parity share as received, no container header) or framed (0: a data shard, BE16 length
+// prepended)
+
 struct WorkerBody {          // 128 bytes
     uint64_t enc;            // device address of the coder's matrix allocation (N x K bytes, then its tables)
     uint64_t mat_id;         // unique per built matrix: the LDS table cache key
@@ -196,6 +228,180 @@ __device__ __forceinline__ void put_out(uint32_t *p, uint32_t v, int light)
     else *p = v;
 }
 
+__device__ uint4 w_zero16;  // never written: the target of the loads a lane does not need
+
+// 16 bytes [16c, 16c + 16) of a shard row whose payload (len bytes at arena byte offset off, 4-aligned) follows
+// an H-byte header (H = 2: the container's BE16 length, compact_into_container; H = 0: a raw parity share),
+// zero past the payload.  Both loads are always issued (a granule without payload reads w_zero16), so every
+// shard's loads can be in flight together.
+__device__ __forceinline__ uint4 shard_granule(const uint32_t *arena32, uint64_t d, int c)
+{
+    const uint64_t off = d & 0xFFFFFFFFFFull;
+    const int len = (int)((d >> 40) & 0xFFFFu), H = (d >> 56) & 1 ? 0 : 2;
+    const int q0 = 16 * c - H;                               // payload index of the granule's first byte
+    const int lo = max(0, -q0), hi = min(16, len - q0);      // payload bytes [lo, hi) of the granule
+    const bool any = hi > lo;
+    const uint64_t a4 = off + (uint64_t)(int64_t)(q0 + 16);  // (>= off + 14: the arena has headroom before it)
+    const uint64_t w4 = a4 >> 2;
+    const uint32_t sh = (uint32_t)(a4 & 3u);
+    const uint4 x = *(any ? reinterpret_cast<const uint4 *>(arena32 + (w4 - 4)) : &w_zero16);
+    const uint32_t x4 = *(any && sh ? arena32 + w4 : &w_zero16.x);
+    const uint32_t dw[5] = {x.x, x.y, x.z, x.w, x4};
+    const uint32_t M = any ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t nib = (M >> (4 * i)) & 0xFu;
+        o[i] = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], sh) & (((nib * 0x00204081u) & 0x01010101u) * 0xFFu);
+    }
+    if (H && c == 0) o[0] |= ((uint32_t)len >> 8) | (((uint32_t)len & 0xFFu) << 8);  // htons(data_length)
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// 16 bytes to host memory at system scope (written through L2: the light release is a wait for the acks)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store16_sys(uint8_t *p, uint4 v)
+{
+    const u32x4 x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(x) : "memory");
+}
+
+// One batch request (see BatchBody).  s_req: the request, copied into LDS by the caller.
+template <int RT>
+__device__ __forceinline__ void batch_items(const BatchBody &b, const uint64_t *s_desc, const uint8_t *s_rec,
+                                            const uint32_t *tab, int g_lo, int i0, int i1, int r0, bool decode)
+{
+    const int K = (int)b.K, R = (int)(b.N - b.K), G16 = ((int)b.B + 15) >> 4;
+    const int nitems = i1 - i0;
+    // S lanes per item, each over the shards j = s, s + S, ...: a batch of few items still spreads its GF work
+    // over every wave; the S partial sums meet by lane shuffles
+    int S = 1;
+    while (S < 16 && S < K && nitems * S * 2 <= kWThreads) S *= 2;
+    while ((K + S - 1) / S > kBatchMaxKS) S *= 2;  // (the host refuses shapes that would need S > 64)
+    const uint32_t *arena32 = reinterpret_cast<const uint32_t *>(b.arena);
+    const int tid = threadIdx.x;
+    for (int base = 0; base < nitems * S; base += kWThreads) {  // (uniform trip count: the shuffles need every lane)
+        const int t = base + tid;
+        const bool valid = t < nitems * S;
+        const int item = i0 + (valid ? t / S : 0), s = t & (S - 1);
+        const int g = item / G16, c = item - g * G16;
+        const uint64_t *dsc = s_desc + (size_t)g * K;
+        const uint32_t *gtab = decode ? tab + (size_t)(g - g_lo) * K * R * 8 : tab;
+        uint32_t acc[RT][4];
+#pragma unroll
+        for (int q = 0; q < RT; ++q) acc[q][0] = acc[q][1] = acc[q][2] = acc[q][3] = 0u;
+        // this lane's shards, 8 at a time with every load of a chunk issued before its MACs
+        for (int j0 = s; j0 < K; j0 += 8 * S) {
+            uint4 x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int j = j0 + u * S;
+                // (no branch around the loads: a lane without this shard takes descriptor 0, an empty payload,
+                //  whose granule loads read w_zero16)
+                const uint64_t dj = dsc[min(j, K - 1)];
+                x[u] = shard_granule(arena32, (valid && j < K) ? dj : 0ull, c);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int j = min(j0 + u * S, K - 1);  // (a clamped row multiplies a zero granule)
+                const uint32_t xv[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+                uint4 ta[RT];
+                uint32_t tb[RT];
+#pragma unroll
+                for (int q = 0; q < RT; ++q) {
+                    const uint32_t *ent = gtab + ((size_t)j * R + r0 + q) * 8;
+                    ta[q] = *reinterpret_cast<const uint4 *>(ent);
+                    tb[q] = ent[4];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t s0 = xv[i] & 0x07070707u, s1 = (xv[i] >> 3) & 0x07070707u, s2 = (xv[i] >> 6) & 0x03030303u;
+#pragma unroll
+                    for (int q = 0; q < RT; ++q) {
+                        const uint32_t tt[5] = {ta[q].x, ta[q].y, ta[q].z, ta[q].w, tb[q]};
+                        acc[q][i] = perm_mac(acc[q][i], tt, s0, s1, s2);
+                    }
+                }
+            }
+        }
+        for (int d = 1; d < S; d <<= 1)
+#pragma unroll
+            for (int q = 0; q < RT; ++q)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[q][i] ^= (uint32_t)__shfl_xor((int)acc[q][i], d);
+        if (valid && s == 0) {
+            const int m = decode ? (int)s_rec[(size_t)g * b.rec_stride] : R;
+            uint8_t *out = reinterpret_cast<uint8_t *>(b.out) + (size_t)b.ooff + 16 * (size_t)c;
+#pragma unroll
+            for (int q = 0; q < RT; ++q)
+                if (r0 + q < m)
+                    store16_sys(out + ((size_t)g * R + r0 + q) * b.opitch, make_uint4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]));
+        }
+    }
+}
+
+__device__ __forceinline__ void serve_batch(const uint8_t *in, uint8_t *smem, uint64_t &s_mat, uint32_t op, uint32_t len16)
+{
+    const int tid = threadIdx.x, w = blockIdx.x, W = gridDim.x;
+    // 1. the whole request into LDS: one burst of 16-byte loads
+    uint4 *s16 = reinterpret_cast<uint4 *>(smem + kLdsData);
+    const uint4 *src = reinterpret_cast<const uint4 *>(in + kOffShares);
+    const int n16 = min((int)len16, (int)(kBatchReqMax / 16));
+    for (int i0 = 0; i0 < n16; i0 += kWThreads * 4) {
+        uint4 r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[u] = src[min(i0 + u * kWThreads + tid, n16 - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i0 + u * kWThreads + tid < n16) s16[i0 + u * kWThreads + tid] = r[u];
+    }
+    __syncthreads();
+    const BatchBody &b = *reinterpret_cast<const BatchBody *>(smem + kLdsData);
+    const bool decode = op == kOpDecode;
+    const int K = (int)b.K, N = (int)b.N, R = N - K, G16 = ((int)b.B + 15) >> 4;
+    const int I = (int)b.n * G16;
+    const int i0 = (int)((int64_t)w * I / W), i1 = (int)((int64_t)(w + 1) * I / W);
+    const uint64_t *s_desc = reinterpret_cast<const uint64_t *>(smem + kLdsData + sizeof(BatchBody));
+    const uint8_t *s_rec = smem + kLdsData + b.rec_off;
+    const int g_lo = i0 / max(G16, 1), g_hi = i1 > i0 ? (i1 - 1) / G16 : g_lo - 1;
+    // 2. tables: encode -- the matrix's parity-row tables (the single-group encode's LDS cache); decode -- the
+    //    perm tables of D for this workgroup's groups, [group][j][u]
+    const uint32_t *tab;
+    if (!decode) {
+        uint32_t *s_tab = reinterpret_cast<uint32_t *>(smem + kLdsTab);
+        if (b.mat_id != s_mat) {
+            const uint32_t *g_tab =
+                reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(b.enc) + enc_tab_offset(K, N));
+            const int rows = (int)enc_tab_rows(R), ne = K * R * 5;
+            for (int i = tid; i < ne; i += kWThreads) {
+                const int e = i / 5, q = i - e * 5, j = e / R, r = e - j * R;
+                s_tab[e * 8 + q] = g_tab[(j * rows + r) * 5 + q];
+            }
+            __syncthreads();
+            if (tid == 0) s_mat = b.mat_id;
+        }
+        tab = s_tab;
+    } else {
+        uint32_t *s_dtab = reinterpret_cast<uint32_t *>(smem + kLdsDtab);
+        const int ne = (g_hi - g_lo + 1) * K * R;
+        for (int e = tid; e < ne; e += kWThreads) {
+            const int gl = e / (K * R), rem = e - gl * K * R, j = rem / R, u = rem - j * R;
+            uint32_t tb[5];
+            gf_perm_tables(s_rec[(size_t)(g_lo + gl) * b.rec_stride + 16 + u * K + j], tb);
+            *reinterpret_cast<uint4 *>(s_dtab + e * 8) = uint4{tb[0], tb[1], tb[2], tb[3]};
+            s_dtab[e * 8 + 4] = tb[4];
+        }
+        tab = s_dtab;
+    }
+    __syncthreads();
+    // 3. the items, row tiles of up to 4
+    for (int r0 = 0; r0 < R; r0 += 4)
+        by_rows(R - r0, [&](auto rt) {
+            constexpr int RT = decltype(rt)::value;
+            batch_items<RT>(b, s_desc, s_rec, tab, g_lo, i0, i1, r0, decode);
+        });
+}
+
 __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, const uint8_t *in, uint64_t *relay,
                                                                 uint32_t gen, uint32_t last_seq, uint64_t idle_ticks,
                                                                 uint64_t lease_ticks, int debug, int direct, int light,
@@ -253,8 +459,9 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, c
 #pragma unroll
                     for (int k = 0; k < NP; ++k) {
                         const uint64_t u = uniform64(xs[k]);
-                        if (!hit && u != 0 && db_seq(u) != last && !deaf) {  // (0: nothing relayed since the launch's memset;
-                                                                             //  deaf: the fallback test's knob)
+                        // (0: nothing relayed since the launch's memset; deaf: the fallback test's knob, which
+                        //  ignores requests but never the relay's quit value ~0, or relay-mode followers spin on)
+                        if (!hit && u != 0 && db_seq(u) != last && (!deaf || u == ~0ull)) {
                             v = u;  // (the relay's quit value ~0 has seq kSeqMask, never posted, and makes v ~0)
                             hit = true;
                         }
@@ -278,12 +485,12 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, c
                 }
             };
             // The lease: workgroup 0 also leaves once the kernel has been resident for lease_ticks, checked only
-            // here, between requests.  Any device-wide synchronisation of the process -- hipFree, hipHostFree,
-            // hipDeviceSynchronize, which wait for every stream -- then waits at most about one lease, even
-            // while other threads keep calling; the next request relaunches the worker (a launch, ~10 us, once
-            // per lease).
-            if (w == 0 && wall_clock64() - t_start > lease_ticks) v = ~0ull;
-            else if (w == 0 || !direct || W <= 1) poll_loop(std::integral_constant<int, 8>());
+            // inside the poll loop after a round of polls found no new doorbell (never ahead of a pending request,
+            // which the other workgroups may already be serving).  Any device-wide synchronisation of the process
+            // -- hipFree, hipHostFree, hipDeviceSynchronize, which wait for every stream -- then waits at most
+            // about one lease, even while other threads keep calling; the next request relaunches the worker (a
+            // launch, ~10 us, once per lease).
+            if (w == 0 || !direct || W <= 1) poll_loop(std::integral_constant<int, 8>());
             else if (W <= 4) poll_loop(std::integral_constant<int, 2>());
             else poll_loop(std::integral_constant<int, 1>());
             if (w == 0 && W > 1 && (!direct || v == ~0ull)) __hip_atomic_store(relay, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -306,6 +513,13 @@ __global__ void __launch_bounds__(kWThreads) kfec_worker_kernel(uint8_t *slot, c
                 else __hip_atomic_store(done, (uint64_t)last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             if (op == kOpStop) break;
+            continue;
+        }
+        if ((v >> 48) == 0) {  // B = 0: a batch request (the queues' small flushes)
+            serve_batch(in, smem, s_mat, op, (uint32_t)((v >> 32) & 0xFFFF));
+            __builtin_amdgcn_s_waitcnt(kVmcntZero);  // every output store acknowledged (system scope)
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(done, (uint64_t)last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             continue;
         }
         const int K = (int)((v >> 32) & 0xFF) + 1, N = (int)((v >> 40) & 0xFF) + 1, R = N - K;
@@ -645,6 +859,7 @@ int env_mode()
 }
 bool env_enabled() { return env_mode() != 0; }
 std::atomic<uint64_t> g_served{0};
+std::atomic<uint64_t> g_batches{0};
 
 int env_int(const char *name, int def, int lo, int hi)
 {
@@ -847,14 +1062,14 @@ int completion(const Slot &s, uint32_t seq, int W)
 }
 
 // post the doorbell and wait for every workgroup's completion word; returns the status (0, 1 singular,
-// 3 refused) or a KFEC_E* code
-int post_and_wait(Slot &s, uint32_t op, int K, int N, int B)
+// 3 refused) or a KFEC_E* code.  hi: the doorbell's bits 32-63 (K, N, B; or a batch request's length)
+int post_and_wait_db(Slot &s, uint32_t op, uint64_t hi)
 {
     const int W = n_wgs();
     uint32_t seq = (s.seq + 1) & kSeqMask;
     if (seq == 0 || seq == kSeqMask) seq = 1;  // (kSeqMask: the seq of the relay's quit value)
     s.seq = seq;
-    ring(s, db_pack(seq, op, (uint32_t)K, (uint32_t)N, (uint32_t)B));
+    ring(s, (uint64_t)(seq & kSeqMask) | ((uint64_t)op << 30) | (hi << 32));
     if (!s.running || leader_exited(s)) {
         const int rc = launch_worker(s);
         if (rc) return rc;
@@ -914,6 +1129,11 @@ int post_and_wait(Slot &s, uint32_t op, int K, int N, int B)
     }
 }
 
+int post_and_wait(Slot &s, uint32_t op, int K, int N, int B)
+{
+    return post_and_wait_db(s, op, db_pack(0, op, (uint32_t)K, (uint32_t)N, (uint32_t)B) >> 32);
+}
+
 bool shape_ok(int K, int N, size_t B, int mrows)
 {
     const int R = N - K, W = n_wgs();
@@ -924,7 +1144,91 @@ bool shape_ok(int K, int N, size_t B, int mrows)
 
 }  // namespace
 
+bool host_solve(const uint8_t *h_enc, int K, int m, const uint8_t *M, const uint8_t *P, uint8_t *D);
+
 bool worker_enabled() { return env_enabled(); }
+
+bool bar_writable(int device) { return bar_staging(device); }
+
+void copy_to_bar(void *dst, const void *src, size_t n)
+{
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) copy_wc_avx2(static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), n);
+    else std::memcpy(dst, src, n);
+}
+
+void bar_fence() { __builtin_ia32_sfence(); }
+
+// The largest number of groups one workgroup's item range touches (the decode's LDS tables hold that many).
+static int batch_groups_per_wg(int n, int G16, int W)
+{
+    const int64_t I = (int64_t)n * G16;
+    int most = 0;
+    for (int w = 0; w < W; ++w) {
+        const int64_t i0 = w * I / W, i1 = (w + 1) * I / W;
+        if (i1 > i0) most = std::max(most, (int)((i1 - 1) / G16 - i0 / G16 + 1));
+    }
+    return most;
+}
+
+bool worker_batch_ok(const BatchSpec &b)
+{
+    if (!env_enabled() || b.n < 1 || b.K < 1 || b.N <= b.K || b.N > 256 || b.B < 1 || b.B > 0xFFFF) return false;
+    const int R = b.N - b.K, G16 = (b.B + 15) / 16;
+    if (R > kBatchMaxR || b.opitch < b.ooff + (size_t)G16 * 16 || (b.opitch & 15) || (b.ooff & 15)) return false;
+    if ((size_t)b.K * R * 32 > kTabMax) return false;  // the matrix tables / one group's D tables
+    size_t bytes = sizeof(BatchBody) + (size_t)b.n * b.K * 8;
+    if (b.op == kBatchDecode) {
+        if (b.rec_stride < 16 + (size_t)R * b.K || (b.rec_stride & 15)) return false;
+        bytes = ((bytes + 15) & ~size_t(15)) + (size_t)b.n * b.rec_stride;
+        if ((size_t)batch_groups_per_wg(b.n, G16, n_wgs()) * b.K * R * 32 > kTabMax) return false;
+    }
+    return bytes <= kBatchReqMax;
+}
+
+int worker_batch(int device, const BatchSpec &b)
+{
+    if (!worker_batch_ok(b)) return 1;
+    DevWorkers *d = get_dev(device);
+    if (!d) return env_mode() == 2 ? KFEC_EHIP : 1;
+    std::unique_lock<std::mutex> lk;
+    Slot &s = acquire(*d, lk);
+    BatchBody body{};
+    body.enc = reinterpret_cast<uint64_t>(b.enc);
+    body.mat_id = b.mat_id;
+    body.arena = reinterpret_cast<uint64_t>(b.arena);
+    body.out = reinterpret_cast<uint64_t>(b.out);
+    body.n = (uint32_t)b.n;
+    body.K = (uint32_t)b.K;
+    body.N = (uint32_t)b.N;
+    body.B = (uint32_t)b.B;
+    body.opitch = (uint32_t)b.opitch;
+    body.ooff = (uint32_t)b.ooff;
+    const size_t dbytes = (size_t)b.n * b.K * 8;
+    size_t bytes = sizeof(BatchBody) + dbytes;
+    if (b.op == kBatchDecode) {
+        body.rec_off = (uint32_t)((bytes + 15) & ~size_t(15));
+        body.rec_stride = (uint32_t)b.rec_stride;
+        bytes = body.rec_off + (size_t)b.n * b.rec_stride;
+    }
+    put(s, kOffShares, &body, sizeof(body));
+    put(s, kOffShares + sizeof(BatchBody), b.desc, dbytes);
+    if (b.op == kBatchDecode) put(s, kOffShares + body.rec_off, b.rec, (size_t)b.n * b.rec_stride);
+    const uint32_t len16 = (uint32_t)((bytes + 15) / 16);
+    const int st = post_and_wait_db(s, b.op == kBatchDecode ? kOpDecode : kOpEncode, (uint64_t)len16);  // B = 0
+    if (st == kWorkerDead) return worker_dead(*d);
+    if (st < 0) return st;
+    if (st) return KFEC_EHIP;
+    g_batches.fetch_add(1, std::memory_order_relaxed);
+    return 0;
+}
+
+uint64_t worker_batches() { return g_batches.load(std::memory_order_relaxed); }
+
+bool worker_solve(const uint8_t *h_enc, int K, int m, const uint8_t *M, const uint8_t *P, uint8_t *D)
+{
+    return m >= 1 && m <= kHostSolveMax && host_solve(h_enc, K, m, M, P, D);
+}
 uint64_t worker_served() { return g_served.load(std::memory_order_relaxed); }
 
 int worker_encode(int device, const uint8_t *d_enc, uint64_t mat_id, int K, int N, size_t B, const uint8_t *input,

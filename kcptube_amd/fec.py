@@ -83,6 +83,8 @@ def load_library():
         "kfec_device": (C.c_int, [_vp]),
         "kfec_worker_requests": (C.c_uint64, []),
         "kfec_worker_ping": (C.c_int, [_vp]),
+        "kfec_cached_matrices": (C.c_size_t, [_vp, _szp]),
+        "kfec_worker_batches": (C.c_uint64, []),
         # include/kfec_frame.h
         "kfec_frame_data_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, sz, sz, _vp, _vp, _vp]),
         "kfec_encode_framed_batch": (C.c_int, [_vp, sz, _vp, sz, _vp, _vp, sz, sz, _vp, _vp, _vp]),

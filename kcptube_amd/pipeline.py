@@ -37,6 +37,30 @@ def iv_draw(seed: int, i: int) -> int:
     return (x ^ (x >> 31)) >> 48
 
 
+def worker_batches() -> int:
+    """Small queue flushes served by the resident worker so far (kfec_worker_batches; process-wide)."""
+    from .fec import load_library
+    return int(load_library().kfec_worker_batches())
+
+
+def set_queue_worker_max(n: int) -> None:
+    """Test hook: the largest flush (groups) the queues send to the resident worker (0: always the launch path;
+    -1: back to KFEC_QUEUE_WORKER_MAX / the default)."""
+    from .fec import load_library
+    lib = load_library()
+    lib.kfec_test_queue_worker_max.argtypes = [C.c_long]
+    lib.kfec_test_queue_worker_max(n)
+
+
+def arm_flush_fault(n: int) -> None:
+    """Test hook: make the n-th HIP step (copy, launch, worker request, synchronisation) of the next queue flush
+    fail once with KFEC_EHIP (0: off)."""
+    from .fec import load_library
+    lib = load_library()
+    lib.kfec_test_fail_flush.argtypes = [C.c_int]
+    lib.kfec_test_fail_flush(n)
+
+
 def _mode_and_handle(mode, aead):
     if aead is not None:
         return aead.mode, aead._h

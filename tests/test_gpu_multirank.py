@@ -93,6 +93,12 @@ def test_bench_eight_ranks_match_single_rank():
     assert eight["config"]["global_groups"] == one["config"]["global_groups"] == 16384
     assert eight["recovered_shards_per_step"] == one["recovered_shards_per_step"] == 3 * 16384
     assert eight["combined_digest"] == one["combined_digest"]
+    # per-rank evidence for the driver's SCALE runs: every rank's own event-timed kernels and device
+    pr = eight["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(8))
+    assert all(r["encode_ms"] > 0 and r["decode_ms"] > 0 and r["groups"] == 2048 for r in pr)
+    assert eight["multi_rank"]["devices"] == eight["n_gpus"]
+    assert 0 < eight["multi_rank"]["scaling_efficiency"] <= 1.5
 
 
 def test_bench_refuses_more_ranks_than_gpus():

@@ -54,7 +54,11 @@ def test_device_wide_syncs_are_bounded_while_calls_continue(gpu):
         assert row["a_calls"] > 1000, row
 
 
-def test_worker_that_does_not_answer_falls_back_to_the_launch_path(oracle):
+@pytest.mark.parametrize("poll", ["1", "0"])
+def test_worker_that_does_not_answer_falls_back_to_the_launch_path(oracle, poll):
+    """Both poll modes: direct (every workgroup polls the host line) and relay (KFEC_WORKER_POLL=0: the followers
+    poll workgroup 0's device-memory relay, whose quit value the deaf knob must not swallow, or they spin on and
+    the process cannot exit)."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -80,7 +84,7 @@ def test_worker_that_does_not_answer_falls_back_to_the_launch_path(oracle):
         print("first_call_s %%.3f requests %%d" %% (t_first, worker_requests()))
         del c
     """ % ROOT)
-    env = dict(os.environ, KFEC_WORKER_TEST_DEAF="1")
+    env = dict(os.environ, KFEC_WORKER_TEST_DEAF="1", KFEC_WORKER_POLL=poll)
     env.pop("KFEC_WORKER", None)  # default mode: fall back (KFEC_WORKER=1 would make it an error)
     t0 = time.time()
     r = subprocess.run([sys.executable, "-c", script], cwd=ROOT, capture_output=True, text=True, timeout=120,

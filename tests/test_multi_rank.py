@@ -157,3 +157,26 @@ def test_bench_refuses_oversubscription_without_rehearsal():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--no-cpu"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "bench.py:" in r.stderr
+
+
+def test_bench_device_check_counts_ranks_per_node():
+    """bench.py compares LOCAL_WORLD_SIZE (ranks on this node), not the global world, with the node's GPUs:
+    2 nodes x 4 GPUs (world 8, 4 local ranks) is allowed on a 4-GPU node, 8 local ranks are not."""
+    import bench
+    assert bench.check_devices(4, 4, False) is None
+    assert "only 4 visible" in bench.check_devices(8, 4, False)
+
+
+def test_per_rank_summary():
+    """The multi-rank evidence: distinct devices over every rank, and value / (world x rank 0's own rate)."""
+    import bench
+    recs = [{"rank": r, "device": f"h{r // 4}:dev{r % 4}", "wall_ms_per_step": 10.0 + r, "groups": 100}
+            for r in range(8)]
+    payload = [1 << 30] * 8  # 1 GiB per rank per step
+    value = 8 * (1 << 30) / 0.017 / 2**30  # what bench.py reports: all payload / the slowest rank's time
+    s = bench.per_rank_summary(recs, value, payload)
+    assert s["devices"] == 8 and s["slowest_rank"] == 7
+    assert abs(s["rank0_equivalent_GiBps"] - 100.0) < 1e-6
+    assert abs(s["scaling_efficiency"] - 10.0 / 17.0) < 1e-3
+    one_dev = [dict(r, device="h0:dev0") for r in recs]  # a rehearsal: every rank on one GPU
+    assert bench.per_rank_summary(one_dev, value, payload)["devices"] == 1
