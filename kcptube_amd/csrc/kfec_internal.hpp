@@ -24,14 +24,13 @@ inline size_t record_stride(size_t K, size_t R)
     const size_t coef = (4 + rec_k4(K) + R * rec_k4(K) + 15) & ~size_t(15);
     return coef > 112 ? coef : 112;
 }
-// after the G records (256-aligned): the syndrome decode's active-group list -- a count and the bucketed
-// decode's per-mask counts / first slots (256 bytes), per-1024-group chunk counts / offsets (8 per chunk: one
-// per used-row mask), then the list of up to G group ids (uint32 each)
+// after the G records (256-aligned): the syndrome decode's active-group list -- a count (+ 252 bytes of
+// padding), per-1024-group chunk counts / offsets, then the list of up to G group ids (uint32 each)
 inline size_t decode_list_offset(size_t G, size_t K, size_t R) { return (G * record_stride(K, R) + 255) & ~size_t(255); }
 inline size_t decode_list_chunks(size_t G) { return (G + 1023) / 1024; }
 inline size_t decode_workspace_bytes(size_t G, size_t K, size_t R)
 {
-    return decode_list_offset(G, K, R) + 256 + 32 * decode_list_chunks(G) + 4 * G;
+    return decode_list_offset(G, K, R) + 256 + 4 * decode_list_chunks(G) + 4 * G;
 }
 
 // The encoding matrix allocation also holds the perm-MAC tables of its parity rows (gf_perm_tables, 5 dwords
@@ -62,7 +61,8 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
                   const void *d_data, const void *d_parity, const uint64_t *d_present, void *d_out,
                   uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s);
 int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, const uint64_t *d_present,
-                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s, bool syn = false);
+                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s, bool syn = false,
+                       bool factored = false);
 int launch_synth(uint64_t seed, int N, size_t g0, size_t G, size_t s0, size_t ns, size_t B, size_t pitch,
                  void *d_out, hipStream_t s);
 int launch_erasure_masks(uint64_t seed, int N, size_t g0, size_t G, size_t pool, size_t count_max,

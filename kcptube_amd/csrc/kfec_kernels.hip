@@ -78,15 +78,15 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #ifndef KFEC_SYN_REC_COMPACT
 #define KFEC_SYN_REC_COMPACT 1  // syndrome records of 40 + 8 RT bytes (64 at R = 3: one full line per group)
 #endif
-#ifndef KFEC_SYN_BUCKET
-#define KFEC_SYN_BUCKET 1  // R <= 3 dense decode over per-row-mask group lists (syn_bucket_kernel); 0: syn_kernel (A/B)
-#endif
 #ifndef KFEC_SYN_ROWMASK
 #define KFEC_SYN_ROWMASK 1  // listed syndrome decode: 0 every parity row, 1 only the rows the group uses,
                             // 2 as 1 but single-row groups run a two-row variant (A/B knob)
 #endif
 #ifndef KFEC_MINW
 #define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the MAC kernels
+#endif
+#ifndef KFEC_DEC_FACTORED
+#define KFEC_DEC_FACTORED 1  // R > 8 decode records carry the Lagrange factors, not the m x K coefficients (A/B knob)
 #endif
 #ifndef KFEC_DEC_TTAB
 #define KFEC_DEC_TTAB 1  // coefficient-form decode (R > 8): LDS entries point into one table of all 256 coefficients'
@@ -203,8 +203,23 @@ struct PrepArgs {
     uint64_t G;
     int K, N, R;
     uint32_t rec_stride;
-    int syn;  // write syndrome-form records (R <= 8) instead of the coefficient form
+    int syn;       // write syndrome-form records (R <= 8) instead of the coefficient form
+    int factored;  // decode_prep_lagrange: write the factored form (dec_expand rebuilds each coefficient)
 };
+
+// Factored coefficient-form record (decode_prep_lagrange for the mac_kernel decode, KFEC_DEC_FACTORED): the
+// m x K coefficients of a group are coef[u][j] = exp(lnum_u - log(xm_u ^ xs_j) - lden_j) (see the prep), so the
+// record keeps the factors -- src[j] (and with it the point xs_j), lden_j, lnum_u and the missing points xm_u --
+// 2 K + 2 R bytes instead of m K: at fec=200:55, 528 bytes per group instead of 11 KB, which the prep no longer
+// writes and the MAC's row tiles no longer read (2.9 GB each way per 256k groups).
+//   [0] status, [1] m, [4, 4 + K4) src, [4 + K4, 4 + 2 K4) lden, [L0, L0 + R8) lnum, [L0 + R8, L0 + 2 R8) xm,
+//   L0 = round16(4 + 2 K4), R8 = round8(R)
+__host__ __device__ inline uint32_t fac_lnum_off(uint32_t K) { return (4 + 2 * ((K + 3) & ~3u) + 15) & ~15u; }
+__host__ __device__ inline uint32_t fac_r8(uint32_t R) { return (R + 7) & ~7u; }
+__host__ __device__ inline size_t fac_record_stride(size_t K, size_t R)
+{
+    return (fac_lnum_off((uint32_t)K) + 2 * fac_r8((uint32_t)R) + 15) & ~size_t(15);
+}
 
 // (no early return: the unrolled q index stays a constant, so w[] lives in registers, not scratch)
 __device__ __forceinline__ int pop_lowest(uint64_t (&w)[4])
@@ -745,6 +760,35 @@ __global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagr
 #endif
         __syncthreads();
         uint32_t *srcw = reinterpret_cast<uint32_t *>(rec + 4);
+        if (a.factored) {
+            // the factors only (see fac_record_stride): src and lden as dwords of 4 columns, lnum and xm per row
+            const uint32_t L0 = fac_lnum_off((uint32_t)K), R8 = fac_r8((uint32_t)R);
+            uint32_t *ldw = reinterpret_cast<uint32_t *>(rec + 4 + K4);
+            for (int d = tid; d < kd; d += kPrepThreads) {
+                uint32_t v = 0, l = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (4 * d + b < K) {
+                        v |= (uint32_t)s_src[4 * d + b] << (8 * b);
+                        l |= (uint32_t)s_lden[4 * d + b] << (8 * b);
+                    }
+                srcw[d] = v;
+                ldw[d] = l;
+            }
+            for (int u = tid; u < m; u += kPrepThreads) {
+                rec[L0 + u] = (uint8_t)s_lnum[u];
+                rec[L0 + R8 + u] = (uint8_t)xpt(s_M[u]);
+            }
+            for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
+            if (tid == 0) {
+                rec[0] = 0;
+                rec[1] = (uint8_t)m;
+                rec[2] = rec[3] = 0;
+                a.status[g] = 0;
+            }
+            __syncthreads();  // the lists are rewritten for the next group
+            continue;
+        }
         uint32_t *coefw = reinterpret_cast<uint32_t *>(rec + 4 + K4);
         for (int d = tid; d < kd; d += kPrepThreads) {
             uint32_t v = 0;
@@ -809,6 +853,7 @@ struct MacArgs {
     uint32_t JC;            // shards per LDS chunk
     uint32_t gmax;          // group slots per chunk
     uint32_t tiles;         // row tiles of MT output rows
+    uint32_t factored;      // decode: factored records (fac_record_stride), coefficients rebuilt by dec_expand
 };
 
 template <int VEC>
@@ -985,7 +1030,7 @@ __device__ __forceinline__ void dec_build_t(uint8_t *s_T)
 // entries of shards [c0, c0 + nj) for group slots [0, ng): share pointer + MT u16 offsets into T
 template <int MT>
 __device__ __forceinline__ void dec_expand(const MacArgs &a, uint8_t *s_ent, uint32_t gfirst, uint32_t ng, uint32_t c0,
-                                           uint32_t nj, uint32_t row0)
+                                           uint32_t nj, uint32_t row0, const uint8_t *s_exp, const uint8_t *s_log)
 {
     static_assert(MT == 8, "entry: 8 offsets");
     const uint32_t items = ng * nj, K4 = (a.K + 3) & ~3u;
@@ -999,8 +1044,21 @@ __device__ __forceinline__ void dec_expand(const MacArgs &a, uint8_t *s_ent, uin
             const uint8_t *rec = a.rec + (uint64_t)(gfirst + gs) * a.rec_stride;
             hd[b] = *reinterpret_cast<const uint16_t *>(rec);  // status | m << 8
             sv[b] = rec[4 + j];
+            if (a.factored) {
+                const uint32_t L0 = fac_lnum_off(a.K), R8 = fac_r8(a.R);
+                const uint2 ln = *reinterpret_cast<const uint2 *>(rec + L0 + row0);  // (row0 % 8 == 0, rows < R8)
+                const uint2 xm = *reinterpret_cast<const uint2 *>(rec + L0 + R8 + row0);
+                const uint32_t ld = rec[4 + K4 + j];
 #pragma unroll
-            for (int r = 0; r < MT; ++r) cv[b][r] = rec[4 + K4 + min(row0 + r, a.R - 1) * K4 + j];
+                for (int r = 0; r < MT; ++r) {
+                    const uint32_t lnr = ((r < 4 ? ln.x : ln.y) >> (8 * (r & 3))) & 0xFFu;
+                    const uint32_t xmr = ((r < 4 ? xm.x : xm.y) >> (8 * (r & 3))) & 0xFFu;
+                    cv[b][r] = lnr | (xmr << 8) | (ld << 16);  // (combined below, after every load is issued)
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < MT; ++r) cv[b][r] = rec[4 + K4 + min(row0 + r, a.R - 1) * K4 + j];
+            }
         }
 #pragma unroll
         for (int b = 0; b < EB; ++b) {
@@ -1014,6 +1072,19 @@ __device__ __forceinline__ void dec_expand(const MacArgs &a, uint8_t *s_ent, uin
             *reinterpret_cast<const uint8_t **>(ent) = p;
             const bool ok = (hd[b] & 0xFFu) == 0;
             const uint32_t m = hd[b] >> 8;
+            // the tile's coefficients of (group, column j) from the record's factors: exp(lnum_u - log(xm_u ^ xs_j)
+            // - lden_j), two lookups each in the workgroup's GF tables; the exponent in [1, 764] is brought under the
+            // doubled antilog table by one compare (as the prep does)
+            if (a.factored) {
+                const uint32_t xs = src ? (uint32_t)s_exp[src] : 0u;  // the point of the column's share (x_0 = 0)
+#pragma unroll
+                for (int r = 0; r < MT; ++r) {
+                    const uint32_t v = cv[b][r];
+                    int ex = (int)(v & 0xFFu) + 510 - (int)s_log[((v >> 8) & 0xFFu) ^ xs] - (int)(v >> 16);
+                    ex = ex >= 510 ? ex - 255 : ex;
+                    cv[b][r] = s_exp[ex];
+                }
+            }
             uint32_t o[MT];
 #pragma unroll
             for (int r = 0; r < MT; ++r) o[r] = (ok && row0 + r < m) ? cv[b][r] * 32u : 0u;  // T[0] = zero tables
@@ -1049,12 +1120,18 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     const bool enc_once = !DEC && K <= a.JC;
     constexpr bool ttab = DEC && KFEC_DEC_TTAB && MT == 8;
     uint8_t *s_T = s_ent;
-    uint8_t *s_E = ttab ? s_ent + kTBytes : s_ent;  // entries (after T)
+    // ttab: T, then (factored records) the GF exp / log tables, then the entries
+    constexpr uint32_t kGfBytes = ttab ? 768u : 0u;
+    uint8_t *s_gexp = s_ent + kTBytes, *s_glog = s_gexp + 512;
+    uint8_t *s_E = ttab ? s_ent + kTBytes + kGfBytes : s_ent;  // entries (after T)
     if (enc_once) {
         mac_expand<MT, false>(a, s_ent, 0, 1, 0, K, row0);
         __syncthreads();
     }
-    if constexpr (ttab) dec_build_t(s_T);  // (ordered by the first chunk's barrier below)
+    if constexpr (ttab) {
+        dec_build_t(s_T);  // (ordered by the first chunk's barrier below)
+        if (a.factored) stage_gf(s_gexp, s_glog);
+    }
     const uint32_t item = base + threadIdx.x;
     const bool in = item < a.total;
     const uint32_t g = in ? item / cols : 0;
@@ -1086,7 +1163,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
         const uint32_t nj = min(a.JC, K - c0);
         if (!enc_once) {
             if (!ttab || c0 > 0) __syncthreads();  // (ttab: nothing to protect before the first chunk)
-            if constexpr (ttab) dec_expand<MT>(a, s_E, gfirst, ng, c0, nj, row0);
+            if constexpr (ttab) dec_expand<MT>(a, s_E, gfirst, ng, c0, nj, row0, s_gexp, s_glog);
             else mac_expand<MT, DEC>(a, s_ent, gfirst, DEC ? ng : 1u, c0, nj, row0);
             __syncthreads();
         }
@@ -1191,9 +1268,8 @@ struct SynArgs {
     uint8_t *out;             // [G][R][pitch] recovered data shards, ascending index
     const uint8_t *rec;       // syndrome-form records (kfec_internal.hpp)
     const uint32_t *etab;     // [K][etab_rows][5] perm tables of the parity rows (zero slack rows)
-    const uint32_t *list;     // ids of the groups with data to recover (active_* / bucket_* kernels)
+    const uint32_t *list;     // ascending ids of the groups with data to recover (active_* kernels)
     const uint32_t *list_count;
-    const uint32_t *bucket;   // bucket_* kernels: [8] groups per used-row mask, [8..16) each mask's first list slot
     uint64_t pitch;
     uint32_t total, cols, cols_pad, G, K, R, B, rec_stride, etab_rows;
 };
@@ -1539,154 +1615,6 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_kernel(SynArgs a
 #endif
 }
 
-// ---- bucketed dense decode (R <= 3, KFEC_SYN_BUCKET) ----------------------------------------------------
-// A group that lost m data shards uses m parity rows (its `used` mask, one bit per row).  syn_kernel computes
-// every row for every group (RT = R; the per-wave row-mask variants cost it registers and occupancy), and its
-// lanes of groups with nothing to recover idle.  Here the groups with data to recover are listed per mask
-// (bucket_* kernels, ascending group order within a mask) and each workgroup takes items (listed group, column)
-// of ONE mask's list: its waves compute exactly the popcount(mask) rows in use (RT = m: 1 or 2 rows for most
-// groups under random 1-3 erasures of 13 shards), with the mask's rows picked by uniform offsets into the same
-// scalar E tables.  Loads are global loads through pointers (a wave's groups are list entries, not a contiguous
-// range a buffer resource could cover); an absent share reads g_zero_gran instead of skipping the load.
-__device__ uint32_t g_zero_gran[8];  // never written
-
-template <int VEC, int RT, int PD>
-__device__ __forceinline__ void bucket_loop(const SynArgs &a, uint32_t (&acc)[RT][Gran<VEC>::W], const uint8_t *drow,
-                                            const uint8_t *prow, const uint32_t (&rows)[RT], const uint8_t *rec,
-                                            uint64_t p0, bool in)
-{
-    constexpr int W = Gran<VEC>::W;
-    const uint32_t K = a.K;
-    const uint64_t pitch = a.pitch;
-    const uint8_t *zero = reinterpret_cast<const uint8_t *>(g_zero_gran);
-#pragma unroll
-    for (int q = 0; q < RT; ++q) {  // the parity shares of the rows in use start the accumulators
-        const Gran<VEC> y = load_gran<VEC>(in ? prow + rows[q] * pitch : zero, 0, a.B);
-#pragma unroll
-        for (int w = 0; w < W; ++w) acc[q][w] = y.d[w];
-    }
-    const uint64_t *pr = reinterpret_cast<const uint64_t *>(rec + 8);
-    const uint64_t p1 = K > 64 ? pr[1] : 0ull, p2 = K > 128 ? pr[2] : 0ull, p3 = K > 192 ? pr[3] : 0ull;
-    auto dptr = [&](uint32_t j) -> const uint8_t * {
-        const uint64_t wq = j < 64 ? p0 : (j < 128 ? p1 : (j < 192 ? p2 : p3));
-        return (in && ((wq >> (j & 63u)) & 1ull)) ? drow + j * pitch : zero;
-    };
-    typedef const __attribute__((address_space(4))) uint32_t cu32;  // uniform: scalar loads into SGPRs
-    uint32_t tn[5 * RT];
-    auto tload = [&](uint32_t j) {
-        const cu32 *tg = (const cu32 *)(a.etab + (size_t)min(j, K - 1) * a.etab_rows * 5);
-#pragma unroll
-        for (int q = 0; q < RT; ++q)
-#pragma unroll
-            for (int i = 0; i < 5; ++i) tn[5 * q + i] = tg[5 * rows[q] + i];
-    };
-    tload(0);
-    auto mac = [&](const Gran<VEC> &cur, uint32_t j) {
-        uint32_t t[5 * RT];
-#pragma unroll
-        for (int i = 0; i < 5 * RT; ++i) t[i] = tn[i];
-        tload(j + 1);
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            const uint32_t xv = cur.d[w];
-            const uint32_t s0 = xv & 0x07070707u, s1 = (xv >> 3) & 0x07070707u, s2 = (xv >> 6) & 0x03030303u;
-#pragma unroll
-            for (int q = 0; q < RT; ++q) acc[q][w] = perm_mac(acc[q][w], t + 5 * q, s0, s1, s2);
-        }
-    };
-    Gran<VEC> x[PD];
-#pragma unroll
-    for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(dptr(min((uint32_t)u, K - 1)), 0, a.B);
-    uint32_t jb = 0;
-    for (; jb + PD <= K; jb += PD) {
-#pragma unroll
-        for (int u = 0; u < PD; ++u) {
-            mac(x[u], jb + u);
-            x[u] = load_gran<VEC>(dptr(min(jb + u + PD, K - 1)), 0, a.B);
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < PD; ++u)
-        if (jb + u < K) mac(x[u], jb + u);
-}
-
-template <int VEC, int RT>
-__device__ __forceinline__ void syn_bucket_body(const SynArgs &a, uint32_t mask, uint32_t blk, uint32_t base, uint32_t cnt,
-                                                uint32_t *s_ct)
-{
-    constexpr int W = Gran<VEC>::W;
-    constexpr int PD = VEC >= 32 ? KFEC_PD : 2 * KFEC_PD;
-    constexpr int TD = SynLayout<RT>::TD;
-    uint32_t rows[RT];
-    {
-        uint32_t mm = mask;
-#pragma unroll
-        for (int q = 0; q < RT; ++q) {
-            rows[q] = (uint32_t)__builtin_ctz(mm | 0x100u);
-            mm &= mm - 1u;
-        }
-    }
-    const uint32_t cols = a.cols, nitems = cnt * cols;
-    const uint32_t item0 = blk * kMacBlock, item = item0 + threadIdx.x;
-    const bool in = item < nitems;
-    const uint32_t li = min(item, nitems - 1) / cols;
-    const uint32_t col = min(item, nitems - 1) - li * cols;
-    const uint32_t off = gran_off<VEC>(col, a.B);
-    // this wave's list slots and their C tables (built and read by this wave only, as syn_kernel's)
-    const uint32_t wli0 = min(item0 + (threadIdx.x & ~63u), nitems - 1) / cols;
-    const uint32_t wli1 = min(item0 + (threadIdx.x | 63u), nitems - 1) / cols;
-    uint32_t *ctw = s_ct + (threadIdx.x / 64) * syn_wave_groups(cols) * RT * TD;
-    const uint32_t ne = (wli1 - wli0 + 1) * RT * RT;
-    const uint32_t e0 = threadIdx.x & 63u;
-    const uint32_t e0s = min(e0, ne - 1) / (RT * RT), e0ur = min(e0, ne - 1) - e0s * (RT * RT);
-    const uint32_t g = a.list[base + li];
-    const uint32_t g_e0 = a.list[base + wli0 + e0s];
-    // C[u][rows[r]] of entry (u, r) (listed groups have status 0), loaded now and expanded after the shard loop
-    const uint32_t c_e0 = a.rec[(uint64_t)g_e0 * a.rec_stride + 40 + 8 * (e0ur / RT) + rows[e0ur % RT]];
-    const uint8_t *rec = a.rec + (uint64_t)g * a.rec_stride;
-    const uint4 h = *reinterpret_cast<const uint4 *>(rec);  // header + present data bits 0..63
-    const uint64_t p0 = (uint64_t)h.z | ((uint64_t)h.w << 32);
-    uint32_t acc[RT][W];
-    bucket_loop<VEC, RT, PD>(a, acc, a.data + (uint64_t)g * a.K * a.pitch + off, a.parity + (uint64_t)g * a.R * a.pitch + off,
-                             rows, rec, p0, in);
-    if (e0 < ne) syn_expand_put<RT>(c_e0, e0ur, ctw + e0s * RT * TD);
-    for (uint32_t e = e0 + 64; e < ne; e += 64) {  // (more than 64 entries: rows of < 64 bytes)
-        const uint32_t es = e / (RT * RT), ur = e - es * (RT * RT);
-        const uint32_t ge = a.list[base + wli0 + es];
-        syn_expand_put<RT>(a.rec[(uint64_t)ge * a.rec_stride + 40 + 8 * (ur / RT) + rows[ur % RT]], ur, ctw + es * RT * TD);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (this wave's LDS writes before its reads)
-    if (in) syn_final<VEC, RT>(a, acc, ctw + (li - wli0) * RT * TD, RT, g, off, col);
-}
-
-template <int VEC>
-__global__ void __launch_bounds__(kMacBlock, KFEC_SYN_MINW) syn_bucket_kernel(SynArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_ct[];  // [wave][group slot][RT][TD]
-    if (a.list_count && syn_listed(a, *a.list_count)) return;  // sparse loss: the listed kernel has it
-    // the mask list this workgroup works on: masks 1..7 in order, ceil(count * cols / 256) workgroups each
-    uint32_t blk = blockIdx.x, mask = 0, base = 0, cnt = 0;
-#pragma unroll
-    for (uint32_t m = 1; m < 8; ++m) {
-        const uint32_t c = a.bucket[m], nb = (c * a.cols + kMacBlock - 1) / kMacBlock;
-        if (mask == 0) {
-            if (blk < nb) {
-                mask = m;
-                cnt = c;
-                base = a.bucket[8 + m];
-            } else {
-                blk -= nb;
-            }
-        }
-    }
-    if (mask == 0) return;
-    switch (__popc(mask)) {
-    case 1: syn_bucket_body<VEC, 1>(a, mask, blk, base, cnt, s_ct); break;
-    case 2: syn_bucket_body<VEC, 2>(a, mask, blk, base, cnt, s_ct); break;
-    default: syn_bucket_body<VEC, 3>(a, mask, blk, base, cnt, s_ct); break;
-    }
-}
-
 // ---- ordered list of the groups with data to recover (out_idx[g * R] != 0xFF), for syn_kernel's listed
 // shape: per-chunk counts, one exclusive scan, a scatter that keeps group order.  kActChunk groups per
 // 256-thread workgroup, 4 per thread.
@@ -1766,91 +1694,6 @@ __global__ void __launch_bounds__(kBlock) active_scatter_kernel(uint64_t G, uint
         if ((f >> k) & 1u) list[at++] = (uint32_t)(g0 + k);
 }
 
-// Per-mask lists for syn_bucket_kernel (R <= 3): every group with data to recover (status 0, m > 0) goes to the
-// list of its used-row mask (1..7), ascending within a mask; the lists are concatenated in mask order, so the
-// whole is also the listed kernel's list.  chunk_cnt: [8][nch] per-chunk counts, then offsets; bucket: [8]
-// counts, [8..16) first slots; *count: their sum.
-__device__ __forceinline__ uint32_t bucket_fields(uint64_t G, const uint8_t *rec, uint32_t rs, uint64_t g0)
-{
-    uint32_t f = 0;  // 3 bits per group: its mask, 0 if it recovers nothing
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint64_t g = g0 + k;
-        if (g < G) {
-            const uint32_t h = *reinterpret_cast<const uint32_t *>(rec + g * rs);
-            if ((h & 0xFFu) == 0 && ((h >> 8) & 0xFFu) != 0) f |= ((h >> 16) & 7u) << (3 * k);
-        }
-    }
-    return f;
-}
-
-__device__ __forceinline__ uint32_t bucket_hits(uint32_t f, uint32_t m)
-{
-    uint32_t b = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) b |= (((f >> (3 * k)) & 7u) == m ? 1u : 0u) << k;
-    return b;
-}
-
-__global__ void __launch_bounds__(kBlock) bucket_count_kernel(uint64_t G, const uint8_t *rec, uint32_t rs, uint32_t nch,
-                                                              uint32_t *chunk_cnt)
-{
-    __shared__ uint32_t s_w[4];
-    const uint32_t f = bucket_fields(G, rec, rs, (uint64_t)blockIdx.x * kActChunk + threadIdx.x * 4u);
-    for (uint32_t m = 1; m < 8; ++m) {
-        uint32_t total = 0;
-        (void)block_exclusive(__popc(bucket_hits(f, m)), s_w, total);
-        if (threadIdx.x == 0) chunk_cnt[m * nch + blockIdx.x] = total;
-        __syncthreads();  // s_w is reused
-    }
-}
-
-__global__ void __launch_bounds__(kBlock) bucket_scan_kernel(uint32_t nch, uint32_t *chunk_cnt, uint32_t *bucket,
-                                                             uint32_t *count)
-{
-    __shared__ uint32_t s_w[4];
-    uint32_t first = 0;
-    for (uint32_t m = 1; m < 8; ++m) {
-        uint32_t carry = 0;
-        for (uint32_t c0 = 0; c0 < nch; c0 += kBlock) {
-            const uint32_t c = c0 + threadIdx.x;
-            const uint32_t v = c < nch ? chunk_cnt[m * nch + c] : 0u;
-            uint32_t total = 0;
-            const uint32_t ex = block_exclusive(v, s_w, total);
-            if (c < nch) chunk_cnt[m * nch + c] = carry + ex;
-            carry += total;
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) {
-            bucket[m] = carry;
-            bucket[8 + m] = first;
-        }
-        first += carry;
-    }
-    if (threadIdx.x == 0) {
-        bucket[0] = bucket[8] = 0;
-        *count = first;
-    }
-}
-
-__global__ void __launch_bounds__(kBlock) bucket_scatter_kernel(uint64_t G, const uint8_t *rec, uint32_t rs, uint32_t nch,
-                                                                const uint32_t *chunk_off, const uint32_t *bucket,
-                                                                uint32_t *list)
-{
-    __shared__ uint32_t s_w[4];
-    const uint64_t g0 = (uint64_t)blockIdx.x * kActChunk + threadIdx.x * 4u;
-    const uint32_t f = bucket_fields(G, rec, rs, g0);
-    for (uint32_t m = 1; m < 8; ++m) {
-        const uint32_t hits = bucket_hits(f, m);
-        uint32_t total = 0;
-        uint32_t at = bucket[8 + m] + chunk_off[m * nch + blockIdx.x] + block_exclusive(__popc(hits), s_w, total);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if ((hits >> k) & 1u) list[at++] = (uint32_t)(g0 + k);
-        __syncthreads();
-    }
-}
-
 // ---------------------------------------------------------------------------------------------------
 // host-side launch helpers
 // ---------------------------------------------------------------------------------------------------
@@ -1880,7 +1723,8 @@ template <int VEC, int MT, bool DEC, int PDX = 0>
 static int run_mac(MacArgs a, hipStream_t s)
 {
     using L = MacLayout<MT>;
-    const size_t lds = (DEC && KFEC_DEC_TTAB && MT == 8) ? kTBytes + (size_t)a.gmax * a.JC * kDecEntry : (size_t)a.gmax * a.JC * L::ENTRY;
+    const size_t lds = (DEC && KFEC_DEC_TTAB && MT == 8) ? kTBytes + 768 + (size_t)a.gmax * a.JC * kDecEntry
+                                                         : (size_t)a.gmax * a.JC * L::ENTRY;
     const uint32_t chunks = (a.total + kMacBlock - 1) / kMacBlock;
     const uint32_t nb = a.tiles > 1 ? ((chunks + 7) & ~7u) * a.tiles : chunks;
     hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), lds, s, a);
@@ -1979,24 +1823,6 @@ static int dispatch_syn(int vec, int rt, SynArgs a, size_t lds, int cus, hipStre
 #undef KFEC_RT_CASES
 }
 
-// the bucketed dense decode (R <= 3) and, for sparse loss, the listed kernel over the same (concatenated) list
-static int run_syn_bucket(SynArgs a, int rt, int cus, hipStream_t s)
-{
-    // a workgroup per 256 items of each mask's list: at most the items of all groups plus one partial
-    // workgroup per mask (the surplus ones find no mask and leave)
-    const uint32_t nb = (a.total + kMacBlock - 1) / kMacBlock + 7;
-    const size_t lds = (size_t)(kMacBlock / 64) * syn_wave_groups(a.cols) * 3 * SynLayout<3>::TD * 4;
-    hipLaunchKernelGGL((syn_bucket_kernel<32>), dim3(nb), dim3(kMacBlock), lds, s, a);
-    const uint64_t tasks = (uint64_t)a.G * (a.cols_pad / 64);
-    const uint32_t nl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((tasks + 3) / 4, (uint64_t)std::max(cus, 1) * 8));
-    switch (rt) {
-    case 1: hipLaunchKernelGGL((syn_list_kernel<32, 1>), dim3(nl), dim3(kMacBlock), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((syn_list_kernel<32, 2>), dim3(nl), dim3(kMacBlock), 0, s, a); break;
-    default: hipLaunchKernelGGL((syn_list_kernel<32, 3>), dim3(nl), dim3(kMacBlock), 0, s, a); break;
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
 static constexpr size_t kLdsBudget = 32 * 1024;
 static constexpr size_t kDecLdsBudget = 40 * 1024;  // T-table decode entries (+ 8 KiB of T): 3 workgroups per CU
 static constexpr size_t kSynLdsMax = 64 * 1024;
@@ -2053,12 +1879,13 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
 // records) of every group into d_workspace (+ d_out_idx, d_status).  The MAC kernels here and in
 // kfec_frame.hip consume them.
 int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, const uint64_t *d_present,
-                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s, bool syn)
+                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s, bool syn, bool factored)
 {
     const int R = N - K;
     if (G == 0) return 0;
     uint8_t *rec = static_cast<uint8_t *>(d_workspace);
-    const size_t rs = syn ? syn_record_stride(K, R) : record_stride(K, R);
+    factored = factored && !syn && std::min(K, R) > 8;  // (only decode_prep_lagrange writes the factored form)
+    const size_t rs = syn ? syn_record_stride(K, R) : factored ? fac_record_stride(K, R) : record_stride(K, R);
     PrepArgs p{};
     p.present = d_present;
     p.enc = d_enc;
@@ -2069,6 +1896,7 @@ int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N,
     p.K = K; p.N = N; p.R = R;
     p.rec_stride = (uint32_t)rs;
     p.syn = syn ? 1 : 0;
+    p.factored = factored ? 1 : 0;
     const int mmax = std::min(K, R);
     if (mmax <= 8) {
         const size_t lds = 768 + (size_t)R * K;
@@ -2115,13 +1943,15 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     const bool syn = R > 0 && R <= KFEC_SYN_MAX_R && lds_syn <= kSynLdsMax && vec != 1 &&
                      gmax_syn * (size_t)K * pitch < (size_t(1) << 31) && gmax_syn * (size_t)R * pitch < (size_t(1) << 31) &&
                      G * (size_t)R < (size_t(1) << 32);
-    if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s, syn)) return -3;
+    // (the mac_kernel decode rebuilds the coefficients of factored records; the prep writes them for K, R > 8)
+    const bool factored = !syn && KFEC_DEC_FACTORED && KFEC_DEC_TTAB && std::min(K, R) > 8;
+    if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s, syn, factored)) return -3;
     if (R == 0 || B == 0) return 0;
     if (syn) {
         const size_t rs_syn = syn_record_stride(K, R);  // (the prep wrote syndrome records)
         uint32_t *count = reinterpret_cast<uint32_t *>(rec + decode_list_offset(G, K, R));
         uint32_t *chunk_cnt = count + 64;
-        uint32_t *list = chunk_cnt + 8 * decode_list_chunks(G);
+        uint32_t *list = chunk_cnt + decode_list_chunks(G);
         const size_t cols_pad = (cols + 63) / 64 * 64;
         const size_t lds = lds_syn;
         return for_group_ranges(G, cols, 1, [&](size_t g0, size_t gn) {
@@ -2131,17 +1961,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
             const bool small = gn <= kLatencyGroups;
             const uint32_t nch = (uint32_t)((gn + kActChunk - 1) / kActChunk);
             const uint8_t *oi = d_out_idx + g0 * R;
-            const bool bucketed = KFEC_SYN_BUCKET && !small && R <= 3 && vec == 32;
-            uint32_t *bucket = count + 16;  // (the list header's free bytes)
-            if (bucketed) {
-                const uint8_t *rg = rec + g0 * rs_syn;
-                hipLaunchKernelGGL(bucket_count_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)gn, rg, (uint32_t)rs_syn,
-                                   nch, chunk_cnt);
-                hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(kBlock), 0, s, nch, chunk_cnt, bucket, count);
-                hipLaunchKernelGGL(bucket_scatter_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)gn, rg, (uint32_t)rs_syn,
-                                   nch, (const uint32_t *)chunk_cnt, (const uint32_t *)bucket, list);
-                if (hipGetLastError() != hipSuccess) return -3;
-            } else if (!small) {
+            if (!small) {
                 hipLaunchKernelGGL(active_count_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)gn, (uint32_t)R, oi, chunk_cnt);
                 hipLaunchKernelGGL(active_scan_kernel, dim3(1), dim3(kBlock), 0, s, nch, chunk_cnt, count);
                 hipLaunchKernelGGL(active_scatter_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)gn, (uint32_t)R, oi,
@@ -2156,7 +1976,6 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
             a.etab = reinterpret_cast<const uint32_t *>(d_enc + enc_tab_offset(K, N));
             a.list = list;
             a.list_count = small ? nullptr : count;  // nullptr: dense only (syn_kernel runs, no listed launch)
-            a.bucket = bucket;
             a.etab_rows = (uint32_t)enc_tab_rows(R);
             a.pitch = pitch;
             a.total = (uint32_t)(gn * cols);
@@ -2165,7 +1984,6 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
             a.G = (uint32_t)gn;
             a.K = K; a.R = R; a.B = (uint32_t)B;
             a.rec_stride = (uint32_t)rs_syn;
-            if (bucketed) return run_syn_bucket(a, rt, di.cus, s);
             return dispatch_syn(vec, rt, a, lds, di.cus, s);
         });
     }
@@ -2191,7 +2009,8 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.cols = (uint32_t)cols;
         a.G = (uint32_t)gn;
         a.K = K; a.R = R; a.B = (uint32_t)B;
-        a.rec_stride = (uint32_t)rs;
+        a.rec_stride = (uint32_t)(factored ? fac_record_stride(K, R) : rs);
+        a.factored = factored ? 1u : 0u;
         a.JC = JC;
         a.gmax = gmax;
         a.tiles = (uint32_t)tiles;

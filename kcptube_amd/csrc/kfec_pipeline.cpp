@@ -20,6 +20,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -100,6 +102,40 @@ struct Steps {
         ++k;
         int f = fail_at();
         return f > 0 && k == f && g_fail_at.compare_exchange_strong(f, 0);
+    }
+};
+
+// KFEC_QUEUE_TRACE=1: per-phase host times of the small flushes (worker paths), summed per queue and printed to
+// stderr when the queue is destroyed (diagnostics)
+struct Trace {
+    static bool on()
+    {
+        static const bool v = env_flag("KFEC_QUEUE_TRACE", false);
+        return v;
+    }
+    double us[6] = {};
+    uint64_t n = 0;
+    std::chrono::steady_clock::time_point t;
+    int k = 0;
+    void start()
+    {
+        if (!on()) return;
+        t = std::chrono::steady_clock::now();
+        k = 0;
+    }
+    void mark()
+    {
+        if (!on() || k >= 6) return;
+        const auto now = std::chrono::steady_clock::now();
+        us[k++] += std::chrono::duration<double, std::micro>(now - t).count();
+        t = now;
+    }
+    void done() { n += on() ? 1 : 0; }
+    void print(const char *what) const
+    {
+        if (!on() || !n) return;
+        fprintf(stderr, "kfec %s: %llu small flushes, us each: prep %.2f worker %.2f launch %.2f sync %.2f emit %.2f\n",
+                what, (unsigned long long)n, us[0] / n, us[1] / n, us[2] / n, us[3] / n, us[4] / n);
     }
 };
 
@@ -211,9 +247,11 @@ struct Arena {
     size_t align = 4;     // staging granule (offsets and lengths rounded up to it)
     size_t reserve = 0;   // device image bytes past cap: the sealed small flush's redundant-packet rows
     Upload up;            // (pinned mode)
-    int init(int device, size_t bytes, bool use_bar, size_t extra = 0)
+    int init(int device, size_t bytes, bool use_bar, size_t max_groups, size_t extra = 0)
     {
-        bar_ok = bar = use_bar;
+        // until the first flush says otherwise (set_mode): BAR mode when the queue cannot hold a large flush
+        bar_ok = use_bar;
+        bar = use_bar && max_groups <= bar_flush_max();
         d.uncached = use_bar;
         align = use_bar ? bar_align() : 4;
         reserve = use_bar ? extra : 0;
@@ -406,7 +444,9 @@ struct kfec_txq {
     Pinned h_sdesc, h_sealed;  // seal descriptors (+ iv draws) up; sealed rows + lengths down
     Device d_sdesc, d_sealed;
     OwnStream own;
+    Trace trace;
     Arena arena;  // declared last: destroyed (and its copy stream drained) first
+    ~kfec_txq() { trace.print("txq"); }
 };
 
 struct kfec_tx {
@@ -502,7 +542,7 @@ int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram,
     const size_t red_rows = std::min(G, worker_flush_max()) * R1 * (16 + round16(max_datagram + KFEC_FEC_CONTAINER_HEADER));
     // (BAR mode stages at whole write-combining lines: one group's worth more, so that partial groups of small
     //  datagrams still fit beside a full queue as with 4-byte staging)
-    if (q->own.init() || q->arena.init(q->device, (GK + (bar ? K : 0)) * q->slot, bar, red_rows + 64) || q->h_pack.ensure(meta) || q->h_res.ensure(res) ||
+    if (q->own.init() || q->arena.init(q->device, (GK + (bar ? K : 0)) * q->slot, bar, G, red_rows + 64) || q->h_pack.ensure(meta) || q->h_res.ensure(res) ||
         q->d_meta.ensure(meta) || q->d_res.ensure(res) || q->d_par.ensure(G * R1 * pitch) || q->d_align.ensure(G * 2)) {
         delete q;
         return KFEC_ENOMEM;
@@ -698,6 +738,7 @@ int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, v
 {
     const size_t n = q->n, nd = q->dpk.size(), K = q->K, R = q->R;
     if (!q->arena.bar || n > worker_flush_max() || (n && R == 0)) return 1;
+    q->trace.start();
     const size_t B = q->mtu + KFEC_FEC_CONTAINER_HEADER, opitch = 16 + round16(B);
     const size_t red_base = (q->used + 63) & ~size_t(63), nr = n * R;
     if (red_base + nr * opitch > q->arena.cap + q->arena.reserve) return 1;
@@ -759,9 +800,14 @@ int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, v
     if (n) {
         for (size_t i = 0; i < n * K; ++i) q->wdesc[i] = kfec::batch_desc(q->off[i], q->len[i], false);
         b.desc = q->wdesc.data();
+        q->trace.mark();
         if (st.fail()) return KFEC_EHIP;
         const int rc = kfec::worker_batch(q->device, b);
         if (rc) return rc;  // (1: the worker is off or gone -> the launch path)
+        q->trace.mark();
+    } else {
+        q->trace.mark();
+        q->trace.mark();
     }
     uint8_t *hs = q->h_sealed.as<uint8_t>();
     uint32_t *s_len = reinterpret_cast<uint32_t *>(hs + sO);
@@ -771,7 +817,9 @@ int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, v
                        reinterpret_cast<const uint32_t *>(ds + dL), reinterpret_cast<const uint16_t *>(ds + dI), hs, spitch,
                        s_len, stream);
     if (rc) return rc;
+    q->trace.mark();
     if (st.fail() || hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) return KFEC_EHIP;
+    q->trace.mark();
     auto red = [&](size_t g) {
         for (size_t r = 0; r < R; ++r) {
             const size_t i = nd + g * R + r;
@@ -783,6 +831,8 @@ int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, v
         if (s_len[i] && cb) cb(user, d.tag, d.sn, d.sub, hs + i * spitch, s_len[i]);
     };
     emit(q, n, data, red);
+    q->trace.mark();
+    q->trace.done();
     q->iv_ctr = iv_ctr;
     q->last_n = n;
     q->n = 0;
@@ -1120,7 +1170,7 @@ int kfec_rxq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_shard, kf
         delete q;
         return KFEC_EHIP;
     }
-    if (q->own.init() || q->arena.init(q->device, (GN + (bar ? q->N : 0)) * q->slot, bar) || q->h_pack.ensure(meta) || q->h_res.ensure(res) ||
+    if (q->own.init() || q->arena.init(q->device, (GN + (bar ? q->N : 0)) * q->slot, bar, G) || q->h_pack.ensure(meta) || q->h_res.ensure(res) ||
         q->d_meta.ensure(meta) || q->d_res.ensure(res) || q->d_align.ensure(G * 2) || q->d_st.ensure(G) ||
         q->d_ws.ensure(kfec_decode_workspace_size(ctx, G))) {
         delete q;

@@ -992,7 +992,14 @@ DevWorkers *get_dev(int dev)
             break;
         }
         std::memset(p, 0, kOffShares);
-        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) {
+        // The worker's stream gets the greatest priority: HIP maps streams onto a few hardware queues per priority
+        // (GPU_MAX_HW_QUEUES, 4 by default) and a stream sharing the resident worker's in-order queue would wait
+        // behind the worker kernel for up to its lease (measured: a queue's seal launch, 2.1 ms per small flush).
+        // The library's and the caller's other streams are normal priority, so none lands on a worker's queue.
+        int prio_lo = 0, prio_hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = prio_lo = 0;
+        if (hipStreamCreateWithPriority(&s.stream, hipStreamNonBlocking, prio_hi) != hipSuccess &&
+            hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) {
             (void)hipHostFree(p);
             (void)hipFree(q);
             break;
