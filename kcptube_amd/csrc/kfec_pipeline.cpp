@@ -1476,7 +1476,11 @@ struct kfec_opener {
     size_t max_packets = 0, max_packet = 0, pitch = 0;
     size_t n = 0, used = 0;
     // h_arena: the staged packets (4-byte offsets); h_desc: off u64 [n], len u32 [n] (one copy up);
-    // h_out: [n][pitch] plaintext, then out_len u32 [n], then ok u8 [n] (one copy down)
+    // h_out: [n][pitch] plaintext, then out_len u32 [n], then ok u8 [n] (one copy down).
+    // bar (large-BAR device, at most kOpenerBarMax packets per flush): each packet is written straight into
+    // d_arena through the BAR when it is added (no host copy), the descriptors likewise at the flush, and the open
+    // kernel writes its rows straight into h_out: a flush is one launch and one synchronisation
+    bool bar = false;
     Pinned h_arena, h_desc, h_out;
     Device d_arena, d_desc, d_out;
     std::vector<uint64_t> tags;
@@ -1503,14 +1507,17 @@ int kfec_opener_create(int mode, const kfec_aead *aead, size_t max_packets, size
     o->pitch = round4(max_packet);
     const size_t arena = max_packets * round4(max_packet), desc = max_packets * 12,
                  res = max_packets * (o->pitch + 5);
+    constexpr size_t kOpenerBarMax = 65536;
+    o->bar = env_flag("KFEC_QUEUE_BAR", true) && max_packets <= kOpenerBarMax && kfec::bar_writable(dev);
+    o->d_arena.uncached = o->d_desc.uncached = o->bar;
     try {
         o->tags.resize(max_packets);
     } catch (...) {
         delete o;
         return KFEC_ENOMEM;
     }
-    if (o->own.init() || o->h_arena.ensure(arena) || o->h_desc.ensure(desc) || o->h_out.ensure(res) ||
-        o->d_arena.ensure(arena) || o->d_desc.ensure(desc) || o->d_out.ensure(res)) {
+    if (o->own.init() || (!o->bar && o->h_arena.ensure(arena)) || o->h_desc.ensure(desc) || o->h_out.ensure(res) ||
+        o->d_arena.ensure(arena) || o->d_desc.ensure(desc) || (!o->bar && o->d_out.ensure(res))) {
         delete o;
         return KFEC_ENOMEM;
     }
@@ -1532,7 +1539,10 @@ int kfec_opener_add(kfec_opener *o, const uint8_t *pkt, size_t len, uint64_t tag
     if (!o || (len && !pkt) || len > o->max_packet) return KFEC_EINVAL;
     if (o->n == o->max_packets) return KFEC_ENOMEM;
     const size_t i = o->n++;
-    if (len) std::memcpy(o->h_arena.as<uint8_t>() + o->used, pkt, len);
+    if (len) {
+        if (o->bar) kfec::copy_to_bar(o->d_arena.as<uint8_t>() + o->used, pkt, len);
+        else std::memcpy(o->h_arena.as<uint8_t>() + o->used, pkt, len);
+    }
     reinterpret_cast<uint64_t *>(o->h_desc.p)[i] = o->used;
     o->tags[i] = tag;
     // lengths follow the offsets once the batch size is known (kfec_opener_flush packs them)
@@ -1553,15 +1563,21 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
     // retried: its first n offsets and first n lengths go up as two copies into [off n*8][len n*4]
     const uint8_t *hd = o->h_desc.as<uint8_t>();
     uint8_t *dd = o->d_desc.as<uint8_t>();
-    uint8_t *dr = o->d_out.as<uint8_t>();
+    // BAR mode: the kernel's rows, lengths and flags land in h_out directly
+    uint8_t *dr = o->bar ? o->h_out.as<uint8_t>() : o->d_out.as<uint8_t>();
     const size_t L = n * o->pitch;
     uint32_t *out_len = reinterpret_cast<uint32_t *>(dr + L);
     uint8_t *ok = dr + L + n * 4;
     const size_t arena = std::max<size_t>(o->used, 4);
-    if (hipMemcpyAsync(o->d_arena.p, o->h_arena.p, arena, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(dd, hd, n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(dd + n * 8, hd + o->max_packets * 8, n * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+    if (o->bar) {
+        kfec::copy_to_bar(dd, hd, n * 8);
+        kfec::copy_to_bar(dd + n * 8, hd + o->max_packets * 8, n * 4);
+        kfec::bar_fence();  // the packets (written at add) and the descriptors before the launch
+    } else if (hipMemcpyAsync(o->d_arena.p, o->h_arena.p, arena, hipMemcpyHostToDevice, s) != hipSuccess ||
+               hipMemcpyAsync(dd, hd, n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+               hipMemcpyAsync(dd + n * 8, hd + o->max_packets * 8, n * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
         return KFEC_EHIP;
+    }
     const uint64_t *d_off = reinterpret_cast<const uint64_t *>(dd);
     const uint32_t *d_len = reinterpret_cast<const uint32_t *>(dd + n * 8);
     const int rc = o->aead ? kfec_aead_open_batch(o->aead, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok,
@@ -1569,7 +1585,7 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
                            : kfec_open_batch(o->mode, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok,
                                              stream);
     if (rc) return rc;
-    if (hipMemcpyAsync(o->h_out.p, dr, L + n * 5, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if ((!o->bar && hipMemcpyAsync(o->h_out.p, dr, L + n * 5, hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipStreamSynchronize(s) != hipSuccess)
         return KFEC_EHIP;
     const uint8_t *ho = o->h_out.as<uint8_t>();
