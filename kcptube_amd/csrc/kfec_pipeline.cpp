@@ -130,11 +130,22 @@ struct Trace {
         us[k++] += std::chrono::duration<double, std::micro>(now - t).count();
         t = now;
     }
-    void done() { n += on() ? 1 : 0; }
+    void done()  // (the queue's first flush -- first launches, cold worker -- is left out)
+    {
+        if (!on()) return;
+        if (!warm) {
+            warm = true;
+            for (double &u : us) u = 0;
+            return;
+        }
+        ++n;
+    }
+    bool warm = false;
     void print(const char *what) const
     {
         if (!on() || !n) return;
-        fprintf(stderr, "kfec %s: %llu small flushes, us each: prep %.2f worker %.2f launch %.2f sync %.2f emit %.2f\n",
+        fprintf(stderr, "kfec %s: %llu small flushes after the first, us each: prep %.2f worker %.2f launch %.2f sync %.2f "
+                        "emit %.2f\n",
                 what, (unsigned long long)n, us[0] / n, us[1] / n, us[2] / n, us[3] / n, us[4] / n);
     }
 };
@@ -201,6 +212,7 @@ struct Upload {
     hipStream_t cs = nullptr;
     hipEvent_t ev = nullptr;
     size_t issued = 0;
+    bool busy = false;  // copies were issued on cs since the last drain (a drain of an idle stream costs ~5 us)
     int init(int device)
     {
         if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess ||
@@ -212,6 +224,7 @@ struct Upload {
     void grow(const uint8_t *h, uint8_t *d, size_t used)
     {
         if (used - issued < kUploadChunk) return;
+        busy = true;
         if (hipMemcpyAsync(d + issued, h + issued, used - issued, hipMemcpyHostToDevice, cs) == hipSuccess)
             issued = used;  // on failure the bytes are simply copied again by finish()
     }
@@ -220,13 +233,20 @@ struct Upload {
     {
         if (issued == 0)  // nothing went up early (a small flush): one copy on s, no cross-stream event
             return (used == 0 || hipMemcpyAsync(d, h, used, hipMemcpyHostToDevice, s) == hipSuccess) ? KFEC_OK : KFEC_EHIP;
+        busy = true;
         if (used > issued && hipMemcpyAsync(d + issued, h + issued, used - issued, hipMemcpyHostToDevice, cs) != hipSuccess)
             return KFEC_EHIP;
         issued = 0;  // (a retried flush uploads everything again on s)
         if (hipEventRecord(ev, cs) != hipSuccess || hipStreamWaitEvent(s, ev, 0) != hipSuccess) return KFEC_EHIP;
         return KFEC_OK;
     }
-    int drain() { return (cs && hipStreamSynchronize(cs) != hipSuccess) ? KFEC_EHIP : KFEC_OK; }
+    int drain()
+    {
+        if (!cs || !busy) return KFEC_OK;
+        if (hipStreamSynchronize(cs) != hipSuccess) return KFEC_EHIP;
+        busy = false;
+        return KFEC_OK;
+    }
     ~Upload()
     {
         (void)drain();
@@ -525,6 +545,9 @@ int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram,
     const size_t meta = round8(GK * 10) + G * 8, res = G * R1 * (pkt_pitch + 2);
     q->d_meta.uncached = bar;
     q->h_wout.flags = hipHostMallocCoherent;
+    // the sealed small flush's seal kernel writes its rows straight into h_sealed: fine-grained (coherent) memory
+    // takes those stores through to the host as they are issued, instead of an L2 write-back at the kernel's end
+    if (bar && env_flag("KFEC_QUEUE_COHERENT_OUT", true)) q->h_sealed.flags = hipHostMallocCoherent;
     try {
         q->off.resize(GK);
         q->len.resize(GK);
@@ -1510,6 +1533,7 @@ int kfec_opener_create(int mode, const kfec_aead *aead, size_t max_packets, size
     constexpr size_t kOpenerBarMax = 65536;
     o->bar = env_flag("KFEC_QUEUE_BAR", true) && max_packets <= kOpenerBarMax && kfec::bar_writable(dev);
     o->d_arena.uncached = o->d_desc.uncached = o->bar;
+    if (o->bar && env_flag("KFEC_QUEUE_COHERENT_OUT", true)) o->h_out.flags = hipHostMallocCoherent;  // (as h_sealed)
     try {
         o->tags.resize(max_packets);
     } catch (...) {
