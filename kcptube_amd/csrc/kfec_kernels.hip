@@ -92,6 +92,9 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #define KFEC_DEC_TTAB 1  // coefficient-form decode (R > 8): LDS entries point into one table of all 256 coefficients'
                          // perm tables (1) instead of holding each coefficient's expanded tables (0; A/B knob)
 #endif
+#ifndef KFEC_DEC_OFS16
+#define KFEC_DEC_OFS16 1  // T-table decode: each row's table offset read by its own 2-byte LDS read (A/B knob)
+#endif
 
 // ---------------------------------------------------------------------------------------------------
 // small device helpers
@@ -1027,10 +1030,18 @@ __device__ __forceinline__ void dec_build_t(uint8_t *s_T)
     }
 }
 
-// entries of shards [c0, c0 + nj) for group slots [0, ng): share pointer + MT u16 offsets into T
+// the LDS address of a pointer into the workgroup's shared memory
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t *p)
+{
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)p;
+}
+
+// entries of shards [c0, c0 + nj) for group slots [0, ng): share pointer + MT u16 offsets into T (KFEC_DEC_OFS16:
+// T's LDS address tbase added, so each is the address its table is read at)
 template <int MT>
 __device__ __forceinline__ void dec_expand(const MacArgs &a, uint8_t *s_ent, uint32_t gfirst, uint32_t ng, uint32_t c0,
-                                           uint32_t nj, uint32_t row0, const uint8_t *s_exp, const uint8_t *s_log)
+                                           uint32_t nj, uint32_t row0, const uint8_t *s_exp, const uint8_t *s_log,
+                                           uint32_t tbase)
 {
     static_assert(MT == 8, "entry: 8 offsets");
     const uint32_t items = ng * nj, K4 = (a.K + 3) & ~3u;
@@ -1087,7 +1098,7 @@ __device__ __forceinline__ void dec_expand(const MacArgs &a, uint8_t *s_ent, uin
             }
             uint32_t o[MT];
 #pragma unroll
-            for (int r = 0; r < MT; ++r) o[r] = (ok && row0 + r < m) ? cv[b][r] * 32u : 0u;  // T[0] = zero tables
+            for (int r = 0; r < MT; ++r) o[r] = tbase + ((ok && row0 + r < m) ? cv[b][r] * 32u : 0u);  // T[0] = zero tables
             uint32_t *ow = reinterpret_cast<uint32_t *>(ent + 8);
 #pragma unroll
             for (int r = 0; r < MT; r += 2) ow[r / 2] = o[r] | (o[r + 1] << 16);
@@ -1163,7 +1174,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
         const uint32_t nj = min(a.JC, K - c0);
         if (!enc_once) {
             if (!ttab || c0 > 0) __syncthreads();  // (ttab: nothing to protect before the first chunk)
-            if constexpr (ttab) dec_expand<MT>(a, s_E, gfirst, ng, c0, nj, row0, s_gexp, s_glog);
+            if constexpr (ttab) dec_expand<MT>(a, s_E, gfirst, ng, c0, nj, row0, s_gexp, s_glog, KFEC_DEC_OFS16 ? lds_addr(s_T) : 0u);
             else mac_expand<MT, DEC>(a, s_ent, gfirst, DEC ? ng : 1u, c0, nj, row0);
             __syncthreads();
         }
@@ -1177,28 +1188,51 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 return enc_base + (uint64_t)(c0 + jj) * a.pitch;
             }
         };
-        // ttab: the T offsets of a shard are read one shard ahead (ofs_lo / ofs_hi), so the table reads of the
-        // shard being multiplied depend on no LDS read still in flight
+        // ttab: the T offsets of a shard are read one shard ahead, so the table reads of the shard being
+        // multiplied depend on no LDS read still in flight.  KFEC_DEC_OFS16: one ds_read_u16 per row straight
+        // into the register that addresses its table (no extraction op per row and shard: 8 of ~370 VALU ops)
+        // instead of two 8-byte reads and a word-select add per row
         uint64_t ofs_lo = 0, ofs_hi = 0;
+        uint32_t ofs16[MT];
         auto read_ofs = [&](uint32_t jj) {
             if constexpr (ttab) {
-                const uint64_t *q = reinterpret_cast<const uint64_t *>(ent0 + min(jj, nj - 1) * ENT + 8);
-                ofs_lo = q[0];
-                ofs_hi = q[1];
+                if constexpr (KFEC_DEC_OFS16) {
+                    // (volatile: kept as separate 2-byte reads, not merged into one wide read and split by VALU)
+                    typedef const volatile __attribute__((address_space(3))) uint16_t lds_u16;
+                    const lds_u16 *q = (const lds_u16 *)(ent0 + min(jj, nj - 1) * ENT + 8);
+#pragma unroll
+                    for (int r = 0; r < MT; ++r) ofs16[r] = q[r];
+                } else {
+                    const uint64_t *q = reinterpret_cast<const uint64_t *>(ent0 + min(jj, nj - 1) * ENT + 8);
+                    ofs_lo = q[0];
+                    ofs_hi = q[1];
+                }
             }
         };
         auto mac = [&](const Gran<VEC> &cur, uint32_t jj) {
             uint32_t t[L::TBL_DW];
             if constexpr (ttab) {
                 const uint64_t lo = ofs_lo, hi = ofs_hi;
+                uint32_t oc[MT];
+#pragma unroll
+                for (int r = 0; r < MT; ++r) oc[r] = KFEC_DEC_OFS16 ? ofs16[r] : 0u;
                 read_ofs(jj + 1);
 #pragma unroll
                 for (int r = 0; r < MT; ++r) {
-                    const uint32_t o = (uint32_t)((r < 4 ? lo : hi) >> (16 * (r & 3))) & 0xFFFFu;
-                    const uint8_t *te = s_T + o;
-                    const uint4 q = *reinterpret_cast<const uint4 *>(te);
-                    t[5 * r] = q.x; t[5 * r + 1] = q.y; t[5 * r + 2] = q.z; t[5 * r + 3] = q.w;
-                    t[5 * r + 4] = *reinterpret_cast<const uint32_t *>(te + 16);
+                    const uint32_t o = KFEC_DEC_OFS16 ? oc[r] : (uint32_t)((r < 4 ? lo : hi) >> (16 * (r & 3))) & 0xFFFFu;
+                    if constexpr (KFEC_DEC_OFS16) {  // o: the table's LDS address (dec_expand added T's base)
+                        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+                        typedef const __attribute__((address_space(3))) v4u lds_u4;
+                        typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+                        const v4u q = *(const lds_u4 *)(uintptr_t)o;
+                        t[5 * r] = q.x; t[5 * r + 1] = q.y; t[5 * r + 2] = q.z; t[5 * r + 3] = q.w;
+                        t[5 * r + 4] = *(const lds_u32 *)(uintptr_t)(o + 16);
+                    } else {
+                        const uint8_t *te = s_T + o;
+                        const uint4 q = *reinterpret_cast<const uint4 *>(te);
+                        t[5 * r] = q.x; t[5 * r + 1] = q.y; t[5 * r + 2] = q.z; t[5 * r + 3] = q.w;
+                        t[5 * r + 4] = *reinterpret_cast<const uint32_t *>(te + 16);
+                    }
                 }
             } else {
                 const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + jj * ENT + 16);
