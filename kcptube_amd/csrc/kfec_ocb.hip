@@ -37,6 +37,8 @@ struct OcbKey {
     uint32_t te[4][256];
     uint32_t td[4][256];
     uint32_t isb[256];
+    uint4 rkr[15];   // rk / dk with every word rotated by 16 (the per-packet kernel's scalar round-key loads)
+    uint4 dkr[15];
 };
 
 __device__ __forceinline__ uint32_t gmul8(uint32_t a, uint32_t b)
@@ -119,6 +121,11 @@ __global__ void ocb_key_kernel(const uint32_t *key, OcbKey *k)
             for (int i = 0; i < 16; ++i) b[i] = m[i];
         }
         k->dk[r] = bytes_to_u4(b);
+        auto r16 = [](uint4 v) {
+            return make_uint4(v.x << 16 | v.x >> 16, v.y << 16 | v.y >> 16, v.z << 16 | v.z >> 16, v.w << 16 | v.w >> 16);
+        };
+        k->rkr[r] = r16(k->rk[r]);
+        k->dkr[r] = r16(k->dk[r]);
     }
     uint8_t z[16] = {}, ls[16], t[16];
     aes256_encrypt(w, z, ls);  // L_*
@@ -180,6 +187,9 @@ __global__ void ocb_iv_kernel(const uint32_t *key, uint4 *off0)
 #endif
 #ifndef KFEC_OCB_ILP
 #define KFEC_OCB_ILP 2  // full blocks per lane through the AES rounds together (1 or 2; A/B knob)
+#endif
+#ifndef KFEC_OCB_KSGPR
+#define KFEC_OCB_KSGPR 1  // the two-block rounds' keys by scalar loads, not LDS broadcast reads (A/B knob)
 #endif
 constexpr int kRow = 8;
 constexpr int kOcbBlock = 512;
@@ -378,7 +388,16 @@ __device__ __forceinline__ uint4 aes_dec(const OcbLds<true> &t, uint32_t c4, uin
 
 // two blocks through the rounds together (KFEC_OCB_ILP 2): twice the independent table reads in flight per
 // wave, for the latency the 4 waves per SIMD that the tables' LDS allows do not hide
-__device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, uint32_t c4, uint4 &x, uint4 &y)
+// round key r of a uniform table in global memory, by scalar loads (the address space of constant data)
+__device__ __forceinline__ uint4 key_at(const uint4 *tab, int r)
+{
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(4))) v4u cu4;
+    const v4u v = ((const cu4 *)tab)[r];
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, const OcbKey *key, uint32_t c4, uint4 &x, uint4 &y)
 {
     uint32_t s0 = x.x ^ t.rk[0].x, s1 = x.y ^ t.rk[0].y, s2 = x.z ^ t.rk[0].z, s3 = x.w ^ t.rk[0].w;
     uint32_t u0 = y.x ^ t.rk[0].x, u1 = y.y ^ t.rk[0].y, u2 = y.z ^ t.rk[0].z, u3 = y.w ^ t.rk[0].w;
@@ -388,7 +407,7 @@ __device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, uint32_t c4, ui
     auto round = [&](int r, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t b0, uint32_t b1,
                      uint32_t b2, uint32_t b3, uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3, uint32_t &e0,
                      uint32_t &e1, uint32_t &e2, uint32_t &e3) {
-        const uint4 k = t.rkr[r];
+        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->rkr, r) : t.rkr[r];
         o0 = tcol(t.te, c4, a0, a1, a2, a3, k.x);
         e0 = tcol(t.te, c4, b0, b1, b2, b3, k.x);
         o1 = tcol(t.te, c4, a1, a2, a3, a0, k.y);
@@ -410,7 +429,7 @@ __device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, uint32_t c4, ui
 #else
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
-        const uint4 k = t.rkr[r];
+        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->rkr, r) : t.rkr[r];
         const uint32_t t0 = tcol(t.te, c4, s0, s1, s2, s3, k.x);
         const uint32_t v0 = tcol(t.te, c4, u0, u1, u2, u3, k.x);
         const uint32_t t1 = tcol(t.te, c4, s1, s2, s3, s0, k.y);
@@ -432,7 +451,7 @@ __device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, uint32_t c4, ui
     y = make_uint4(last(u0, u1, u2, u3) ^ k.x, last(u1, u2, u3, u0) ^ k.y, last(u2, u3, u0, u1) ^ k.z, last(u3, u0, u1, u2) ^ k.w);
 }
 
-__device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, uint32_t c4, uint4 &x, uint4 &y)
+__device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, const OcbKey *key, uint32_t c4, uint4 &x, uint4 &y)
 {
     uint32_t s0 = x.x ^ t.dk[0].x, s1 = x.y ^ t.dk[0].y, s2 = x.z ^ t.dk[0].z, s3 = x.w ^ t.dk[0].w;
     uint32_t u0 = y.x ^ t.dk[0].x, u1 = y.y ^ t.dk[0].y, u2 = y.z ^ t.dk[0].z, u3 = y.w ^ t.dk[0].w;
@@ -440,7 +459,7 @@ __device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, uint32_t c4, uin
     auto round = [&](int r, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t b0, uint32_t b1,
                      uint32_t b2, uint32_t b3, uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3, uint32_t &e0,
                      uint32_t &e1, uint32_t &e2, uint32_t &e3) {
-        const uint4 k = t.dkr[r];
+        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->dkr, r) : t.dkr[r];
         o0 = tcol(t.td, c4, a0, a3, a2, a1, k.x);
         e0 = tcol(t.td, c4, b0, b3, b2, b1, k.x);
         o1 = tcol(t.td, c4, a1, a0, a3, a2, k.y);
@@ -462,7 +481,7 @@ __device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, uint32_t c4, uin
 #else
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
-        const uint4 k = t.dkr[r];
+        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->dkr, r) : t.dkr[r];
         const uint32_t t0 = tcol(t.td, c4, s0, s3, s2, s1, k.x);
         const uint32_t v0 = tcol(t.td, c4, u0, u3, u2, u1, k.x);
         const uint32_t t1 = tcol(t.td, c4, s1, s0, s3, s2, k.y);
@@ -581,8 +600,8 @@ __global__ void __launch_bounds__(kOcbBlock, 4) ocb_kernel(OcbArgs a)  // (4 wav
                 const uint4 ib = load16(a.src, a.src_dw, off + 16 * (j - 1));
                 const uint4 oa = ocb_offset(s, o0, i), ob = ocb_offset(s, o0, j);
                 uint4 xa = u4_xor(ia, oa), xb = u4_xor(ib, ob);
-                if constexpr (OPEN) aes_dec2(s, c, xa, xb);
-                else aes_enc2(s, c, xa, xb);
+                if constexpr (OPEN) aes_dec2(s, a.key, c, xa, xb);
+                else aes_enc2(s, a.key, c, xa, xb);
                 xa = u4_xor(xa, oa);
                 xb = u4_xor(xb, ob);
                 if constexpr (OPEN) {
