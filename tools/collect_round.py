@@ -16,7 +16,9 @@ for name in ("bench_203.json", "bench_103dec.json", "bench_20055.json", "bench_2
              "box.txt"):
     src = os.path.join(rnd, name)
     if os.path.exists(src):
-        shutil.copy(src, os.path.join(prof, f"{tag}_{name.replace('.log', '.txt')}"))
+        # (the round pass's latency line goes beside the curated <tag>_latency.json, never over it)
+        dst = name.replace('.log', '.txt').replace("latency.json", "latency_roundpass.json")
+        shutil.copy(src, os.path.join(prof, f"{tag}_{dst}"))
 for cfg, groups, ptag in (("20:3", 1 << 20, "203"), ("10:3dec", 1 << 20, "103dec"), ("200:55", 1 << 18, "20055"),
                           ("20:3loss1", 1 << 20, "203loss1")):
     d = os.path.join(go, f"prof_{tag}_{ptag}")
