@@ -92,6 +92,9 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #define KFEC_DEC_TTAB 1  // coefficient-form decode (R > 8): LDS entries point into one table of all 256 coefficients'
                          // perm tables (1) instead of holding each coefficient's expanded tables (0; A/B knob)
 #endif
+#ifndef KFEC_DEC_EXPAND2
+#define KFEC_DEC_EXPAND2 1  // factored-record entries by dec_expand_fac (0: the flat-index dec_expand; A/B knob)
+#endif
 #ifndef KFEC_DEC_OFS16
 #define KFEC_DEC_OFS16 1  // T-table decode: each row's table offset read by its own 2-byte LDS read (A/B knob)
 #endif
@@ -944,6 +947,9 @@ struct MacLayout {
 // one per 26-shard chunk, and no per-entry table construction.
 constexpr int kDecEntry = 24;
 constexpr uint32_t kTBytes = 256 * 32;
+// after T (factored records): the GF exp (512) / log (256) tables, then the T-address table of dec_expand_fac
+// (768 u16: tbase + 32 exp(e mod 255) for every exponent e the coefficient form produces, [2, 764])
+constexpr uint32_t kDecGfBytes = 768 + 768 * 2;
 
 // Workgroup b -> (column chunk, row tile).  With R > MT the tiles of one column chunk are numbered
 // b, b+8, b+16, ...: the dispatcher deals workgroups round-robin over the 8 XCDs, so those run back to back
@@ -1106,6 +1112,65 @@ __device__ __forceinline__ void dec_expand(const MacArgs &a, uint8_t *s_ent, uin
     }
 }
 
+// dec_expand for factored records (KFEC_DEC_EXPAND2): one column per thread (nj <= K < 256 = the workgroup),
+// groups in batches of four whose two per-column bytes (src, lden) are loaded together; a group's header and the
+// tile's 8 lnum / xm bytes are uniform (scalar loads), and each coefficient's T address is one lookup of its
+// exponent in s_taddr -- no division of the flat entry index, no per-entry header loads, no exponent fold.
+// staged_sync: the first chunk's barrier for the tables the workgroup staged (after the loads are issued).
+template <int MT>
+__device__ __forceinline__ void dec_expand_fac(const MacArgs &a, uint8_t *s_ent, uint32_t gfirst, uint32_t ng, uint32_t c0,
+                                               uint32_t nj, uint32_t row0, const uint8_t *s_exp, const uint8_t *s_log,
+                                               const uint16_t *s_taddr, uint32_t tbase, bool staged_sync)
+{
+    static_assert(MT == 8, "entry: 8 offsets");
+    typedef const __attribute__((address_space(4))) uint32_t cu32;
+    const uint32_t K = a.K, K4 = (K + 3) & ~3u, L0 = fac_lnum_off(K), R8 = fac_r8(a.R);
+    const bool has = threadIdx.x < nj;
+    const uint32_t jj = has ? threadIdx.x : nj - 1, j = c0 + jj;
+    constexpr uint32_t GB = 4;
+    for (uint32_t gs0 = 0; gs0 < ng; gs0 += GB) {  // (uniform)
+        uint32_t sv[GB], lv[GB];
+#pragma unroll
+        for (uint32_t b = 0; b < GB; ++b) {
+            const uint8_t *rec = a.rec + (uint64_t)(gfirst + min(gs0 + b, ng - 1)) * a.rec_stride;
+            sv[b] = rec[4 + j];
+            lv[b] = rec[4 + K4 + j];
+        }
+        if (gs0 == 0 && staged_sync) __syncthreads();
+#pragma unroll
+        for (uint32_t b = 0; b < GB; ++b) {
+            const uint32_t gs = gs0 + b;
+            if (gs >= ng) break;
+            const uint64_t g = __builtin_amdgcn_readfirstlane(gfirst + gs);  // (uniform: the record by scalar loads)
+            const cu32 *rq = (const cu32 *)(a.rec + g * a.rec_stride);
+            const uint32_t hd = rq[0];  // status | m << 8
+            const uint32_t ln0 = rq[(L0 + row0) / 4], ln1 = rq[(L0 + row0) / 4 + 1];
+            const uint32_t xm0 = rq[(L0 + R8 + row0) / 4], xm1 = rq[(L0 + R8 + row0) / 4 + 1];
+            const uint32_t m = (hd >> 8) & 0xFFu;
+            const uint32_t nrow = ((hd & 0xFFu) == 0 && m > row0) ? min(m - row0, (uint32_t)MT) : 0u;
+            const uint32_t src = sv[b];
+            const uint32_t xs = src ? (uint32_t)s_exp[src] : 0u;  // the point of the column's share (x_0 = 0)
+            const uint32_t base = 510u - lv[b];
+            uint32_t o[MT];
+#pragma unroll
+            for (int r = 0; r < MT; ++r) {
+                // coef = exp(lnum_u - log(xm_u ^ xs_j) - lden_j); rows past the group's m take T[0] (zero tables)
+                const uint32_t lnr = ((r < 4 ? ln0 : ln1) >> (8 * (r & 3))) & 0xFFu;
+                const uint32_t xmr = ((r < 4 ? xm0 : xm1) >> (8 * (r & 3))) & 0xFFu;
+                o[r] = (uint32_t)r < nrow ? (uint32_t)s_taddr[lnr + base - s_log[xmr ^ xs]] : tbase;
+            }
+            if (has) {
+                const uint8_t *p = (src < K) ? a.data + (g * K + src) * a.pitch : a.parity + (g * a.R + (src - K)) * a.pitch;
+                uint8_t *ent = s_ent + (gs * a.JC + jj) * kDecEntry;
+                *reinterpret_cast<const uint8_t **>(ent) = p;
+                uint32_t *ow = reinterpret_cast<uint32_t *>(ent + 8);
+#pragma unroll
+                for (int r = 0; r < MT; r += 2) ow[r / 2] = o[r] | (o[r + 1] << 16);
+            }
+        }
+    }
+}
+
 // One lane = one (group, V-byte column) item; consecutive lanes take consecutive columns and wrap into the
 // next group, so a wave-instruction reads 2 KiB of one shard row (V = 32).  One workgroup per 256 items
 // (non-persistent grid: the dispatcher refills each CU as workgroups retire).  Per lane: K loads of V bytes
@@ -1132,8 +1197,9 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     constexpr bool ttab = DEC && KFEC_DEC_TTAB && MT == 8;
     uint8_t *s_T = s_ent;
     // ttab: T, then (factored records) the GF exp / log tables, then the entries
-    constexpr uint32_t kGfBytes = ttab ? 768u : 0u;
+    constexpr uint32_t kGfBytes = ttab ? kDecGfBytes : 0u;
     uint8_t *s_gexp = s_ent + kTBytes, *s_glog = s_gexp + 512;
+    uint16_t *s_taddr = reinterpret_cast<uint16_t *>(s_gexp + 768);
     uint8_t *s_E = ttab ? s_ent + kTBytes + kGfBytes : s_ent;  // entries (after T)
     if (enc_once) {
         mac_expand<MT, false>(a, s_ent, 0, 1, 0, K, row0);
@@ -1141,7 +1207,13 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     }
     if constexpr (ttab) {
         dec_build_t(s_T);  // (ordered by the first chunk's barrier below)
-        if (a.factored) stage_gf(s_gexp, s_glog);
+        if (a.factored) {
+            stage_gf(s_gexp, s_glog);
+            if (KFEC_DEC_EXPAND2) {
+                const uint32_t tb = KFEC_DEC_OFS16 ? lds_addr(s_T) : 0u;
+                for (uint32_t i = threadIdx.x; i < 768; i += blockDim.x) s_taddr[i] = (uint16_t)(tb + 32u * c_gf.exp[i % 255u]);
+            }
+        }
     }
     const uint32_t item = base + threadIdx.x;
     const bool in = item < a.total;
@@ -1173,8 +1245,14 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     for (uint32_t c0 = 0; c0 < K; c0 += a.JC) {
         const uint32_t nj = min(a.JC, K - c0);
         if (!enc_once) {
-            if (!ttab || c0 > 0) __syncthreads();  // (ttab: nothing to protect before the first chunk)
-            if constexpr (ttab) dec_expand<MT>(a, s_E, gfirst, ng, c0, nj, row0, s_gexp, s_glog, KFEC_DEC_OFS16 ? lds_addr(s_T) : 0u);
+            // (ttab: T is read only after the expansion's barrier; the factored form's GF tables are read by the
+            // expansion itself -- dec_expand_fac waits for them after issuing its loads, dec_expand here)
+            if (!ttab || c0 > 0 || (a.factored && !KFEC_DEC_EXPAND2)) __syncthreads();
+            if constexpr (ttab) {
+                const uint32_t tb = KFEC_DEC_OFS16 ? lds_addr(s_T) : 0u;
+                if (KFEC_DEC_EXPAND2 && a.factored) dec_expand_fac<MT>(a, s_E, gfirst, ng, c0, nj, row0, s_gexp, s_glog, s_taddr, tb, c0 == 0);
+                else dec_expand<MT>(a, s_E, gfirst, ng, c0, nj, row0, s_gexp, s_glog, tb);
+            }
             else mac_expand<MT, DEC>(a, s_ent, gfirst, DEC ? ng : 1u, c0, nj, row0);
             __syncthreads();
         }
@@ -1757,7 +1835,7 @@ template <int VEC, int MT, bool DEC, int PDX = 0>
 static int run_mac(MacArgs a, hipStream_t s)
 {
     using L = MacLayout<MT>;
-    const size_t lds = (DEC && KFEC_DEC_TTAB && MT == 8) ? kTBytes + 768 + (size_t)a.gmax * a.JC * kDecEntry
+    const size_t lds = (DEC && KFEC_DEC_TTAB && MT == 8) ? kTBytes + kDecGfBytes + (size_t)a.gmax * a.JC * kDecEntry
                                                          : (size_t)a.gmax * a.JC * L::ENTRY;
     const uint32_t chunks = (a.total + kMacBlock - 1) / kMacBlock;
     const uint32_t nb = a.tiles > 1 ? ((chunks + 7) & ~7u) * a.tiles : chunks;
