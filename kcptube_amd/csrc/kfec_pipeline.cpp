@@ -680,6 +680,24 @@ int kfec_tx_send(kfec_tx *tx, const uint8_t *datagram, size_t len, uint32_t time
 
 namespace {
 
+// Emission reads rows the GPU has just written into pinned host memory -- in DRAM, in no CPU cache -- and a
+// callback typically copies each one out; requesting the rows a few packets ahead (KFEC_QUEUE_PREFETCH) keeps
+// those copies from paying a DRAM round trip every few lines: the send flushes and the opener (whose packets are
+// always read, by the socket send or kfec_rx_push).  Not the receive flush: most of a group's recovered rows are
+// often unused, and prefetching them cost a consumer that does not read them (tools/latency_bench) 17 -> 18 /
+// 95 -> 114 us per 16 / 256-group flush (profiles/r05_emit_prefetch_ab.txt).
+bool prefetch_on()
+{
+    static const bool v = env_flag("KFEC_QUEUE_PREFETCH", true);
+    return v;
+}
+constexpr size_t kPrefetchAhead = 4;  // rows
+inline void prefetch_bytes(const void *p, size_t n)
+{
+    const char *c = static_cast<const char *>(p);
+    for (size_t o = 0; o < n; o += 64) __builtin_prefetch(c + o, 0, 3);
+}
+
 // The flush's packets in emission order: the redundant ones in queue order or, with deferred data packets,
 // every packet in send order with a group's redundant packets right after the data packet completing it.
 template <typename Data, typename Red>
@@ -729,7 +747,10 @@ int txq_flush_worker(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *u
     const int rc = kfec::worker_batch(q->device, b);
     if (rc) return rc;  // (1: the worker is off or gone -> the launch path)
     uint8_t *wo = q->h_wout.as<uint8_t>();
+    const bool pf = prefetch_on();
+    if (pf) prefetch_bytes(wo, std::min(n, kPrefetchAhead) * R * opitch);
     auto red = [&](size_t g) {
+        if (pf && g + kPrefetchAhead < n) prefetch_bytes(wo + (g + kPrefetchAhead) * R * opitch, R * opitch);
         uint16_t mx = 0;  // align = max datagram length + 2 (data_operations.cpp:613-616)
         for (size_t i = 0; i < K; ++i) mx = std::max(mx, q->len[g * K + i]);
         const size_t align = (size_t)mx + KFEC_FEC_CONTAINER_HEADER;
@@ -843,13 +864,20 @@ int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, v
     q->trace.mark();
     if (st.fail() || hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) return KFEC_EHIP;
     q->trace.mark();
+    const bool pf = prefetch_on();
+    if (pf) {
+        prefetch_bytes(hs, std::min(nd, kPrefetchAhead) * spitch);
+        prefetch_bytes(hs + nd * spitch, std::min(n, (size_t)1) * R * spitch);
+    }
     auto red = [&](size_t g) {
+        if (pf && g + 1 < n) prefetch_bytes(hs + (nd + (g + 1) * R) * spitch, R * spitch);
         for (size_t r = 0; r < R; ++r) {
             const size_t i = nd + g * R + r;
             if (s_len[i] && cb) cb(user, q->tags[g], q->sn[g], (uint8_t)(K + r), hs + i * spitch, s_len[i]);
         }
     };
     auto data = [&](size_t i) {
+        if (pf && i + kPrefetchAhead < nd) prefetch_bytes(hs + (i + kPrefetchAhead) * spitch, spitch);
         const kfec_txq::DataPkt &d = q->dpk[i];
         if (s_len[i] && cb) cb(user, d.tag, d.sn, d.sub, hs + i * spitch, s_len[i]);
     };
@@ -977,7 +1005,15 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
     const uint16_t *pk_len = reinterpret_cast<const uint16_t *>(pk + P);
     const uint8_t *hs = q->h_sealed.as<uint8_t>();
     const uint32_t *s_len = reinterpret_cast<const uint32_t *>(hs + sO);
+    const bool pf = prefetch_on();
+    const size_t rpitch = seal ? spitch : pkt_pitch;  // redundant rows: hs + nd * spitch, or pk
+    const uint8_t *rbase = seal ? hs + nd * spitch : pk;
+    if (pf) {
+        if (seal) prefetch_bytes(hs, std::min(nd, kPrefetchAhead) * spitch);
+        prefetch_bytes(rbase, std::min(n, (size_t)1) * R * rpitch);
+    }
     auto red = [&](size_t g) {
+        if (pf && g + 1 < n) prefetch_bytes(rbase + (g + 1) * R * rpitch, R * rpitch);
         for (size_t r = 0; r < R; ++r) {
             const size_t i = g * R + r;
             const uint8_t *p = seal ? hs + (nd + i) * spitch : pk + i * pkt_pitch;
@@ -986,6 +1022,7 @@ int kfec_txq_flush(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, void *use
         }
     };
     auto data = [&](size_t i) {
+        if (pf && seal && i + kPrefetchAhead < nd) prefetch_bytes(hs + (i + kPrefetchAhead) * spitch, spitch);
         const kfec_txq::DataPkt &d = q->dpk[i];
         const uint8_t *p = seal ? hs + i * spitch : q->arena.host(d.off);
         const size_t plen = seal ? s_len[i] : d.len;
@@ -1475,7 +1512,7 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
     if (st.fail() || hipStreamSynchronize(s) != hipSuccess) return KFEC_EHIP;
     const uint8_t *hr = q->h_res.as<uint8_t>();
     const uint8_t *rec_idx = hr + D;
-    for (size_t g = 0; g < n && cb && R; ++g)
+    for (size_t g = 0; g < n && cb && R; ++g) {
         for (size_t t = 0; t < R; ++t) {
             const uint8_t idx = rec_idx[g * R + t];
             if (idx == 0xFF) continue;
@@ -1484,6 +1521,7 @@ int kfec_rxq_flush(kfec_rxq *q, kfec_datagram_cb cb, void *user, void *stream)
             if (dlen + KFEC_FEC_CONTAINER_HEADER > B) continue;     // inconsistent group (kfec_unframe_batch's 0xFFFF)
             cb(user, q->tags[g], q->sns[g], idx, shard + KFEC_FEC_CONTAINER_HEADER, dlen);
         }
+    }
     q->last_n = n;
     q->n = 0;
     return rx_compact(q);  // keep the shards of the groups still waiting for K shares
@@ -1615,7 +1653,12 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
     const uint8_t *ho = o->h_out.as<uint8_t>();
     const uint32_t *h_len = reinterpret_cast<const uint32_t *>(ho + L);
     const uint8_t *h_ok = ho + L + n * 4;
-    for (size_t i = 0; i < n && cb; ++i) cb(user, o->tags[i], ho + i * o->pitch, h_ok[i] ? h_len[i] : 0, h_ok[i] ? 1 : 0);
+    const bool pf = prefetch_on();
+    if (pf) prefetch_bytes(ho, std::min(n, kPrefetchAhead) * o->pitch);
+    for (size_t i = 0; i < n && cb; ++i) {
+        if (pf && i + kPrefetchAhead < n) prefetch_bytes(ho + (i + kPrefetchAhead) * o->pitch, o->pitch);
+        cb(user, o->tags[i], ho + i * o->pitch, h_ok[i] ? h_len[i] : 0, h_ok[i] ? 1 : 0);
+    }
     o->n = 0;
     o->used = 0;
     return KFEC_OK;
