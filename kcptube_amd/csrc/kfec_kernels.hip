@@ -57,6 +57,9 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #ifndef KFEC_SYN_EARLY
 #define KFEC_SYN_EARLY 1  // syn_kernel: C-table bytes loaded with the record header, expanded after the shard loop
 #endif
+#ifndef KFEC_SYN_XORONLY
+#define KFEC_SYN_XORONLY 0  // ablation (timing only, wrong results): the syndrome MACs as plain XORs, same loads / stores
+#endif
 #ifndef KFEC_SYN_TPRE
 #define KFEC_SYN_TPRE 1  // syn_loop: the next shard's E tables loaded into SGPRs one shard ahead (0: at use; A/B knob)
 #endif
@@ -1494,7 +1497,8 @@ __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][G
             const uint32_t s2 = (xv >> 6) & 0x03030303u;
 #pragma unroll
             for (int r = 0; r < RT; ++r)
-                if ((ROWS >> r) & 1u) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+                if ((ROWS >> r) & 1u)
+                    acc[r][w] = KFEC_SYN_XORONLY ? acc[r][w] ^ xv ^ t[5 * r] : perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
         }
     };
     // PD shards in flight, every load unconditional (see mac_kernel)
@@ -1540,7 +1544,8 @@ __device__ __forceinline__ void syn_final(const SynArgs &a, const uint32_t (&acc
                 for (int r = 0; r < RT; ++r) {
                     if (!((ROWS >> r) & 1u)) continue;  // (C[u][r] = 0 for a row no lane of the wave uses)
                     const uint32_t yv = acc[r][w];
-                    v = perm_mac(v, t + 5 * r, yv & 0x07070707u, (yv >> 3) & 0x07070707u, (yv >> 6) & 0x03030303u);
+                    v = KFEC_SYN_XORONLY ? v ^ yv ^ t[5 * r]
+                                         : perm_mac(v, t + 5 * r, yv & 0x07070707u, (yv >> 3) & 0x07070707u, (yv >> 6) & 0x03030303u);
                 }
                 o[w] = v;
             }
