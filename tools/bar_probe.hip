@@ -43,6 +43,20 @@ static void copy_store(void *dst, const void *src, size_t n)
     for (size_t i = 0; i < n / 32; ++i) _mm256_storeu_si256(d + i, _mm256_loadu_si256(s + i));
     _mm_sfence();
 }
+__attribute__((target("avx512f"))) static void copy_store512(void *dst, const void *src, size_t n)
+{
+    auto *d = static_cast<__m512i *>(dst);
+    auto *s = static_cast<const __m512i *>(src);
+    for (size_t i = 0; i < n / 64; ++i) _mm512_storeu_si512(d + i, _mm512_loadu_si512(s + i));
+    _mm_sfence();
+}
+__attribute__((target("avx512f"))) static void copy_stream512(void *dst, const void *src, size_t n)
+{
+    auto *d = static_cast<__m512i *>(dst);
+    auto *s = static_cast<const __m512i *>(src);
+    for (size_t i = 0; i < n / 64; ++i) _mm512_stream_si512(d + i, _mm512_loadu_si512(s + i));
+    _mm_sfence();
+}
 static void copy_movsb(void *dst, const void *src, size_t n)
 {
     asm volatile("rep movsb" : "+D"(dst), "+S"(src), "+c"(n) : : "memory");
@@ -56,8 +70,14 @@ static void time_variants(const char *name, void *p)
     for (size_t i = 0; i < n; ++i) src[i] = (uint8_t)(i * 5 + 1);
     struct V { const char *v; void (*f)(void *, const void *, size_t); };
     const V vs[] = {{"memcpy+sfence", [](void *d, const void *s, size_t k) { std::memcpy(d, s, k); _mm_sfence(); }},
-                    {"avx2 stream", copy_stream}, {"avx2 store", copy_store}, {"rep movsb", copy_movsb}};
+                    {"avx2 stream", copy_stream}, {"avx2 store", copy_store}, {"rep movsb", copy_movsb},
+                    {"avx512 store", copy_store512}, {"avx512 stream", copy_stream512}};
+    const bool avx512 = __builtin_cpu_supports("avx512f");
     for (const V &v : vs) {
+        if (!avx512 && std::strncmp(v.v, "avx512", 6) == 0) {
+            printf("%s: %s: no avx512f on this CPU\n", name, v.v);
+            continue;
+        }
         for (int i = 0; i < 50; ++i) v.f(p, src, n);
         const int reps = 4000;
         auto t0 = std::chrono::steady_clock::now();
