@@ -75,6 +75,29 @@ def test_sender_flush_paths_match_oracle(dev, oracle, path, K, N, mtu):
     assert [(t, p) for t, _, _, p in got] == exp  # queue order, byte for byte
 
 
+@pytest.mark.parametrize("K,N,mtu,groups,worker", [
+    (64, 72, 200, 31, True),    # K x R = 512: the matrix tables fill the worker's 16 KiB; 31 x 64 descriptors fit
+    (64, 72, 200, 32, False),   # one group more: the request (128 + 32 x 64 x 8 bytes) exceeds 16 KiB
+    (65, 73, 200, 4, False),    # K x R = 520: the tables do not fit
+    (20, 29, 100, 8, False),    # R = 9: more parity rows than a batch request carries
+    (100, 104, 64, 20, True),   # K > 64 (two present words), R = 4
+])
+def test_sender_worker_limits(dev, oracle, K, N, mtu, groups, worker):
+    """At and just past the worker's shape limits (kfec_worker.hip: kTabMax, kBatchReqMax, kBatchMaxR) a small
+    flush takes the worker exactly when the request fits, and either path gives the oracle's packets."""
+    from kcptube_amd.pipeline import TxQueue, set_queue_worker_max, worker_batches
+    set_queue_worker_max(64)
+    try:
+        q = TxQueue(_coder(K, N), max_groups=groups + 2, max_datagram=mtu)
+        exp, _ = _send_groups(oracle, q, K, N, mtu, groups=groups, seed=K + N + groups)
+        b0 = worker_batches()
+        got = q.flush(timestamp=4321)
+        assert (worker_batches() > b0) == worker
+        assert [(t, p) for t, _, _, p in got] == exp
+    finally:
+        set_queue_worker_max(-1)
+
+
 @pytest.mark.parametrize("K,N,mtu", [(20, 23, 1440), (10, 13, 1400), (6, 9, 300), (8, 16, 200), (1, 2, 7)])
 def test_receiver_flush_paths_match_oracle(dev, oracle, path, K, N, mtu):
     """A lossy, duplicated, reordered three-connection channel; small flushes at random points."""
@@ -153,6 +176,26 @@ def _fill_rx(oracle, rq, K, N, mtu, groups, seed):
             exp[i] += out if p[8] >= K else out[:-1]
         g += 1
     return rx, ref, exp
+
+
+@pytest.mark.parametrize("K,N,mtu,groups", [(64, 72, 200, 12), (100, 104, 64, 12), (20, 29, 100, 8), (65, 73, 200, 4)])
+def test_receiver_worker_limits(dev, oracle, K, N, mtu, groups):
+    """Receive flushes of shapes at and past the worker's limits (decode tables per workgroup, R > 8): whichever
+    path a flush takes, the recovered datagrams are the oracle's."""
+    from kcptube_amd.pipeline import RxQueue, set_queue_worker_max
+    set_queue_worker_max(64)
+    try:
+        rq = RxQueue(_coder(K, N), max_groups=groups + 2, max_shard=mtu + 2)
+        rx, ref, exp = _fill_rx(oracle, rq, K, N, mtu, groups=groups, seed=K * 3 + N)
+        got = rq.flush()
+        per_tag = [[], []]
+        for tag, sn, idx, d in got:
+            per_tag[tag].append(d)
+        for i in range(2):
+            assert sorted(per_tag[i]) == sorted(exp[i])
+        assert sum(len(x) for x in per_tag) == groups * min(3, N - K)
+    finally:
+        set_queue_worker_max(-1)
 
 
 @pytest.mark.parametrize("step", range(1, 9))
