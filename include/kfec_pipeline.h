@@ -33,10 +33,12 @@
  * bytes; otherwise finished 8 MiB stretches of the arena go H2D on the queue's own copy stream while the host
  * keeps filling it, so a flush waits only for the tail (KFEC_QUEUE_BAR=0: always the latter).
  * Flush paths: a flush of at most KFEC_QUEUE_WORKER_MAX groups (default 64) in BAR mode is one request to the
- * resident worker (kfec.h; no kernel launch, no stream synchronisation: ~10 us for one 20:3 group, ~16-22 us for
+ * resident worker (kfec.h; no kernel launch, no stream synchronisation: ~10 us for one 20:3 group, ~16-21 us for
  * 16); a sealed one is a worker request plus one seal launch; larger flushes run kernel launches on `stream`.
  * Both give the same bytes.  `stream` NULL: the queue's own non-blocking stream (HIP's null stream would also
- * wait for every other stream of the device, a resident worker's included).
+ * wait for every other stream of the device, a resident worker's included).  The callbacks of a send flush and
+ * of kfec_opener_flush get rows the device has just written to pinned memory; the flush requests each a few
+ * packets before its callback (KFEC_QUEUE_PREFETCH=0: not).
  * A flush that returns an error leaves the queue as it was -- queued groups, staged packets, the sealed iv
  * counter -- and can be retried.
  */
