@@ -75,6 +75,12 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #ifndef KFEC_PREP_PREFETCH
 #define KFEC_PREP_PREFETCH 1  // decode_prep_lagrange loads the next group's present bits one group ahead (A/B knob)
 #endif
+#ifndef KFEC_PREP_WAVE
+#define KFEC_PREP_WAVE 1  // decode_prep_lagrange: one wave per group, four groups per workgroup (0: the workgroup; A/B)
+#endif
+#ifndef KFEC_PREP_WAVE_MINW
+#define KFEC_PREP_WAVE_MINW 4  // the same for one wave per group (4: 128 VGPRs, 16 groups in flight per CU)
+#endif
 #ifndef KFEC_PREP_MINW
 #define KFEC_PREP_MINW 8  // decode_prep_lagrange: minimum waves per SIMD (8: 64 VGPRs, 12 spilled, 3% faster than uncapped)
 #endif
@@ -641,24 +647,38 @@ constexpr bool gf_exp_periodic()
 static_assert(make_gf_tables().log[0] % 255 == 0, "decode_prep_lagrange relies on log[0] == 255 (0 mod 255)");
 static_assert(gf_exp_periodic(), "decode_prep_lagrange indexes exp[] up to 509 without reduction");
 
-__global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagrange(PrepArgs a)
+// TEAM threads solve one group: the whole workgroup (256, barriers between the steps) or one wave (64:
+// four groups per workgroup at once, each wave with its own lists and no workgroup barrier inside the group loop --
+// a wave's LDS operations complete in order, the fences only keep the compiler from reordering them).
+template <int TEAM>
+__global__ void __launch_bounds__(kPrepThreads, TEAM == 64 ? KFEC_PREP_WAVE_MINW : KFEC_PREP_MINW) decode_prep_lagrange(PrepArgs a)
 {
+    static_assert(TEAM == kPrepThreads || TEAM == 64, "a team is the workgroup or one wave");
+    constexpr int NT = kPrepThreads / TEAM;  // teams (groups in flight) per workgroup
     __shared__ uint8_t s_exp[512], s_log[256];
     __shared__ uint16_t s_full[256];  // FULL_s mod 255
-    __shared__ uint8_t s_C[256];      // ids outside S, ascending
-    __shared__ uint8_t s_xC[256];     // their points
-    __shared__ uint8_t s_M[256];      // missing data ids, ascending
-    __shared__ uint8_t s_P[256];      // parity share used for missing rank t: the highest present ids, descending
-    __shared__ uint8_t s_src[256];    // source share of column j
-    __shared__ uint16_t s_lden[256];  // log den of the source of column j
-    __shared__ uint16_t s_lnum[256];  // log num_u without the (x_{M_u} ^ x_i) factor
-    __shared__ uint8_t s_xs[256];     // KFEC_PREP_COEF2: the point of column j's source
-    const int K = a.K, N = a.N, R = a.R, tid = threadIdx.x;
+    __shared__ uint8_t s_C_all[NT][256];      // ids outside S, ascending
+    __shared__ uint8_t s_xC_all[NT][256];     // their points
+    __shared__ uint8_t s_M_all[NT][256];      // missing data ids, ascending
+    __shared__ uint8_t s_P_all[NT][256];      // parity share used for missing rank t: the highest present ids, descending
+    __shared__ uint8_t s_src_all[NT][256];    // source share of column j
+    __shared__ uint16_t s_lden_all[NT][256];  // log den of the source of column j
+    __shared__ uint16_t s_lnum_all[NT][256];  // log num_u without the (x_{M_u} ^ x_i) factor
+    __shared__ uint8_t s_xs_all[NT][256];     // KFEC_PREP_COEF2: the point of column j's source
+    const int K = a.K, N = a.N, R = a.R;
+    const int team = threadIdx.x / TEAM, tid = threadIdx.x % TEAM;  // (tid: the thread's index in its team)
+    uint8_t *s_C = s_C_all[team], *s_xC = s_xC_all[team], *s_M = s_M_all[team], *s_P = s_P_all[team];
+    uint8_t *s_src = s_src_all[team], *s_xs = s_xs_all[team];
+    uint16_t *s_lden = s_lden_all[team], *s_lnum = s_lnum_all[team];
+    auto team_sync = [&]() {
+        if constexpr (TEAM == kPrepThreads) __syncthreads();
+        else __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    };
     const int K4 = (K + 3) & ~3, kd = K4 / 4;
     stage_gf(s_exp, s_log);
     __syncthreads();
     auto xpt = [&](int sid) -> uint32_t { return sid ? (uint32_t)s_exp[sid] : 0u; };  // s_exp[255] = 1
-    for (int sid = tid; sid < N; sid += kPrepThreads) {
+    for (int sid = threadIdx.x; sid < N; sid += kPrepThreads) {
         const uint32_t xs = xpt(sid);
         uint32_t acc = 0;
         for (int k = 0; k < N; ++k)
@@ -668,18 +688,19 @@ __global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagr
     __syncthreads();
 
     // KFEC_PREP_PREFETCH: the next group's present bits are loaded while this group is solved
+    const uint64_t g0 = (uint64_t)blockIdx.x * NT + team, gstride = (uint64_t)gridDim.x * NT;
     uint64_t pn[4] = {0, 0, 0, 0};
-    if (KFEC_PREP_PREFETCH && blockIdx.x < a.G) {
+    if (KFEC_PREP_PREFETCH && g0 < a.G) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pn[q] = a.present[(uint64_t)blockIdx.x * 4 + q];
+        for (int q = 0; q < 4; ++q) pn[q] = a.present[g0 * 4 + q];
     }
-    for (uint64_t g = blockIdx.x; g < a.G; g += gridDim.x) {
+    for (uint64_t g = g0; g < a.G; g += gstride) {
         uint64_t w[4], dm[4], pc[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) pc[q] = KFEC_PREP_PREFETCH ? pn[q] : a.present[g * 4 + q];
-        if (KFEC_PREP_PREFETCH && g + gridDim.x < a.G) {
+        if (KFEC_PREP_PREFETCH && g + gstride < a.G) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) pn[q] = a.present[(g + gridDim.x) * 4 + q];
+            for (int q = 0; q < 4; ++q) pn[q] = a.present[(g + gstride) * 4 + q];
         }
         int cnt = 0, m = 0;
 #pragma unroll
@@ -690,24 +711,24 @@ __global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagr
             m += __popcll(dm[q]);
         }
         uint8_t *rec = a.rec + g * a.rec_stride;
-        if (cnt < K) {  // uniform over the workgroup
+        if (cnt < K) {  // uniform over the team
             if (tid == 0) {
                 rec[0] = 1;
                 rec[1] = 0;
                 a.status[g] = 1;
             }
-            for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = 0xFF;
+            for (int t = tid; t < R; t += TEAM) a.out_idx[g * R + t] = 0xFF;
             continue;
         }
         // P_t = the present id with exactly t present ids above it (t < m; all parity since cnt >= K);
         // the lowest of them, P_{m-1}, bounds the used-parity set from below
-        for (int sid = tid; sid < N; sid += kPrepThreads) {
+        for (int sid = tid; sid < N; sid += TEAM) {
             if ((w[sid >> 6] >> (sid & 63)) & 1ull) {
                 const int above = cnt - 1 - rank_below(w, sid);
                 if (above < m) s_P[above] = (uint8_t)sid;
             }
         }
-        __syncthreads();
+        team_sync();
         const int thr = m > 0 ? (int)s_P[m - 1] : 256;
         uint64_t Cb[4];
 #pragma unroll
@@ -716,7 +737,7 @@ __global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagr
             const uint64_t S = (w[q] & bits_below(K, q)) | used_par;
             Cb[q] = ~S & bits_below(N, q);
         }
-        for (int sid = tid; sid < N; sid += kPrepThreads) {
+        for (int sid = tid; sid < N; sid += TEAM) {
             const int q = sid >> 6, b = sid & 63;
             if ((Cb[q] >> b) & 1ull) {
                 const int r = rank_below(Cb, sid);
@@ -725,12 +746,12 @@ __global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagr
             }
             if (sid < K && ((dm[q] >> b) & 1ull)) s_M[rank_below(dm, sid)] = (uint8_t)sid;
         }
-        __syncthreads();
+        team_sync();
 #if KFEC_PREP_FUSED
         // the K column denominators and the m numerators are one kind of sum, log FULL_s - sum_c log(x_s ^ x_c),
         // so they are one pass of K + m <= N <= 256 items (one per thread) instead of two loops that wave 0
         // ran back to back; a numerator's excluded term c = M_u has x_s ^ x_c = 0, and log[0] = 255 = 0 mod 255
-        for (int it = tid; it < K + m; it += kPrepThreads) {
+        for (int it = tid; it < K + m; it += TEAM) {
             int sid;
             if (it < K) {
                 const bool miss = (dm[it >> 6] >> (it & 63)) & 1ull;
@@ -749,7 +770,7 @@ __global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagr
             else s_lnum[it - K] = v;
         }
 #else
-        for (int j = tid; j < K; j += kPrepThreads) {
+        for (int j = tid; j < K; j += TEAM) {
             const bool miss = (dm[j >> 6] >> (j & 63)) & 1ull;
             const int i = miss ? (int)s_P[rank_below(dm, j)] : j;
             s_src[j] = (uint8_t)i;
@@ -758,7 +779,7 @@ __global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagr
             for (int c = 0; c < R; ++c) acc += s_log[xi ^ s_xC[c]];
             s_lden[j] = (uint16_t)((s_full[i] + 255u - acc % 255u) % 255u);
         }
-        for (int u = tid; u < m; u += kPrepThreads) {
+        for (int u = tid; u < m; u += TEAM) {
             const int mu = s_M[u];
             const uint32_t xm = xpt(mu);
             uint32_t acc = 0;
@@ -767,13 +788,13 @@ __global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagr
             s_lnum[u] = (uint16_t)((s_full[mu] + 255u - acc % 255u) % 255u);
         }
 #endif
-        __syncthreads();
+        team_sync();
         uint32_t *srcw = reinterpret_cast<uint32_t *>(rec + 4);
         if (a.factored) {
             // the factors only (see fac_record_stride): src and lden as dwords of 4 columns, lnum and xm per row
             const uint32_t L0 = fac_lnum_off((uint32_t)K), R8 = fac_r8((uint32_t)R);
             uint32_t *ldw = reinterpret_cast<uint32_t *>(rec + 4 + K4);
-            for (int d = tid; d < kd; d += kPrepThreads) {
+            for (int d = tid; d < kd; d += TEAM) {
                 uint32_t v = 0, l = 0;
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
@@ -784,29 +805,29 @@ __global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagr
                 srcw[d] = v;
                 ldw[d] = l;
             }
-            for (int u = tid; u < m; u += kPrepThreads) {
+            for (int u = tid; u < m; u += TEAM) {
                 rec[L0 + u] = (uint8_t)s_lnum[u];
                 rec[L0 + R8 + u] = (uint8_t)xpt(s_M[u]);
             }
-            for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
+            for (int t = tid; t < R; t += TEAM) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
             if (tid == 0) {
                 rec[0] = 0;
                 rec[1] = (uint8_t)m;
                 rec[2] = rec[3] = 0;
                 a.status[g] = 0;
             }
-            __syncthreads();  // the lists are rewritten for the next group
+            team_sync();  // the lists are rewritten for the next group
             continue;
         }
         uint32_t *coefw = reinterpret_cast<uint32_t *>(rec + 4 + K4);
-        for (int d = tid; d < kd; d += kPrepThreads) {
+        for (int d = tid; d < kd; d += TEAM) {
             uint32_t v = 0;
 #pragma unroll
             for (int b = 0; b < 4; ++b)
                 if (4 * d + b < K) v |= (uint32_t)s_src[4 * d + b] << (8 * b);
             srcw[d] = v;
         }
-        for (int e = tid; e < m * kd; e += kPrepThreads) {
+        for (int e = tid; e < m * kd; e += TEAM) {
             const int u = e / kd, d = e - u * kd;
             const uint32_t xm = xpt(s_M[u]);
             const int ln = s_lnum[u];
@@ -829,14 +850,14 @@ __global__ void __launch_bounds__(kPrepThreads, KFEC_PREP_MINW) decode_prep_lagr
             }
             coefw[u * kd + d] = v;
         }
-        for (int t = tid; t < R; t += kPrepThreads) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
+        for (int t = tid; t < R; t += TEAM) a.out_idx[g * R + t] = (t < m) ? s_M[t] : (uint8_t)0xFF;
         if (tid == 0) {
             rec[0] = 0;
             rec[1] = (uint8_t)m;
             rec[2] = rec[3] = 0;
             a.status[g] = 0;
         }
-        __syncthreads();  // the lists are rewritten for the next group
+        team_sync();  // the lists are rewritten for the next group
     }
 }
 
@@ -2028,12 +2049,14 @@ int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N,
         else if (mmax == 4) hipLaunchKernelGGL((decode_prep_perm<4>), dim3(blocks), dim3(kBlock), lds4, s, p);
         else hipLaunchKernelGGL((decode_prep_small<8>), dim3(blocks), dim3(kBlock), lds, s, p);
     } else {
+        constexpr int kTeam = KFEC_PREP_WAVE ? 64 : kPrepThreads;
+        const void *fn = reinterpret_cast<const void *>(&decode_prep_lagrange<kTeam>);
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)decode_prep_lagrange, kPrepThreads, 0) !=
-                hipSuccess || occ <= 0)
-            occ = 1;
-        const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>(G, (size_t)std::max(di.cus, 1) * occ));
-        hipLaunchKernelGGL(decode_prep_lagrange, dim3(blocks), dim3(kPrepThreads), 0, s, p);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kPrepThreads, 0) != hipSuccess || occ <= 0) occ = 1;
+        const size_t teams = kPrepThreads / kTeam;
+        const uint32_t blocks =
+            (uint32_t)std::max<size_t>(1, std::min<size_t>((G + teams - 1) / teams, (size_t)std::max(di.cus, 1) * occ));
+        hipLaunchKernelGGL((decode_prep_lagrange<kTeam>), dim3(blocks), dim3(kPrepThreads), 0, s, p);
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
