@@ -36,26 +36,49 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+# per-source compiler flags of the shipped library.  kfec_ocb.hip: LLVM's iterative ILP scheduler keeps more of a
+# round's table reads in flight (aes_ocb seal 8.31-8.33 -> 8.16 ms, profiles/r05_ocb_sched_ab.txt); applied to
+# that file only (the same flag crashes the compiler on kfec_kernels.hip)
+FILE_FLAGS: dict[str, list[str]] = {"kfec_ocb.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
+
+
+def _compile_link(out: str, common: list[str], file_flags: dict[str, list[str]], verbose: bool = False) -> None:
+    """Each source to an object (in parallel, so a source can carry flags of its own), then one link."""
+    import concurrent.futures
+    import tempfile
+    base = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"] + common
+    with tempfile.TemporaryDirectory(prefix="kfec_build_") as tmp:
+        def one(src: str) -> str:
+            obj = os.path.join(tmp, src + ".o")
+            cmd = base + file_flags.get(src, []) + ["-c", "-o", obj, os.path.join(CSRC, src)]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.check_call(cmd, cwd=CSRC)
+            return obj
+        jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "8"))))
+        with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
+            objs = list(ex.map(one, SOURCES))
+        subprocess.check_call([_hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out] + objs, cwd=CSRC)
+
+
 def build_lib(force: bool = False, verbose: bool = False) -> str:
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", h) for h in ("kfec.h", "kfec_frame.h", "kfec_pipeline.h", "kfec_aead.h")]
     if force or _stale(LIB, deps):
-        cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wno-unused-result", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
-        if verbose:
-            print(" ".join(cmd), file=sys.stderr)
-        subprocess.check_call(cmd, cwd=CSRC)
+        _compile_link(LIB + ".tmp", [], FILE_FLAGS, verbose)
         os.replace(LIB + ".tmp", LIB)
     return LIB
 
 
-def build_variant(name: str, defines: dict[str, int]) -> str:
-    """Timing/ablation variant of the library (tools/ab.py): kcptube_amd/variants/libkfec_<name>.so."""
+def build_variant(name: str, defines: dict[str, int], flags: dict[str, list[str]] | None = None) -> str:
+    """Timing/ablation variant of the library (tools/ab.py): kcptube_amd/variants/libkfec_<name>.so.
+    `flags` maps a source file to extra compiler flags (on top of the shipped library's)."""
     out_dir = os.path.join(PKG, "variants")
     os.makedirs(out_dir, exist_ok=True)
     out = os.path.join(out_dir, f"libkfec_{name}.so")
-    cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-           "-o", out] + [f"-D{k}={v}" for k, v in defines.items()] + [os.path.join(CSRC, s) for s in SOURCES]
-    subprocess.check_call(cmd, cwd=CSRC)
+    ff = {k: list(v) for k, v in FILE_FLAGS.items()}
+    for k, v in (flags or {}).items():
+        ff[k] = ff.get(k, []) + list(v)
+    _compile_link(out, [f"-D{k}={v}" for k, v in defines.items()], ff)
     return out
 
 
