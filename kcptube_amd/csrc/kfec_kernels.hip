@@ -39,6 +39,12 @@ static constexpr int kBlock = 256;
 static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened MAC kernel
 
 // build-time tuning knobs (tools/ab.py builds variants; the shipped library uses the defaults)
+#ifndef KFEC_MAC_BURST
+#define KFEC_MAC_BURST 2  // encode MAC (MT 3..4): 2 = tables, MACs, next loads as bursts; 1 = loads only; 0 = interleaved
+#endif
+#ifndef KFEC_MAC_PD
+#define KFEC_MAC_PD KFEC_PD  // the same for the MAC kernel's 32-byte shape with MT < 8
+#endif
 #ifndef KFEC_PD
 #define KFEC_PD 4  // granules per lane in the load pipeline of the 32-byte shape (PD - 1 in flight during a MAC)
 #endif
@@ -1207,7 +1213,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     // shards in flight per lane (~64 B per lane); PDX: the latency shape (a handful of groups, often read
     // straight from pinned host memory) keeps many more loads in flight so the PCIe round trips overlap
     // (MT = 8, the VALU-bound tall tiles: 2, to keep 3 waves per SIMD)
-    constexpr int PD = PDX ? PDX : (VEC >= 32 ? (MT >= 8 ? 2 : KFEC_PD) : 2 * KFEC_PD);
+    constexpr int PD = PDX ? PDX : (VEC >= 32 ? (MT >= 8 ? 2 : KFEC_MAC_PD) : 2 * KFEC_PD);
     constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
 
@@ -1362,12 +1368,50 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
         read_ofs(0);
         uint32_t jb = 0;
         for (; jb + PD <= nj; jb += PD) {
+            if constexpr (!DEC && MT >= 3 && MT <= 4 && VEC >= 32 && KFEC_MAC_BURST == 2) {
+                // every table of the PD granules first (one LDS burst), the PD MACs, then the next PD
+                // granules' loads as one burst: 129 VGPRs at MT = 3 (3 waves per SIMD, from 98 and 5); encode
+                // 20:3 2.2% and 8:4 4% faster, 10:3 within 1%, in an interleaved A/B (profiles/r05_enc_burst_ab.txt;
+                // 20:1 was 0.9% slower, so MT < 3 keeps the interleaved loop); 4 waves per SIMD (launch bounds)
+                // and the loads alone as a burst measured slower
+                uint32_t tt[PD][L::TBL_DW];
 #pragma unroll
-            for (int u = 0; u < PD; ++u) {
-                // consume, then refill the same registers: PD - 1 granules stay in flight during the MAC
-                // (loading first would need a fresh register set and a copy -- and a wait -- per iteration)
-                mac(x[u], jb + u);
-                x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
+                for (int u = 0; u < PD; ++u) {
+                    const uint4 *tv = reinterpret_cast<const uint4 *>(ent0 + (jb + u) * ENT + 16);
+#pragma unroll
+                    for (int i = 0; i < L::TBL_DW / 4; ++i) {
+                        const uint4 q = tv[i];
+                        tt[u][4 * i] = q.x; tt[u][4 * i + 1] = q.y; tt[u][4 * i + 2] = q.z; tt[u][4 * i + 3] = q.w;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < PD; ++u) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w) {
+                        const uint32_t xv = x[u].d[w];
+                        const uint32_t s0 = xv & 0x07070707u;
+                        const uint32_t s1 = (xv >> 3) & 0x07070707u;
+                        const uint32_t s2 = (xv >> 6) & 0x03030303u;
+#pragma unroll
+                        for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], tt[u] + 5 * r, s0, s1, s2);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
+            } else if constexpr (!DEC && KFEC_MAC_BURST == 1) {
+                // the PD granules' MACs, then the next PD granules' loads as one burst
+#pragma unroll
+                for (int u = 0; u < PD; ++u) mac(x[u], jb + u);
+#pragma unroll
+                for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
+            } else {
+#pragma unroll
+                for (int u = 0; u < PD; ++u) {
+                    // consume, then refill the same registers: PD - 1 granules stay in flight during the MAC
+                    // (loading first would need a fresh register set and a copy -- and a wait -- per iteration)
+                    mac(x[u], jb + u);
+                    x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
+                }
             }
         }
 #pragma unroll
