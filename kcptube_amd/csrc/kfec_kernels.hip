@@ -1572,6 +1572,8 @@ __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][G
     for (int u = 0; u < PD; ++u) x[u] = bload<VEC>(rd, dofs(min((uint32_t)u, K - 1)));
     uint32_t jb = 0;
     for (; jb + PD <= K; jb += PD) {
+        // (the encode's burst order, KFEC_MAC_BURST, measured slower here, also at 3 or 2 waves per SIMD:
+        // profiles/r05_syn_burst_ab.txt)
 #pragma unroll
         for (int u = 0; u < PD; ++u) {
             mac(x[u], jb + u);
