@@ -215,6 +215,9 @@ CASES = [
     (40, 60, 1440, 1440, 64, 20, "R=20, V=32: T-table decode entries, ~7 groups per workgroup, one chunk"),
     (30, 42, 97, 97, 21, 12, "R=12, odd pitch: bytewise T-table decode, entries in several chunks"),
     (60, 80, 1440, 1440, 33, None, "R=20, random 0..21 erasures over all 80: mixed m, some groups empty"),
+    (2, 5, 1440, 1440, 40, 2, "K < PD with MT=3: the encode's burst loop runs its tail only"),
+    (7, 11, 1440, 1440, 30, 4, "MT=4, K=7: one burst trip and a 3-shard tail"),
+    (9, 12, 1024, 1024, 50, None, "MT=3, K=9: two burst trips and a 1-shard tail, random erasures"),
 ]
 
 
