@@ -218,6 +218,8 @@ CASES = [
     (2, 5, 1440, 1440, 40, 2, "K < PD with MT=3: the encode's burst loop runs its tail only"),
     (7, 11, 1440, 1440, 30, 4, "MT=4, K=7: one burst trip and a 3-shard tail"),
     (9, 12, 1024, 1024, 50, None, "MT=3, K=9: two burst trips and a 1-shard tail, random erasures"),
+    (10, 13, 1400, 1400, 3001, None, "516 chunks: XCD span order (KFEC_XCD_ORDER) with a padded last run, random"),
+    (8, 12, 256, 256, 16411, 4, "513 chunks: XCD span order, one chunk past the threshold, MT=4"),
 ]
 
 
