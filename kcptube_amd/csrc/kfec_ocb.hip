@@ -191,8 +191,18 @@ __global__ void ocb_iv_kernel(const uint32_t *key, uint4 *off0)
 #ifndef KFEC_OCB_KSGPR
 #define KFEC_OCB_KSGPR 1  // the two-block rounds' keys by scalar loads, not LDS broadcast reads (A/B knob)
 #endif
+#ifndef KFEC_OCB_T4
+#define KFEC_OCB_T4 1  // four replicated tables (128 KiB, 1024-lane workgroups) and no rotate per column (A/B knob)
+#endif
+#if KFEC_OCB_T4
+#define OCB_RKEY rk  // the round keys as they are (no rotated half to fold them into)
+#define OCB_DKEY dk
+#else
+#define OCB_RKEY rkr
+#define OCB_DKEY dkr
+#endif
 constexpr int kRow = 8;
-constexpr int kOcbBlock = 512;
+constexpr int kOcbBlock = KFEC_OCB_T4 ? 1024 : 512;
 constexpr int kRowsPerBlock = kOcbBlock / kRow;
 
 struct OcbArgs {
@@ -225,6 +235,30 @@ constexpr int kRep = 32;
 #endif
 template <bool OPEN>
 struct OcbLds;
+//   KFEC_OCB_T4: Te2 / Te3 (Td2 / Td3) replicated as well, in a second 64 KiB half right after the first, so a
+//   column is T0[a] ^ T1[b] ^ T2[c] ^ T3[d] ^ k with no rotate (a 4-cycle op on gfx950, one of ~7 per column);
+//   128 KiB per workgroup, so one 1024-lane workgroup per CU keeps the 4 waves per SIMD of two 512-lane ones.
+#if KFEC_OCB_T4
+template <>
+struct OcbLds<false> {
+    uint32_t te[256][2][kRep];    // row v: the 32 copies of Te0[v], then of Te1[v] (256 B)
+    uint32_t te23[256][2][kRep];  // the same for Te2 / Te3, at te + 64 KiB
+    uint4 rk[15];
+    uint4 dk[15];
+    uint4 l[32];
+    uint4 rkr[15];
+    uint4 dkr[15];
+};
+template <>
+struct OcbLds<true> {
+    uint32_t td[256][2][kRep];
+    uint32_t td23[256][2][kRep];
+    uint4 rk[15];
+    uint4 dk[15];
+    uint4 l[32];
+    uint4 rkr[15];
+    uint4 dkr[15];
+#else
 template <>
 struct OcbLds<false> {
     uint4 rk[15];
@@ -242,6 +276,7 @@ struct OcbLds<true> {
     uint4 rkr[15];
     uint4 dkr[15];
     uint32_t td[256][2][kRep];
+#endif
 #if KFEC_OCB_ISB4
     uint32_t isb4[256][8];  // row v: 8 copies of InvS(v) in all four bytes (8 KiB; copy = lane % 8)
 #else
@@ -268,6 +303,26 @@ __device__ __forceinline__ uint32_t rep_at(const uint32_t (*T)[2][kRep], uint32_
     return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(T) + o + 128 * J);
 }
 
+#if KFEC_OCB_T4
+// one column of a round from the four tables: T0[b0(a)] ^ T1[b1(b)] ^ T2[b2(cc)] ^ T3[b3(d)] ^ k.  T2 / T3 sit
+// 64 KiB above T0 / T1: byte 2 of their lane term (c4 | 0x10000, loop-invariant) carries it through the same
+// single permute that places the state byte, so the halves cost the same address work and no rotate is left
+__device__ __forceinline__ uint32_t tcol(const uint32_t (*T)[2][kRep], uint32_t c4, uint32_t a, uint32_t b, uint32_t cc,
+                                         uint32_t d, uint32_t k)
+{
+    const uint8_t *base = reinterpret_cast<const uint8_t *>(T);
+    const uint32_t c4h = c4 | 0x10000u;
+    const uint32_t o0 = __builtin_amdgcn_perm(a, c4, 0x0C0C0400u);
+    const uint32_t o1 = KFEC_OCB_BITOP3 ? __builtin_amdgcn_bitop3_b32(b, 0xFF00u, c4, 0xEA)
+                                        : __builtin_amdgcn_perm(b, c4, 0x0C0C0500u);
+    const uint32_t o2 = __builtin_amdgcn_perm(cc, c4h, 0x0C020600u);
+    const uint32_t o3 = __builtin_amdgcn_perm(d, c4h, 0x0C020700u);
+    auto at = [&](uint32_t o, uint32_t imm) { return *reinterpret_cast<const uint32_t *>(base + o + imm); };
+    return xor3(xor3(at(o0, 0), at(o1, 128), at(o2, 0)), at(o3, 128), k);
+}
+static_assert(offsetof(OcbLds<false>, te23) == offsetof(OcbLds<false>, te) + 65536, "T2 / T3 half at +64 KiB");
+static_assert(offsetof(OcbLds<true>, td23) == offsetof(OcbLds<true>, td) + 65536, "Td2 / Td3 half at +64 KiB");
+#else
 // one column of a round: T0[b0(a)] ^ T1[b1(b)] ^ rotl16(T0[b2(cc)] ^ T1[b3(d)]) ^ k, with kr = rotl16(k) folded
 // into the rotated half: rotl16(T0[..] ^ T1[..] ^ kr) = rotl16(T0[..] ^ T1[..]) ^ k -- three VALU ops, not four
 __device__ __forceinline__ uint32_t tcol(const uint32_t (*T)[2][kRep], uint32_t c4, uint32_t a, uint32_t b, uint32_t cc,
@@ -276,6 +331,7 @@ __device__ __forceinline__ uint32_t tcol(const uint32_t (*T)[2][kRep], uint32_t 
     const uint32_t hi = xor3(rep_at<0, 2>(T, cc, c4), rep_at<1, 3>(T, d, c4), kr);
     return xor3(rep_at<0, 0>(T, a, c4), rep_at<1, 1>(T, b, c4), rotl(hi, 16));
 }
+#endif
 
 // Te0 holds S(x) in byte 1 (Te0[x] = {2S, S, S, 3S})
 __device__ __forceinline__ uint32_t sbox_col(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3)
@@ -292,7 +348,7 @@ __device__ __forceinline__ uint4 aes_enc(const OcbLds<false> &t, uint32_t c4, ui
     uint32_t s0 = in.x ^ t.rk[0].x, s1 = in.y ^ t.rk[0].y, s2 = in.z ^ t.rk[0].z, s3 = in.w ^ t.rk[0].w;
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
-        const uint4 k = t.rkr[r];
+        const uint4 k = t.OCB_RKEY[r];
         const uint32_t t0 = tcol(t.te, c4, s0, s1, s2, s3, k.x);
         const uint32_t t1 = tcol(t.te, c4, s1, s2, s3, s0, k.y);
         const uint32_t t2 = tcol(t.te, c4, s2, s3, s0, s1, k.z);
@@ -370,7 +426,7 @@ __device__ __forceinline__ uint4 aes_dec(const OcbLds<true> &t, uint32_t c4, uin
     uint32_t s0 = in.x ^ t.dk[0].x, s1 = in.y ^ t.dk[0].y, s2 = in.z ^ t.dk[0].z, s3 = in.w ^ t.dk[0].w;
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
-        const uint4 k = t.dkr[r];
+        const uint4 k = t.OCB_DKEY[r];
         // InvShiftRows: output column c row r takes input column c - r
         const uint32_t t0 = tcol(t.td, c4, s0, s3, s2, s1, k.x);
         const uint32_t t1 = tcol(t.td, c4, s1, s0, s3, s2, k.y);
@@ -407,7 +463,7 @@ __device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, const OcbKey *k
     auto round = [&](int r, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t b0, uint32_t b1,
                      uint32_t b2, uint32_t b3, uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3, uint32_t &e0,
                      uint32_t &e1, uint32_t &e2, uint32_t &e3) {
-        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->rkr, r) : t.rkr[r];
+        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->OCB_RKEY, r) : t.OCB_RKEY[r];
         o0 = tcol(t.te, c4, a0, a1, a2, a3, k.x);
         e0 = tcol(t.te, c4, b0, b1, b2, b3, k.x);
         o1 = tcol(t.te, c4, a1, a2, a3, a0, k.y);
@@ -429,7 +485,7 @@ __device__ __forceinline__ void aes_enc2(const OcbLds<false> &t, const OcbKey *k
 #else
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
-        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->rkr, r) : t.rkr[r];
+        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->OCB_RKEY, r) : t.OCB_RKEY[r];
         const uint32_t t0 = tcol(t.te, c4, s0, s1, s2, s3, k.x);
         const uint32_t v0 = tcol(t.te, c4, u0, u1, u2, u3, k.x);
         const uint32_t t1 = tcol(t.te, c4, s1, s2, s3, s0, k.y);
@@ -459,7 +515,7 @@ __device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, const OcbKey *ke
     auto round = [&](int r, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t b0, uint32_t b1,
                      uint32_t b2, uint32_t b3, uint32_t &o0, uint32_t &o1, uint32_t &o2, uint32_t &o3, uint32_t &e0,
                      uint32_t &e1, uint32_t &e2, uint32_t &e3) {
-        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->dkr, r) : t.dkr[r];
+        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->OCB_DKEY, r) : t.OCB_DKEY[r];
         o0 = tcol(t.td, c4, a0, a3, a2, a1, k.x);
         e0 = tcol(t.td, c4, b0, b3, b2, b1, k.x);
         o1 = tcol(t.td, c4, a1, a0, a3, a2, k.y);
@@ -481,7 +537,7 @@ __device__ __forceinline__ void aes_dec2(const OcbLds<true> &t, const OcbKey *ke
 #else
 #pragma unroll 1
     for (int r = 1; r < 14; ++r) {
-        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->dkr, r) : t.dkr[r];
+        const uint4 k = KFEC_OCB_KSGPR ? key_at(key->OCB_DKEY, r) : t.OCB_DKEY[r];
         const uint32_t t0 = tcol(t.td, c4, s0, s3, s2, s1, k.x);
         const uint32_t v0 = tcol(t.td, c4, u0, u3, u2, u1, k.x);
         const uint32_t t1 = tcol(t.td, c4, s1, s0, s3, s2, k.y);
@@ -520,14 +576,14 @@ __device__ __forceinline__ uint4 ocb_offset(const Lds &t, uint4 o0, uint32_t i)
 // the full blocks of each packet in turn, then lane b finishes packet b of the batch -- pad, checksum, tag --
 // so the pads of 8 packets cost one AES time, and so do their tags.
 template <bool OPEN>
-__global__ void __launch_bounds__(kOcbBlock, 4) ocb_kernel(OcbArgs a)  // (4 waves per SIMD: two workgroups per CU)
+__global__ void __launch_bounds__(kOcbBlock, 4) ocb_kernel(OcbArgs a)  // (4 waves per SIMD: two 512-lane or one 1024-lane workgroup per CU)
 {
     __shared__ OcbLds<OPEN> s;
     {
         // stage the round keys, L values and tables (open: the decryption half and Te0 once)
         const uint32_t *k32 = reinterpret_cast<const uint32_t *>(a.key);
-        uint32_t *s32 = reinterpret_cast<uint32_t *>(&s);
-        constexpr int kKeys = (int)(offsetof(OcbLds<OPEN>, l) / 4) + 32 * 4;
+        uint32_t *s32 = reinterpret_cast<uint32_t *>(s.rk);
+        constexpr int kKeys = (int)((offsetof(OcbLds<OPEN>, l) - offsetof(OcbLds<OPEN>, rk)) / 4) + 32 * 4;
         for (int i = threadIdx.x; i < kKeys; i += kOcbBlock) {
             // OcbLds: rk, dk, l -- OcbKey: rk, dk, lstar, ldollar, l
             const int src = i < 120 ? i : i + 8;
@@ -538,6 +594,10 @@ __global__ void __launch_bounds__(kOcbBlock, 4) ocb_kernel(OcbArgs a)  // (4 wav
         if constexpr (OPEN) {
             for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
                 s.td[i / (2 * kRep)][i / kRep % 2][i % kRep] = a.key->td[i / kRep % 2][i / (2 * kRep)];
+#if KFEC_OCB_T4
+            for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
+                s.td23[i / (2 * kRep)][i / kRep % 2][i % kRep] = a.key->td[2 + i / kRep % 2][i / (2 * kRep)];
+#endif
 #if KFEC_OCB_ISB4
             for (int i = threadIdx.x; i < 256 * 8; i += kOcbBlock) s.isb4[i / 8][i % 8] = a.key->isb[i / 8] * 0x01010101u;
 #else
@@ -551,6 +611,10 @@ __global__ void __launch_bounds__(kOcbBlock, 4) ocb_kernel(OcbArgs a)  // (4 wav
         } else {
             for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
                 s.te[i / (2 * kRep)][i / kRep % 2][i % kRep] = a.key->te[i / kRep % 2][i / (2 * kRep)];
+#if KFEC_OCB_T4
+            for (int i = threadIdx.x; i < 2 * 256 * kRep; i += kOcbBlock)
+                s.te23[i / (2 * kRep)][i / kRep % 2][i % kRep] = a.key->te[2 + i / kRep % 2][i / (2 * kRep)];
+#endif
         }
         __syncthreads();
     }
