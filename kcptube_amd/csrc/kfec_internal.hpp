@@ -146,8 +146,13 @@ int launch_framed_encode(const uint8_t *d_enc, int K, int N, size_t G, const voi
 // off[i] = i * pitch, len32[i] = len16[i] for i < P: descriptors of a packet array for the seal / open calls
 int launch_pkt_desc(size_t P, size_t pitch, const uint16_t *len16, uint64_t *off, uint32_t *len32, hipStream_t s);
 // packet integrity (kfec_seal.hip)
+// done (optional, out-of-place only): coherent pinned u32 that each workgroup adds 1 to when its rows are stored
+// and visible to the host; *blocks = the count to wait for (0: nothing launched / no count).  The queues count
+// launches of at most kSealCountRows rows (8 workgroups) only: measured faster there, slower with 23 workgroups.
+constexpr size_t kSealCountRows = 128;
 int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
-                const uint32_t *len, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok, hipStream_t s);
+                const uint32_t *len, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok, hipStream_t s,
+                uint32_t *done = nullptr, uint32_t *blocks = nullptr);
 
 }  // namespace kfec
 

@@ -462,6 +462,9 @@ struct kfec_txq {
     };
     std::vector<DataPkt> dpk;  // staged since the last flush, in send order
     Pinned h_sdesc, h_sealed;  // seal descriptors (+ iv draws) up; sealed rows + lengths down
+    Pinned h_done;             // the small sealed flush's completion count (coherent; launch_seal's `done`)
+    uint32_t done_sum = 0;     // workgroups launched into h_done so far (never reset: a kernel left running by a
+                               // failed flush still counts into it, ahead of the retry's in stream order)
     Device d_sdesc, d_sealed;
     OwnStream own;
     Trace trace;
@@ -548,6 +551,7 @@ int kfec_txq_create(const kfec_ctx *ctx, size_t max_groups, size_t max_datagram,
     // the sealed small flush's seal kernel writes its rows straight into h_sealed: fine-grained (coherent) memory
     // takes those stores through to the host as they are issued, instead of an L2 write-back at the kernel's end
     if (bar && env_flag("KFEC_QUEUE_COHERENT_OUT", true)) q->h_sealed.flags = hipHostMallocCoherent;
+    q->h_done.flags = hipHostMallocCoherent;
     try {
         q->off.resize(GK);
         q->len.resize(GK);
@@ -686,6 +690,34 @@ namespace {
 // always read, by the socket send or kfec_rx_push).  Not the receive flush: most of a group's recovered rows are
 // often unused, and prefetching them cost a consumer that does not read them (tools/latency_bench) 17 -> 18 /
 // 95 -> 114 us per 16 / 256-group flush (profiles/r05_emit_prefetch_ab.txt).
+// The small sealed flush and the opener (checksum16 / plain_xor, at most kSealCountRows packets) wait for the
+// seal kernel's own completion count instead of the stream (KFEC_QUEUE_SEAL_COUNT, default on): the workgroups
+// add themselves to a coherent pinned word once their rows are visible to the host, so the flush skips the
+// runtime's completion signal and stream wait (one 20:3 group: 15-16 -> 10-11 us; kfec_seal.hip count_done).
+bool seal_count_on()
+{
+    static const bool v = env_flag("KFEC_QUEUE_SEAL_COUNT", true);
+    return v;
+}
+
+// spin until the running count *done reaches `want` (modulo 2^32).  The stream is polled only once the wait has
+// lasted 2 ms (then every ms), so that a launch that failed or a kernel that faulted ends the wait with an error
+// instead of spinning forever: polling it every few thousand spins put ~15 us into a 16-group flush's wait.
+int wait_count(const volatile uint32_t *done, uint32_t want, hipStream_t s)
+{
+    auto reached = [&] { return (int32_t)(*done - want) >= 0; };
+    auto next = std::chrono::steady_clock::now() + std::chrono::milliseconds(2);
+    for (uint32_t spin = 1;; ++spin) {
+        if (reached()) return 0;
+        if ((spin & 1023u) == 0 && std::chrono::steady_clock::now() >= next) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e != hipErrorNotReady) return e == hipSuccess && reached() ? 0 : -1;
+            next = std::chrono::steady_clock::now() + std::chrono::milliseconds(1);
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 bool prefetch_on()
 {
     static const bool v = env_flag("KFEC_QUEUE_PREFETCH", true);
@@ -857,12 +889,32 @@ int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, v
     uint32_t *s_len = reinterpret_cast<uint32_t *>(hs + sO);
     const uint8_t *ds = q->d_sdesc.as<uint8_t>();
     if (st.fail()) return KFEC_EHIP;
-    int rc = seal_rows(q->seal_mode, q->aead, rows, dimg, red_base + nr * opitch, reinterpret_cast<const uint64_t *>(ds),
+    const bool count = !q->aead && seal_count_on() && rows <= kfec::kSealCountRows;
+    uint32_t blocks = 0;
+    int rc;
+    if (count) {
+        if (!q->h_done.p) {
+            if (q->h_done.ensure(64)) return KFEC_ENOMEM;
+            *q->h_done.as<volatile uint32_t>() = 0;
+            q->done_sum = 0;
+        }
+        rc = kfec::launch_seal(false, q->seal_mode, rows, dimg, red_base + nr * opitch, reinterpret_cast<const uint64_t *>(ds),
+                               reinterpret_cast<const uint32_t *>(ds + dL), hs, spitch, s_len, nullptr,
+                               static_cast<hipStream_t>(stream), q->h_done.as<uint32_t>(), &blocks)
+                 ? KFEC_EHIP
+                 : KFEC_OK;
+        if (rc == KFEC_OK) q->done_sum += blocks;
+    } else {
+        rc = seal_rows(q->seal_mode, q->aead, rows, dimg, red_base + nr * opitch, reinterpret_cast<const uint64_t *>(ds),
                        reinterpret_cast<const uint32_t *>(ds + dL), reinterpret_cast<const uint16_t *>(ds + dI), hs, spitch,
                        s_len, stream);
+    }
     if (rc) return rc;
     q->trace.mark();
-    if (st.fail() || hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) return KFEC_EHIP;
+    if (st.fail()) return KFEC_EHIP;
+    if (count ? wait_count(q->h_done.as<volatile uint32_t>(), q->done_sum, static_cast<hipStream_t>(stream)) != 0
+              : hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess)
+        return KFEC_EHIP;
     q->trace.mark();
     const bool pf = prefetch_on();
     if (pf) {
@@ -1544,6 +1596,8 @@ struct kfec_opener {
     bool bar = false;
     Pinned h_arena, h_desc, h_out;
     Device d_arena, d_desc, d_out;
+    Pinned h_done;          // BAR mode, checksum16 / plain_xor: the open kernel's completion count (as kfec_txq's)
+    uint32_t done_sum = 0;
     std::vector<uint64_t> tags;
     OwnStream own;
 };
@@ -1642,14 +1696,33 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
     }
     const uint64_t *d_off = reinterpret_cast<const uint64_t *>(dd);
     const uint32_t *d_len = reinterpret_cast<const uint32_t *>(dd + n * 8);
-    const int rc = o->aead ? kfec_aead_open_batch(o->aead, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok,
-                                                 stream)
-                           : kfec_open_batch(o->mode, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok,
-                                             stream);
+    // BAR mode without AEAD: wait for the kernel's own completion count, not the stream (see seal_count_on)
+    const bool count = o->bar && !o->aead && seal_count_on() && n <= kfec::kSealCountRows;
+    int rc;
+    if (count) {
+        if (!o->h_done.p) {
+            o->h_done.flags = hipHostMallocCoherent;
+            if (o->h_done.ensure(64)) return KFEC_ENOMEM;
+            *o->h_done.as<volatile uint32_t>() = 0;
+            o->done_sum = 0;
+        }
+        uint32_t blocks = 0;
+        rc = kfec::launch_seal(true, o->mode, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok, s,
+                               o->h_done.as<uint32_t>(), &blocks)
+                 ? KFEC_EHIP
+                 : KFEC_OK;
+        if (rc == KFEC_OK) o->done_sum += blocks;
+    } else {
+        rc = o->aead ? kfec_aead_open_batch(o->aead, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok, stream)
+                     : kfec_open_batch(o->mode, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok, stream);
+    }
     if (rc) return rc;
-    if ((!o->bar && hipMemcpyAsync(o->h_out.p, dr, L + n * 5, hipMemcpyDeviceToHost, s) != hipSuccess) ||
-        hipStreamSynchronize(s) != hipSuccess)
+    if (count) {
+        if (wait_count(o->h_done.as<volatile uint32_t>(), o->done_sum, s) != 0) return KFEC_EHIP;
+    } else if ((!o->bar && hipMemcpyAsync(o->h_out.p, dr, L + n * 5, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+               hipStreamSynchronize(s) != hipSuccess) {
         return KFEC_EHIP;
+    }
     const uint8_t *ho = o->h_out.as<uint8_t>();
     const uint32_t *h_len = reinterpret_cast<const uint32_t *>(ho + L);
     const uint8_t *h_ok = ho + L + n * 4;

@@ -462,7 +462,26 @@ struct SealArgs {
     const uint32_t *unshift;  // tab + kCrcWords
     uint64_t P;
     int mode;
+    uint32_t *done;  // optional completion count in coherent pinned host memory (launch_seal)
 };
+
+// The queues' small sealed flushes (kfec_pipeline.cpp, up to kSealCountRows rows) wait for this count instead of
+// the stream: every wave waits for its own stores, the workgroup meets at a barrier, and one lane releases at
+// system scope and adds the workgroup in (the producer form of MI355X_MICROARCH.md's hand-off recipe, with the
+// host as the consumer).  The host sees the rows once the last workgroup has counted itself, without the
+// runtime's completion signal and stream wait: one 20:3 group's flush waits 15-16 -> 10-11 us.  With many
+// workgroups it loses (16 groups: 24 -> 40 us, whether the release is a system-scope fence in every thread or
+// this one per workgroup, and 56 us with every output store written through at system scope instead).
+__device__ __forceinline__ void count_done(const SealArgs &a)
+{
+    if (!a.done) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
 
 __device__ __forceinline__ uint32_t *dst_row(const SealArgs &a, uint64_t p)
 {
@@ -737,6 +756,7 @@ __global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu
         }
         if (lane == 0) a.out_len[p] = n;
     });
+    count_done(a);
 }
 
 __global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu(4))) open_kernel(SealArgs a)
@@ -820,6 +840,7 @@ __global__ void __launch_bounds__(kSealBlock) __attribute__((amdgpu_waves_per_eu
             a.ok[p] = checksum16(crc) == trailer;
         }
     });
+    count_done(a);
 }
 
 // Checksum mode in place (kfec_seal_batch / kfec_open_batch with d_dst == NULL): the packets stay where they
@@ -897,8 +918,10 @@ uint32_t *crc_tables(hipStream_t s)
 }  // namespace
 
 int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
-                const uint32_t *len, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok, hipStream_t s)
+                const uint32_t *len, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok, hipStream_t s,
+                uint32_t *done, uint32_t *blocks)
 {
+    if (blocks) *blocks = 0;
     if (P == 0) return 0;
     SealArgs a{};
     a.src = static_cast<const uint32_t *>(src);
@@ -912,6 +935,7 @@ int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes
     a.ok = ok;
     a.P = P;
     a.mode = mode;
+    a.done = dst ? done : nullptr;  // (the in-place kernel does not count)
     a.tab = crc_tables(s);
     if (!a.tab) return -3;
     a.unshift = a.tab + kCrcWords;
@@ -930,6 +954,7 @@ int launch_seal(bool open, int mode, size_t P, const void *src, size_t src_bytes
     const int fit = !dst ? fit_in_place : open ? fit_open : fit_seal;
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
     const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * fit));
+    if (blocks && a.done) *blocks = grid.x;
     if (!dst) hipLaunchKernelGGL(seal_in_place_kernel, grid, dim3(kSealBlock), 0, s, a, open);  // checksum mode
     else if (open) hipLaunchKernelGGL(open_kernel, grid, dim3(kSealBlock), 0, s, a);
     else hipLaunchKernelGGL(seal_kernel, grid, dim3(kSealBlock), 0, s, a);
