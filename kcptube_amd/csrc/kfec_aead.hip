@@ -27,6 +27,7 @@
 #include <new>
 
 #include "../../include/kfec_aead.h"
+#include "kfec_count.hpp"
 #include "kfec_internal.hpp"
 #include "kfec_pkt.hpp"
 
@@ -369,6 +370,7 @@ struct AeadArgs {
     const uint4 *ks;  // keystream table (16-lane kernels, KFEC_AEAD_KS)
     uint64_t P;
     uint32_t key[8];
+    uint32_t *done;   // counted launch (kfec_count.hpp)
 };
 
 // seal (OPEN = false) or open one packet per row.  IETF: xchacha20 (subkey from the table, RFC 8439 MAC)
@@ -581,6 +583,7 @@ __global__ void __launch_bounds__(kAeadBlock) aead_kernel(AeadArgs a)
             if (lane == 0) a.out_len[p] = n + KFEC_AEAD_OVERHEAD;
         }
     }
+    count_workgroup_done(a.done);
 }
 
 // ---- 16-lane rows (KFEC_AEAD_ROW16) --------------------------------------------------------------------
@@ -845,6 +848,7 @@ __global__ void __launch_bounds__(kAeadBlock) aead16_kernel(AeadArgs a)
             if (lane == 0) a.out_len[p] = n + KFEC_AEAD_OVERHEAD;
         }
     }
+    count_workgroup_done(a.done);
 }
 
 int aead_cus() { return current_device_cus(); }
@@ -853,13 +857,14 @@ int aead_cus() { return current_device_cus(); }
 
 int launch_aead(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
                 const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
-                hipStream_t s)
+                hipStream_t s, uint32_t *done, uint32_t *blocks)
 {
+    if (blocks) *blocks = 0;
     if (P == 0) return 0;
     if (k->mode == KFEC_AEAD_AES_GCM)
-        return launch_gcm(k, open, P, src, src_bytes, off, len, iv, dst, dst_pitch, out_len, ok, s);
+        return launch_gcm(k, open, P, src, src_bytes, off, len, iv, dst, dst_pitch, out_len, ok, s, done, blocks);
     if (k->mode == KFEC_AEAD_AES_OCB)
-        return launch_ocb(k, open, P, src, src_bytes, off, len, iv, dst, dst_pitch, out_len, ok, s);
+        return launch_ocb(k, open, P, src, src_bytes, off, len, iv, dst, dst_pitch, out_len, ok, s, done, blocks);
     AeadArgs a{};
     a.src = static_cast<const uint32_t *>(src);
     a.src_dw = (src_bytes + 3) / 4;
@@ -873,11 +878,13 @@ int launch_aead(const kfec_aead *k, bool open, size_t P, const void *src, size_t
     a.tab = k->d_tab;
     a.ks = reinterpret_cast<const uint4 *>(k->d_ks);
     a.P = P;
+    a.done = done;
     for (int i = 0; i < 8; ++i) a.key[i] = k->key[i];
     const bool x = k->mode == KFEC_AEAD_XCHACHA20;
     if (KFEC_AEAD_ROW16) {
         const uint64_t rows = kAeadBlock / kRow16;
         const dim3 grid16((uint32_t)std::min<uint64_t>((P + rows - 1) / rows, (uint64_t)aead_cus() * 16));
+        if (blocks && done) *blocks = grid16.x;
         if (x && open) hipLaunchKernelGGL((aead16_kernel<true, true>), grid16, dim3(kAeadBlock), 0, s, a);
         else if (x) hipLaunchKernelGGL((aead16_kernel<true, false>), grid16, dim3(kAeadBlock), 0, s, a);
         else if (open) hipLaunchKernelGGL((aead16_kernel<false, true>), grid16, dim3(kAeadBlock), 0, s, a);
@@ -886,6 +893,7 @@ int launch_aead(const kfec_aead *k, bool open, size_t P, const void *src, size_t
     }
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
     const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)aead_cus() * 16));
+    if (blocks && done) *blocks = grid.x;
     if (x && open) hipLaunchKernelGGL((aead_kernel<true, true>), grid, dim3(kAeadBlock), 0, s, a);
     else if (x) hipLaunchKernelGGL((aead_kernel<true, false>), grid, dim3(kAeadBlock), 0, s, a);
     else if (open) hipLaunchKernelGGL((aead_kernel<false, true>), grid, dim3(kAeadBlock), 0, s, a);

@@ -22,6 +22,7 @@
 #include "kfec_aes.hpp"
 #include "kfec_pkt.hpp"
 #include "kfec_gf.hpp"
+#include "kfec_count.hpp"
 #include "kfec_internal.hpp"
 
 namespace kfec {
@@ -157,6 +158,7 @@ struct GcmArgs {
     const uint8_t *ks;    // [65536][kKsBytes] keystream
     const uint8_t *rk;    // AES round keys (blocks past the table)
     uint64_t P;
+    uint32_t *done;       // counted launch (kfec_count.hpp)
 };
 
 // a * H^(p+1) from the LDS tables T = s_gh[p] ([32][16] entries): per input dword 8 lookups in flight, folded
@@ -339,6 +341,7 @@ __global__ void __launch_bounds__(kGcmBlock) __attribute__((amdgpu_waves_per_eu(
             if (lane == 0) a.out_len[p] = n + KFEC_AEAD_OVERHEAD;
         }
     }
+    count_workgroup_done(a.done);
 }
 
 }  // namespace
@@ -369,8 +372,9 @@ void gcm_free(kfec_aead *k)
 
 int launch_gcm(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
                const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
-               hipStream_t s)
+               hipStream_t s, uint32_t *done, uint32_t *blocks)
 {
+    if (blocks) *blocks = 0;
     if (P == 0) return 0;
     GcmArgs a{};
     a.src = static_cast<const uint32_t *>(src);
@@ -387,11 +391,13 @@ int launch_gcm(const kfec_aead *k, bool open, size_t P, const void *src, size_t 
     a.ks = k->d_ks;
     a.rk = k->d_rk;
     a.P = P;
+    a.done = done;
     const int cus = current_device_cus();
     // 40 KiB of GHASH tables per workgroup: 3 resident per CU at 512 lanes (6 waves per SIMD), 4 at 256;
     // grid-stride over packets
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
     const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * (kGcmBlock >= 512 ? 3 : 4)));
+    if (blocks && done) *blocks = grid.x;
     if (open) hipLaunchKernelGGL(gcm_kernel<true>, grid, dim3(kGcmBlock), 0, s, a);
     else hipLaunchKernelGGL(gcm_kernel<false>, grid, dim3(kGcmBlock), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;

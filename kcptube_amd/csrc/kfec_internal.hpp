@@ -175,10 +175,15 @@ namespace kfec {
 int gcm_setup(kfec_aead *k, const uint32_t *d_key, hipStream_t s);
 void gcm_free(kfec_aead *k);  // every AES-mode table (gcm and ocb)
 int ocb_setup(kfec_aead *k, const uint32_t *d_key, hipStream_t s);
+// done / blocks: a counted launch, as launch_seal's (kfec_count.hpp)
 int launch_ocb(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
                const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
-               hipStream_t s);
+               hipStream_t s, uint32_t *done = nullptr, uint32_t *blocks = nullptr);
 int launch_gcm(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
                const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
-               hipStream_t s);
+               hipStream_t s, uint32_t *done = nullptr, uint32_t *blocks = nullptr);
+// every AEAD mode (chacha20 / xchacha20 here, aes_gcm / aes_ocb through the two above)
+int launch_aead(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
+                const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
+                hipStream_t s, uint32_t *done = nullptr, uint32_t *blocks = nullptr);
 }  // namespace kfec

@@ -19,6 +19,7 @@
 #include "../../include/kfec_aead.h"
 #include "kfec_aes.hpp"
 #include "kfec_gf.hpp"
+#include "kfec_count.hpp"
 #include "kfec_internal.hpp"
 #include "kfec_pkt.hpp"
 
@@ -218,6 +219,7 @@ struct OcbArgs {
     const OcbKey *key;
     const uint4 *off0;
     uint64_t P;
+    uint32_t *done;  // counted launch (kfec_count.hpp)
 };
 
 // What one workgroup stages into LDS.  AES is LDS-bound here: 16 byte-indexed table reads per round on random
@@ -765,6 +767,7 @@ __global__ void __launch_bounds__(kOcbBlock, 4) ocb_kernel(OcbArgs a)  // (4 wav
         }
         (void)t_off;
     }
+    count_workgroup_done(a.done);
 }
 
 }  // namespace
@@ -783,8 +786,9 @@ int ocb_setup(kfec_aead *k, const uint32_t *d_key, hipStream_t s)
 
 int launch_ocb(const kfec_aead *k, bool open, size_t P, const void *src, size_t src_bytes, const uint64_t *off,
                const uint32_t *len, const uint16_t *iv, void *dst, size_t dst_pitch, uint32_t *out_len, uint8_t *ok,
-               hipStream_t s)
+               hipStream_t s, uint32_t *done, uint32_t *blocks)
 {
+    if (blocks) *blocks = 0;
     if (P == 0) return 0;
     OcbArgs a{};
     a.src = static_cast<const uint32_t *>(src);
@@ -799,6 +803,7 @@ int launch_ocb(const kfec_aead *k, bool open, size_t P, const void *src, size_t 
     a.key = reinterpret_cast<const OcbKey *>(k->d_ocb);
     a.off0 = reinterpret_cast<const uint4 *>(k->d_ivt);
     a.P = P;
+    a.done = done;
     const int cus = current_device_cus();
     // one workgroup per resident slot (LDS tables and VGPRs decide how many fit on a CU)
     auto occupancy = [](const void *f) {
@@ -811,6 +816,7 @@ int launch_ocb(const kfec_aead *k, bool open, size_t P, const void *src, size_t 
     const int fit = open ? fit_open : fit_seal;
     const uint64_t want = (P + kRowsPerBlock - 1) / kRowsPerBlock;
     const dim3 grid((uint32_t)std::min<uint64_t>(want, (uint64_t)cus * fit));
+    if (blocks && done) *blocks = grid.x;
     if (open) hipLaunchKernelGGL(ocb_kernel<true>, grid, dim3(kOcbBlock), 0, s, a);
     else hipLaunchKernelGGL(ocb_kernel<false>, grid, dim3(kOcbBlock), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;

@@ -690,8 +690,8 @@ namespace {
 // always read, by the socket send or kfec_rx_push).  Not the receive flush: most of a group's recovered rows are
 // often unused, and prefetching them cost a consumer that does not read them (tools/latency_bench) 17 -> 18 /
 // 95 -> 114 us per 16 / 256-group flush (profiles/r05_emit_prefetch_ab.txt).
-// The small sealed flush and the opener (checksum16 / plain_xor, at most kSealCountRows packets) wait for the
-// seal kernel's own completion count instead of the stream (KFEC_QUEUE_SEAL_COUNT, default on): the workgroups
+// The small sealed flush and the opener (every mode, at most kSealCountRows packets) wait for the seal / open
+// kernel's own completion count instead of the stream (KFEC_QUEUE_SEAL_COUNT, default on): the workgroups
 // add themselves to a coherent pinned word once their rows are visible to the host, so the flush skips the
 // runtime's completion signal and stream wait (one 20:3 group: 15-16 -> 10-11 us; kfec_seal.hip count_done).
 bool seal_count_on()
@@ -889,7 +889,7 @@ int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, v
     uint32_t *s_len = reinterpret_cast<uint32_t *>(hs + sO);
     const uint8_t *ds = q->d_sdesc.as<uint8_t>();
     if (st.fail()) return KFEC_EHIP;
-    const bool count = !q->aead && seal_count_on() && rows <= kfec::kSealCountRows;
+    const bool count = seal_count_on() && rows <= kfec::kSealCountRows;
     uint32_t blocks = 0;
     int rc;
     if (count) {
@@ -898,9 +898,17 @@ int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, v
             *q->h_done.as<volatile uint32_t>() = 0;
             q->done_sum = 0;
         }
-        rc = kfec::launch_seal(false, q->seal_mode, rows, dimg, red_base + nr * opitch, reinterpret_cast<const uint64_t *>(ds),
-                               reinterpret_cast<const uint32_t *>(ds + dL), hs, spitch, s_len, nullptr,
-                               static_cast<hipStream_t>(stream), q->h_done.as<uint32_t>(), &blocks)
+        if (q->aead && hipSetDevice(q->aead->device) != hipSuccess) return KFEC_EHIP;  // (as kfec_aead_seal_batch)
+        const hipStream_t strm = static_cast<hipStream_t>(stream);
+        const size_t src_bytes = red_base + nr * opitch;
+        const uint64_t *d_off = reinterpret_cast<const uint64_t *>(ds);
+        const uint32_t *d_len = reinterpret_cast<const uint32_t *>(ds + dL);
+        uint32_t *cnt = q->h_done.as<uint32_t>();
+        rc = (q->aead ? kfec::launch_aead(q->aead, false, rows, dimg, src_bytes, d_off, d_len,
+                                          reinterpret_cast<const uint16_t *>(ds + dI), hs, spitch, s_len, nullptr, strm, cnt,
+                                          &blocks)
+                      : kfec::launch_seal(false, q->seal_mode, rows, dimg, src_bytes, d_off, d_len, hs, spitch, s_len,
+                                          nullptr, strm, cnt, &blocks))
                  ? KFEC_EHIP
                  : KFEC_OK;
         if (rc == KFEC_OK) q->done_sum += blocks;
@@ -1696,8 +1704,8 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
     }
     const uint64_t *d_off = reinterpret_cast<const uint64_t *>(dd);
     const uint32_t *d_len = reinterpret_cast<const uint32_t *>(dd + n * 8);
-    // BAR mode without AEAD: wait for the kernel's own completion count, not the stream (see seal_count_on)
-    const bool count = o->bar && !o->aead && seal_count_on() && n <= kfec::kSealCountRows;
+    // BAR mode, at most kSealCountRows packets: wait for the kernel's own completion count, not the stream
+    const bool count = o->bar && seal_count_on() && n <= kfec::kSealCountRows;
     int rc;
     if (count) {
         if (!o->h_done.p) {
@@ -1707,8 +1715,10 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
             o->done_sum = 0;
         }
         uint32_t blocks = 0;
-        rc = kfec::launch_seal(true, o->mode, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok, s,
-                               o->h_done.as<uint32_t>(), &blocks)
+        rc = (o->aead ? kfec::launch_aead(o->aead, true, n, o->d_arena.p, arena, d_off, d_len, nullptr, dr, o->pitch,
+                                          out_len, ok, s, o->h_done.as<uint32_t>(), &blocks)
+                      : kfec::launch_seal(true, o->mode, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok,
+                                          s, o->h_done.as<uint32_t>(), &blocks))
                  ? KFEC_EHIP
                  : KFEC_OK;
         if (rc == KFEC_OK) o->done_sum += blocks;

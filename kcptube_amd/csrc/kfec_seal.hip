@@ -18,6 +18,7 @@
 #include <mutex>
 
 #include "../../include/kfec_frame.h"
+#include "kfec_count.hpp"
 #include "kfec_internal.hpp"
 
 namespace kfec {
@@ -472,16 +473,7 @@ struct SealArgs {
 // runtime's completion signal and stream wait: one 20:3 group's flush waits 15-16 -> 10-11 us.  With many
 // workgroups it loses (16 groups: 24 -> 40 us, whether the release is a system-scope fence in every thread or
 // this one per workgroup, and 56 us with every output store written through at system scope instead).
-__device__ __forceinline__ void count_done(const SealArgs &a)
-{
-    if (!a.done) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
+__device__ __forceinline__ void count_done(const SealArgs &a) { count_workgroup_done(a.done); }
 
 __device__ __forceinline__ uint32_t *dst_row(const SealArgs &a, uint64_t p)
 {
