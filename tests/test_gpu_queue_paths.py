@@ -218,12 +218,15 @@ def test_sender_flush_retry_after_failure(dev, oracle, path, step):
     assert [(t, p) for t, _, _, p in got] == exp
 
 
+@pytest.mark.parametrize("groups", [14, 3])
 @pytest.mark.parametrize("enc", ["none", "chacha20", "aes_gcm"])
 @pytest.mark.parametrize("step", range(1, 12))
-def test_sealed_flush_retry_after_failure(dev, oracle, path, enc, step):
+def test_sealed_flush_retry_after_failure(dev, oracle, path, enc, step, groups):
     """Sealed deferred queue: a failed flush keeps the staged data packets, the groups and the iv counter; the
     retry emits every packet sealed with the same iv draws as an unfailed flush (replayed from the oracle).
-    worker: the small sealed flush (worker parity rows + one seal launch); launch: pack + seal kernels."""
+    worker: the small sealed flush (worker parity rows + one seal launch); launch: pack + seal kernels.
+    groups = 3 keeps the worker path's seal launch under kSealCountRows, so the flush waits for the kernel's
+    completion count (a failure after the launch leaves that kernel counting ahead of the retry's)."""
     from kcptube_amd.aead import AeadCipher
     from kcptube_amd.fec import KfecError
     from kcptube_amd.pipeline import FecSender, TxQueue, arm_flush_fault, iv_draw
@@ -237,7 +240,7 @@ def test_sealed_flush_retry_after_failure(dev, oracle, path, enc, step):
     txs = [FecSender(q, conv=0x77 + i, tag=i) for i in range(2)]
     refs = [fo.FecTx(K, N, lambda d, t, a: oracle.encode(K, N, d, a, t), conv=0x77 + i) for i in range(2)]
     plain = []
-    while q.pending() < 14:
+    while q.pending() < groups:
         i = rng.randrange(2)
         d = rng.randbytes(rng.randint(0, mtu))
         txs[i].send(d, timestamp=5)
@@ -247,7 +250,7 @@ def test_sealed_flush_retry_after_failure(dev, oracle, path, enc, step):
         got = q.flush(timestamp=5)
         arm_flush_fault(0)
     except KfecError:
-        assert q.pending() == 14 and q.staged() > 0
+        assert q.pending() == groups and q.staged() > 0
         got = q.flush(timestamp=5)
 
     def sealed(p, iv):
