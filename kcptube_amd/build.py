@@ -19,7 +19,7 @@ LIB = os.path.join(PKG, "libkfec.so")
 COMPAT_TEST = os.path.join(PKG, "compat_test")
 
 SOURCES = ["kfec_kernels.hip", "kfec_frame.hip", "kfec_seal.hip", "kfec_aead.hip", "kfec_gcm.hip", "kfec_ocb.hip", "kfec_worker.hip", "kfec_api.cpp", "kfec_pipeline.cpp"]
-HEADERS = ["kfec_gf.hpp", "kfec_internal.hpp", "kfec_count.hpp", "kfec_aes.hpp", "kfec_pkt.hpp"]
+HEADERS = ["kfec_gf.hpp", "kfec_internal.hpp", "kfec_count.hpp", "kfec_xcd.hpp", "kfec_aes.hpp", "kfec_pkt.hpp"]
 
 
 def _hipcc() -> str:

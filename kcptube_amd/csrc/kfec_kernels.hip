@@ -23,6 +23,7 @@
 //   reference's K x K Gauss-Jordan result bit for bit (the inverse is unique).
 #include "kfec_gf.hpp"
 #include "kfec_internal.hpp"
+#include "kfec_xcd.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -99,9 +100,6 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #endif
 #ifndef KFEC_MINW
 #define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the MAC kernels
-#endif
-#ifndef KFEC_XCD_ORDER
-#define KFEC_XCD_ORDER 16  // S > 0: single-tile MAC and dense syndrome launches give each XCD runs of S adjacent chunks
 #endif
 #ifndef KFEC_DEC_FACTORED
 #define KFEC_DEC_FACTORED 1  // R > 8 decode records carry the Lagrange factors, not the m x K coefficients (A/B knob)
@@ -989,34 +987,6 @@ constexpr uint32_t kDecGfBytes = 768 + 768 * 2;
 // on ONE XCD and all but the first read the chunk's shard bytes from that XCD's L2 (speed only: any
 // placement gives the same bytes).  The previous (chunk = x, tile = y) grid ran every chunk of tile 0 before
 // tile 1, so each of the 7 tiles of fec=200:55 re-read the 75.5 GB of data from HBM.
-// Single-tile grids (R <= 8) of at least kXcdMinGrid chunks with KFEC_XCD_ORDER = S: the grid is a multiple of
-// 8 S and, within each run of 8 S workgroups, XCD x (workgroups x, x + 8, ...) takes the S adjacent chunks
-// x S .. x S + S - 1, so the 128-byte lines that a group split between two of them shares (its rows at the split
-// column; at B = 1400 also the line between two groups) are fetched into, and written back from, one L2
-// instead of two, for 15 of every 16 splits.  Chunks past the last are padding and exit.  Measured
-// (profiles/r05_xcd_span_ab.txt, three boxes): S = 16 takes the 20:3 encode 4% and its decode 1-2% faster, the
-// 10:3 random decode 1-2%, the 8:4 encode 6%; one contiguous eighth per XCD made 20:3 6% slower.  Smaller grids
-// (small flushes) keep the plain order and no padding.
-constexpr uint32_t kXcdMinGrid = 512;
-
-__device__ __forceinline__ uint32_t xcd_chunk(uint32_t b)
-{
-    constexpr uint32_t S = KFEC_XCD_ORDER;
-    if constexpr (S == 0) {
-        return b;
-    } else {
-        if (gridDim.x < kXcdMinGrid) return b;
-        const uint32_t r = b % (8u * S);
-        return (b - r) + (r & 7u) * S + (r >> 3);
-    }
-}
-
-__host__ __device__ constexpr uint32_t xcd_grid(uint32_t chunks)
-{
-    return KFEC_XCD_ORDER && chunks >= kXcdMinGrid ? (chunks + 8u * KFEC_XCD_ORDER - 1u) / (8u * KFEC_XCD_ORDER) * (8u * KFEC_XCD_ORDER)
-                                                    : chunks;
-}
-
 __device__ __forceinline__ void block_chunk_tile(uint32_t b, uint32_t tiles, uint32_t &chunk, uint32_t &tile)
 {
     if (tiles <= 1) {
