@@ -53,8 +53,11 @@ int kfec_create(size_t K, size_t N, kfec_ctx **out);
  * Matrices are shared per (device, K, N) and immutable: create and reset build one on the first use of a shape
  * and are a lookup afterwards (no allocation, launch or synchronisation); the old matrix stays valid for
  * batched launches still in flight.  Matrices no coder uses stay cached up to 8 shapes / 4 MiB per device (the
- * least recently released beyond that are freed; that free waits for the device's in-flight work); the rest
- * are released with the device's last coder. */
+ * least recently released beyond that are freed; that free waits for the device's in-flight work).  Worst case:
+ * the reset (or destroy) that pushes the cache past its bound blocks its own thread until the longest batched
+ * launch in flight on the device ends (~150 ms at fec=200:55, 256k groups); the free runs outside the cache's
+ * lock, so other threads' create / reset / kfec_cached_matrices do not wait for it.  The rest are released with
+ * the device's last coder. */
 int kfec_reset(kfec_ctx *ctx, size_t K, size_t N);
 void kfec_destroy(kfec_ctx *ctx);
 size_t kfec_get_K(const kfec_ctx *ctx);

@@ -112,10 +112,11 @@ int probe_device(kfec::DeviceInfo &di)
     return KFEC_OK;
 }
 
-// Free the least recently released unreferenced matrices while more than kKeepUnused (or kKeepUnusedBytes) of
-// them are cached.  Called with dm.mu held.
-void evict_unused(DevMatrices &dm)
+// Unlink the least recently released unreferenced matrices while more than kKeepUnused (or kKeepUnusedBytes) of
+// them are cached.  Called with dm.mu held; the caller frees what it returns after releasing the lock.
+std::vector<Matrix *> evict_unused(DevMatrices &dm)
 {
+    std::vector<Matrix *> gone;
     for (;;) {
         size_t n = 0, bytes = 0;
         Matrix *oldest = nullptr;
@@ -125,10 +126,14 @@ void evict_unused(DevMatrices &dm)
             bytes += kfec::enc_alloc_bytes(m->K, m->N);
             if (!oldest || m->released < oldest->released) oldest = m;
         }
-        if (!oldest || (n <= kKeepUnused && bytes <= kKeepUnusedBytes)) return;
-        (void)hipFree(oldest->d);  // (waits for the device's in-flight work, which may still read it)
+        if (!oldest || (n <= kKeepUnused && bytes <= kKeepUnusedBytes)) return gone;
         dm.all.erase(std::remove(dm.all.begin(), dm.all.end(), oldest), dm.all.end());
-        delete oldest;
+        try {
+            gone.push_back(oldest);
+        } catch (...) {
+            (void)hipFree(oldest->d);  // (out of host memory: free it here, under the lock, as before)
+            delete oldest;
+        }
     }
 }
 
@@ -136,10 +141,20 @@ void unref_matrix(int dev, Matrix *m)
 {
     if (!m) return;
     DevMatrices &dm = g_mats[dev];
-    std::lock_guard<std::mutex> lk(dm.mu);
-    if (m->refs && --m->refs == 0) {
-        m->released = ++dm.clock;
-        evict_unused(dm);
+    std::vector<Matrix *> gone;
+    {
+        std::lock_guard<std::mutex> lk(dm.mu);
+        if (m->refs && --m->refs == 0) {
+            m->released = ++dm.clock;
+            gone = evict_unused(dm);
+        }
+    }
+    // hipFree waits for the device's in-flight work (which may still read the matrix) -- up to the longest
+    // batched launch, ~150 ms at fec=200:55 -- so it runs without the lock: kfec_create / kfec_reset /
+    // kfec_cached_matrices of other threads on this device do not queue behind it
+    for (Matrix *g : gone) {
+        (void)hipFree(g->d);
+        delete g;
     }
 }
 

@@ -310,11 +310,24 @@ struct Arena {
     }
     // before the host copy is compacted: no upload may still be reading it
     int quiesce() { return up.drain(); }
-    // after the host copy was compacted to [0, used): rewrite the image (BAR) / restart the upload
-    void restage(size_t used)
+    // the mode for the flushes after a compaction; true when the device image must then be rewritten whole (BAR
+    // mode now, not before: the image holds only what the uploads carried).  Otherwise a compaction mirrors just
+    // the ranges it moved (moved()): the unmoved live bytes are in the image since their staging.
+    bool switch_mode(size_t last_flush_groups)
+    {
+        const bool was = bar;
+        set_mode(last_flush_groups);
+        return bar && !was;
+    }
+    void moved(size_t at, size_t n, bool whole)
+    {
+        if (!whole) mirror(at, n);
+    }
+    // after the host copy was compacted to [0, used): restart the upload (pinned) / rewrite the image if whole
+    void restage(size_t used, bool whole)
     {
         up.issued = 0;
-        mirror(0, used);
+        if (whole) mirror(0, used);
     }
     // room for `need` more bytes after `used` when nothing is queued: doubles both copies, keeps [0, used)
     int grow(size_t used, size_t need)
@@ -472,6 +485,13 @@ struct kfec_txq {
     ~kfec_txq() { trace.print("txq"); }
 };
 
+// test-only hook (not in the headers): the coherent completion count minus the baseline the next counted wait
+// adds to (0 whenever no counted kernel is in flight, e.g. after any flush returned, failed ones included)
+extern "C" int32_t kfec_test_txq_count_drift(const kfec_txq *q)
+{
+    return q && q->h_done.p ? (int32_t)(*q->h_done.as<volatile uint32_t>() - q->done_sum) : 0;
+}
+
 struct kfec_tx {
     kfec_txq *q = nullptr;
     uint32_t conv = 0;
@@ -507,15 +527,18 @@ int tx_compact(kfec_txq *q)
     for (kfec_tx *tx : q->txs)
         for (size_t i = 0; i < tx->cached; ++i) part.push_back({tx->cache_off[i], tx->cache_len[i], &tx->cache_off[i]});
     std::sort(part.begin(), part.end());
+    const bool whole = q->arena.switch_mode(q->last_n);
     size_t at = 0;
     for (const Part &p : part) {
-        if (p.len && at != p.off) std::memmove(q->arena.host(at), q->arena.host(p.off), p.len);
+        if (p.len && at != p.off) {
+            std::memmove(q->arena.host(at), q->arena.host(p.off), p.len);
+            q->arena.moved(at, p.len, whole);
+        }
         *p.rec = at;
         at += q->arena.step(p.len);
     }
     q->used = at;
-    q->arena.set_mode(q->last_n);
-    q->arena.restage(at);
+    q->arena.restage(at, whole);
     return KFEC_OK;
 }
 
@@ -718,6 +741,17 @@ int wait_count(const volatile uint32_t *done, uint32_t want, hipStream_t s)
     }
 }
 
+// A counted flush that fails after its launch was attempted: the launch's error code (hipGetLastError) says
+// nothing certain about whether the kernel was enqueued, so the running count may or may not grow by its
+// workgroups.  Drain the stream, then take the coherent count itself as the new baseline: the next counted wait
+// can then neither return before its own kernel's rows are written nor spin on workgroups that never ran.
+void count_resync(const Pinned &h_done, uint32_t &done_sum, hipStream_t s)
+{
+    (void)hipStreamSynchronize(s);
+    (void)hipGetLastError();
+    done_sum = *h_done.as<volatile uint32_t>();
+}
+
 bool prefetch_on()
 {
     static const bool v = env_flag("KFEC_QUEUE_PREFETCH", true);
@@ -904,6 +938,7 @@ int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, v
         const uint64_t *d_off = reinterpret_cast<const uint64_t *>(ds);
         const uint32_t *d_len = reinterpret_cast<const uint32_t *>(ds + dL);
         uint32_t *cnt = q->h_done.as<uint32_t>();
+        (void)hipGetLastError();  // (no stale error of an earlier call may read as this launch's)
         rc = (q->aead ? kfec::launch_aead(q->aead, false, rows, dimg, src_bytes, d_off, d_len,
                                           reinterpret_cast<const uint16_t *>(ds + dI), hs, spitch, s_len, nullptr, strm, cnt,
                                           &blocks)
@@ -917,12 +952,17 @@ int txq_flush_sealed_small(kfec_txq *q, uint32_t timestamp, kfec_packet_cb cb, v
                        reinterpret_cast<const uint32_t *>(ds + dL), reinterpret_cast<const uint16_t *>(ds + dI), hs, spitch,
                        s_len, stream);
     }
-    if (rc) return rc;
+    const hipStream_t ss = static_cast<hipStream_t>(stream);
+    auto fail = [&](int code) {
+        if (count) count_resync(q->h_done, q->done_sum, ss);
+        return code;
+    };
+    if (rc) return fail(rc);
     q->trace.mark();
-    if (st.fail()) return KFEC_EHIP;
-    if (count ? wait_count(q->h_done.as<volatile uint32_t>(), q->done_sum, static_cast<hipStream_t>(stream)) != 0
-              : hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess)
-        return KFEC_EHIP;
+    if (st.fail()) return fail(KFEC_EHIP);
+    if (count ? wait_count(q->h_done.as<volatile uint32_t>(), q->done_sum, ss) != 0
+              : hipStreamSynchronize(ss) != hipSuccess)
+        return fail(KFEC_EHIP);
     q->trace.mark();
     const bool pf = prefetch_on();
     if (pf) {
@@ -1219,15 +1259,18 @@ int rx_compact(kfec_rxq *q)
                 }
         }
     std::sort(part.begin(), part.end());
+    const bool whole = q->arena.switch_mode(q->last_n);
     size_t at = 0;
     for (const Part &p : part) {
-        if (p.len && at != *p.off) std::memmove(q->arena.host(at), q->arena.host(*p.off), p.len);
+        if (p.len && at != *p.off) {
+            std::memmove(q->arena.host(at), q->arena.host(*p.off), p.len);
+            q->arena.moved(at, p.len, whole);
+        }
         *p.off = at;
         at += q->arena.step(p.len);
     }
     q->used = at;
-    q->arena.set_mode(q->last_n);
-    q->arena.restage(at);
+    q->arena.restage(at, whole);
     return KFEC_OK;
 }
 
@@ -1612,6 +1655,12 @@ struct kfec_opener {
 
 extern "C" {
 
+// test-only hook (not in the headers): as kfec_test_txq_count_drift
+int32_t kfec_test_opener_count_drift(const kfec_opener *o)
+{
+    return o && o->h_done.p ? (int32_t)(*o->h_done.as<volatile uint32_t>() - o->done_sum) : 0;
+}
+
 int kfec_opener_create(int mode, const kfec_aead *aead, size_t max_packets, size_t max_packet, kfec_opener **out)
 {
     if (!out) return KFEC_EINVAL;
@@ -1715,6 +1764,7 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
             o->done_sum = 0;
         }
         uint32_t blocks = 0;
+        (void)hipGetLastError();  // (no stale error of an earlier call may read as this launch's)
         rc = (o->aead ? kfec::launch_aead(o->aead, true, n, o->d_arena.p, arena, d_off, d_len, nullptr, dr, o->pitch,
                                           out_len, ok, s, o->h_done.as<uint32_t>(), &blocks)
                       : kfec::launch_seal(true, o->mode, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok,
@@ -1726,9 +1776,15 @@ int kfec_opener_flush(kfec_opener *o, kfec_opened_cb cb, void *user, void *strea
         rc = o->aead ? kfec_aead_open_batch(o->aead, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok, stream)
                      : kfec_open_batch(o->mode, n, o->d_arena.p, arena, d_off, d_len, dr, o->pitch, out_len, ok, stream);
     }
-    if (rc) return rc;
+    if (rc) {
+        if (count) count_resync(o->h_done, o->done_sum, s);
+        return rc;
+    }
     if (count) {
-        if (wait_count(o->h_done.as<volatile uint32_t>(), o->done_sum, s) != 0) return KFEC_EHIP;
+        if (wait_count(o->h_done.as<volatile uint32_t>(), o->done_sum, s) != 0) {
+            count_resync(o->h_done, o->done_sum, s);
+            return KFEC_EHIP;
+        }
     } else if ((!o->bar && hipMemcpyAsync(o->h_out.p, dr, L + n * 5, hipMemcpyDeviceToHost, s) != hipSuccess) ||
                hipStreamSynchronize(s) != hipSuccess) {
         return KFEC_EHIP;

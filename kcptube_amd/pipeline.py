@@ -96,6 +96,13 @@ class TxQueue:
     def staged(self) -> int:
         return int(self._lib.kfec_txq_staged(self._q))
 
+    def count_drift(self) -> int:
+        """Test hook: the sealed small flush's completion count minus the baseline its next wait adds to (0 when
+        no counted kernel is in flight -- after every flush, a failed one included)."""
+        self._lib.kfec_test_txq_count_drift.restype = C.c_int32
+        self._lib.kfec_test_txq_count_drift.argtypes = [C.c_void_p]
+        return int(self._lib.kfec_test_txq_count_drift(self._q))
+
     def flush(self, timestamp: int = 0) -> list[tuple[int, int, int, bytes]]:
         """Encode every queued group; returns [(tag, sn, sub_sn, packet bytes)] in emission order: the redundant
         packets in queue order or, with deferred data packets, every packet in the order fec_maker sends it."""
@@ -228,6 +235,12 @@ class Opener:
 
     def pending(self) -> int:
         return int(self._lib.kfec_opener_pending(self._o))
+
+    def count_drift(self) -> int:
+        """Test hook: as TxQueue.count_drift, for the opener's counted flushes."""
+        self._lib.kfec_test_opener_count_drift.restype = C.c_int32
+        self._lib.kfec_test_opener_count_drift.argtypes = [C.c_void_p]
+        return int(self._lib.kfec_test_opener_count_drift(self._o))
 
     def add(self, pkt: bytes, tag: int = 0) -> None:
         buf = (C.c_uint8 * max(len(pkt), 1)).from_buffer_copy(bytes(pkt) or b"\0")

@@ -251,11 +251,26 @@ def test_sealed_flush_retry_after_failure(dev, oracle, path, enc, step, groups):
         arm_flush_fault(0)
     except KfecError:
         assert q.pending() == groups and q.staged() > 0
+        # a failure after the counted launch re-baselines the count on the drained stream (advisor, round 5):
+        # neither ahead (the next wait would return before its kernel wrote its rows) nor behind (it would spin)
+        assert q.count_drift() == 0
         got = q.flush(timestamp=5)
+    assert q.count_drift() == 0
 
     def sealed(p, iv):
         return fo.seal(p, 0) if enc == "none" else ao.aead_seal(enc, password, p, iv)
     assert [(t, p) for t, _, _, p in got] == [(t, sealed(p, iv_draw(seed, k))) for k, (t, p) in enumerate(plain)]
+    # the flush after the retried one waits on the re-based count: its packets are the oracle's too
+    k0 = len(plain)
+    more = []
+    while q.pending() < groups:
+        i = rng.randrange(2)
+        d = rng.randbytes(rng.randint(0, mtu))
+        txs[i].send(d, timestamp=6)
+        more += [(i, p) for p in refs[i].send(d, timestamp=6)]
+    got2 = q.flush(timestamp=6)
+    assert q.count_drift() == 0
+    assert [(t, p) for t, _, _, p in got2] == [(t, sealed(p, iv_draw(seed, k0 + k))) for k, (t, p) in enumerate(more)]
 
 
 @pytest.mark.parametrize("step", range(1, 8))
