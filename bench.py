@@ -19,13 +19,15 @@ Also reported (rank 0):
   roofline      the dominant kernel (the encode MAC launch; decode for decode-only configs) from HIP events
                 on its stream, plus the whole step (encode + decode algorithmic bytes / ms_per_step) as total
                 and read-only fractions of the 8 TB/s spec AND of this box's measured linear-read ceiling
-                (tools/libkfec_calib.so, timed in the same run), and against the "mix ceiling": the same
-                launch's reads + writes per group in their ideal streaming form (one workgroup per group,
-                contiguous 16-B loads, nt stores, no GF arithmetic), timed in the same run; for fec=200:55
-                (VALU-bound) the byte-MAC rate against the measured GF-MAC VALU ceiling of the same
-                instruction mix.
+                (tools/libkfec_calib.so, timed in the same run), and against the "mix ceiling": the faster of
+                (a) the same launch's reads + writes per group in their ideal streaming form (calib_mix: one
+                workgroup per group, contiguous 16-B loads, nt stores, no GF arithmetic) and (b) the product's
+                own kernel with its GF arithmetic removed (tools/libkfec_arithfree.so: same grid, loads, stores),
+                both timed in the same run; for fec=200:55 (VALU-bound) the byte-MAC rate against the measured
+                GF-MAC VALU ceiling of the same instruction mix.  Every rank measures its own GPU's ceilings
+                (per_rank carries each rank's fractions).
   cpu_baseline  the reference coder (oracle/_ref, compiled from the reference's own sources) on all usable
-                host cores over >= 64k distinct groups (rank 0, N = 1 only).
+                host cores over >= 64k distinct groups: rank 0, at every N, after every rank's GPU work.
 """
 from __future__ import annotations
 
@@ -165,6 +167,66 @@ def cpu_baseline(K, N, B, pool, erase, mode, target_cpu_s, groups, decode_only=F
                       f"per thread); value_1core: {g1} groups x 1 pass on 1 thread"}
 
 
+def best_ms(torch, launch, reps=5):
+    """Fastest of reps + 1 event-timed launches on the current stream (launch(stream) -> 0 on success), or None."""
+    s = torch.cuda.current_stream()
+    best = None
+    for _ in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        if launch(s.cuda_stream) != 0:
+            return None
+        e1.record(s)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    return best
+
+
+class ArithFree:
+    """tools/libkfec_arithfree.so (kcptube_amd/build.py): the product's own sources with every GF multiply-accumulate
+    of mac_kernel and syn_kernel replaced by a plain XOR of the shard granules and no table reads -- the same grids
+    (XCD spans), prep kernels, loads and stores.  Measurement only (its bytes are wrong): its launch time on the
+    bench's own tensors is the ceiling of the product kernel's access pattern, timed in the same run."""
+
+    def __init__(self, K, N):
+        path = os.path.join(ROOT, "tools", "libkfec_arithfree.so")
+        self.lib = ctypes.CDLL(path) if os.path.exists(path) else None
+        self.ctx = ctypes.c_void_p()
+        if not self.lib:
+            return
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        self.lib.kfec_create.argtypes = [sz, sz, ctypes.POINTER(vp)]
+        self.lib.kfec_destroy.argtypes = [vp]
+        self.lib.kfec_encode_batch.argtypes = [vp, sz, sz, sz, vp, vp, vp]
+        self.lib.kfec_decode_workspace_size.argtypes = [vp, sz]
+        self.lib.kfec_decode_workspace_size.restype = sz
+        self.lib.kfec_decode_batch.argtypes = [vp, sz, sz, sz, vp, vp, vp, vp, vp, vp, vp, vp]
+        if self.lib.kfec_create(K, N, ctypes.byref(self.ctx)) != 0:
+            self.lib = None
+
+    def encode_ms(self, torch, data, parity, B):
+        if not self.lib:
+            return None
+        G, _, pitch = data.shape
+        return best_ms(torch, lambda st: self.lib.kfec_encode_batch(self.ctx, G, B, pitch, data.data_ptr(),
+                                                                    parity.data_ptr(), st))
+
+    def decode_ms(self, torch, data, parity, present, out, out_idx, status, B, dev):
+        if not self.lib:
+            return None
+        G, _, pitch = data.shape
+        ws = torch.empty(max(self.lib.kfec_decode_workspace_size(self.ctx, G), 16), dtype=torch.uint8, device=dev)
+        return best_ms(torch, lambda st: self.lib.kfec_decode_batch(
+            self.ctx, G, B, pitch, data.data_ptr(), parity.data_ptr(), present.data_ptr(), out.data_ptr(),
+            out_idx.data_ptr(), status.data_ptr(), ws.data_ptr(), st))
+
+    def close(self):
+        if self.lib and self.ctx.value:
+            self.lib.kfec_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+
 class Calib:
     """tools/libkfec_calib.so: on-box read ceiling and GF-MAC VALU ceiling (measurement only)."""
 
@@ -182,18 +244,7 @@ class Calib:
                                            ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
 
     def _time(self, torch, launch, reps=5):
-        s = torch.cuda.current_stream()
-        best = None
-        for _ in range(reps + 1):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            if launch(s.cuda_stream) != 0:
-                return None
-            e1.record(s)
-            e1.synchronize()
-            ms = e0.elapsed_time(e1)
-            best = ms if best is None else min(best, ms)
-        return best
+        return best_ms(torch, launch, reps)
 
     def read_ceiling(self, torch, buf):
         """GB/s of a linear read of `buf` (a device tensor of a few GB)."""
@@ -411,15 +462,6 @@ def main():
 
     enc_ms = sum(ev[i][0].elapsed_time(ev[i][1]) for i in range(n_ev)) / n_ev
     dec_ms = sum(ev[i][1].elapsed_time(ev[i][2]) for i in range(n_ev)) / n_ev
-    # every rank's own timing and device, gathered after the timed region (per_rank in the JSON line)
-    my_rec = {"rank": rank, "device": device_ident(torch, dev, local_dev), "name": torch.cuda.get_device_name(dev),
-              "groups": G, "encode_ms": round(enc_ms, 4) if do_enc else None, "decode_ms": round(dec_ms, 4),
-              "wall_ms_per_step": round(local_elapsed / args.steps * 1e3, 4)}
-    records = [my_rec]
-    if world > 1:
-        records = [None] * world
-        dist.all_gather_object(records, my_rec)
-    devices = len({r["device"] for r in records})  # distinct GPUs over every rank (and node)
 
     # correctness of what was timed (untimed): every erased data shard recovered bit-exact
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -461,7 +503,7 @@ def main():
     value = payload / elapsed / 2**30
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline: algorithmic HBM bytes per launch / measured launch duration (rank 0's share)
+    # roofline: algorithmic HBM bytes per launch / measured launch duration (this rank's share)
     enc_bytes = G * (K + R) * B                    # read K*B, write R*B per group
     dec_bytes = n_dec * K * B + n_rec * B          # read the K selected shares, write the m recovered
     enc_read = G * K * B
@@ -491,14 +533,25 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    # ceilings, measured on EVERY rank's own GPU after the timed region and the verification (the buffers they
+    # write -- out, idx, st -- have been checked already): the linear-read ceiling, the ideal streaming form of the
+    # dominant launch's byte mix (calib_mix), and the product's own kernels with the GF arithmetic removed
+    # (tools/libkfec_arithfree.so: same grid, loads and stores); the mix ceiling is the faster of the two
     calib = Calib()
-    read_ceiling = calib.read_ceiling(torch, data) if rank == 0 else None
-    # the dominant launch's byte mix (per decoded / encoded group: reads, writes) in its ideal streaming form
+    read_ceiling = calib.read_ceiling(torch, data)
     if do_enc:
         mix_r, mix_w, mix_g = K * B, R * B, G
     else:
         mix_r, mix_w, mix_g = K * B, (n_rec * B / n_dec if n_dec else 0), max(n_dec, 1)
-    mix_ceiling = calib.mix_ceiling(torch, data, out, mix_g, mix_r, mix_w) if rank == 0 and args.config != "200:55" else None
+    mix_calib = calib.mix_ceiling(torch, data, out, mix_g, mix_r, mix_w) if args.config != "200:55" else None
+    af = ArithFree(K, N)
+    if do_enc:
+        af_ms = af.encode_ms(torch, data, out, B)
+    else:
+        af_ms = af.decode_ms(torch, data, par, masks, out, idx, st, B, dev)
+    af.close()
+    af_rate = dom_bytes / (af_ms * 1e-3) / 1e9 if af_ms else None
+    mix_ceiling = max(mix_calib or 0.0, af_rate or 0.0) or None
     roof = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),
@@ -511,11 +564,18 @@ def main():
             "step_frac_of_ceiling": round(step_gbs / read_ceiling, 4) if read_ceiling else None,
             "step_frac_read_of_ceiling": round(step_read_gbs / read_ceiling, 4) if read_ceiling else None,
             "frac_of_ceiling": round(achieved / read_ceiling, 4) if read_ceiling else None,
-            # the same launch against the ideal streaming form of its own read + write mix (calib_mix)
+            # the same launch against the faster of two ideal forms of its own read + write mix, both timed in this
+            # run: calib_mix (one workgroup per group, contiguous, no arithmetic) and the arithmetic-free build of the
+            # product kernel itself (best of 5 launches; the product's time is the mean over the timed steps)
             "mix_ceiling": round(mix_ceiling, 1) if mix_ceiling else None,
+            "mix_ceiling_kind": (None if not mix_ceiling else
+                                 "arithfree" if (af_rate or 0) >= (mix_calib or 0) else "calib_mix"),
+            "mix_ceiling_calib": round(mix_calib, 1) if mix_calib else None,
+            "arithfree_ms": round(af_ms, 4) if af_ms else None,
+            "arithfree_GBps": round(af_rate, 1) if af_rate else None,
             "mix_ceiling_bytes_per_group": [mix_r, round(mix_w, 1)],
             "frac_of_mix_ceiling": round(achieved / mix_ceiling, 4) if mix_ceiling else None}
-    if args.config == "200:55" and rank == 0:
+    if args.config == "200:55":
         # VALU-bound: byte-MACs per second of each kernel against the perm MAC's issue bound on this box
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         ceil_mac = calib.gfmac_ceiling(torch, dev, cus)
@@ -529,6 +589,19 @@ def main():
                      "hbm_achieved": round(achieved, 1), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
                      "ceiling_kernel": "issue bound: 4 byte-MACs per lane per (3 v_perm_b32 + v_bitop3_b32 + "
                                        "v_xor_b32) at the rates tools/calib.hip measures on this box"})
+
+    # every rank's own timing, device and fractions, gathered after the timed region (per_rank in the JSON line)
+    my_rec = {"rank": rank, "device": device_ident(torch, dev, local_dev), "name": torch.cuda.get_device_name(dev),
+              "groups": G, "encode_ms": round(enc_ms, 4) if do_enc else None, "decode_ms": round(dec_ms, 4),
+              "wall_ms_per_step": round(local_elapsed / args.steps * 1e3, 4),
+              "frac": roof["frac"], "frac_of_ceiling": roof["frac_of_ceiling"],
+              "frac_of_mix_ceiling": roof["frac_of_mix_ceiling"], "read_ceiling": roof["read_ceiling"],
+              "mix_ceiling": roof["mix_ceiling"]}
+    records = [my_rec]
+    if world > 1:
+        records = [None] * world
+        dist.all_gather_object(records, my_rec)
+    devices = len({r["device"] for r in records})  # distinct GPUs over every rank (and node)
 
     result = {
         "metric": METRIC,
@@ -562,7 +635,11 @@ def main():
         result["multi_rank"] = per_rank_summary(records, value, [K * B * r["groups"] for r in records])
     if parts:
         result["combined_digest"] = combine_digests([d for ds in all_digs for d in ds])
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if world > 1:
+        dist.barrier()  # every rank is past its GPU work: the CPU leg below cannot perturb any GPU timing
+    if rank == 0 and not args.no_cpu:
+        # the reference coder on this node's host cores, in the same run, at every N (north_star): rank 0 only,
+        # after the timed region and every rank's ceilings
         try:
             result["cpu_baseline"] = cpu_baseline(K, N, B, pool, erase, mode, args.cpu_seconds, args.cpu_groups,
                                                   decode_only=not do_enc)
@@ -571,6 +648,7 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
+        dist.barrier()  # (the other ranks wait for rank 0's CPU leg instead of tearing the group down under it)
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)

@@ -42,7 +42,8 @@ def _stale(target: str, deps: list[str]) -> bool:
 FILE_FLAGS: dict[str, list[str]] = {"kfec_ocb.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 
 
-def _compile_link(out: str, common: list[str], file_flags: dict[str, list[str]], verbose: bool = False) -> None:
+def _compile_link(out: str, common: list[str], file_flags: dict[str, list[str]], verbose: bool = False,
+                  link_extra: list[str] | None = None) -> None:
     """Each source to an object (in parallel, so a source can carry flags of its own), then one link."""
     import concurrent.futures
     import tempfile
@@ -58,7 +59,8 @@ def _compile_link(out: str, common: list[str], file_flags: dict[str, list[str]],
         jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "8"))))
         with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
             objs = list(ex.map(one, SOURCES))
-        subprocess.check_call([_hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out] + objs, cwd=CSRC)
+        subprocess.check_call([_hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out] + objs + (link_extra or []),
+                              cwd=CSRC)
 
 
 def build_lib(force: bool = False, verbose: bool = False) -> str:
@@ -110,6 +112,16 @@ def build_tools(force: bool = False) -> list[str]:
                                "-Wno-unused-result", src, "-o", so + ".tmp"])
         os.replace(so + ".tmp", so)
     out.append(so)
+    # tools/libkfec_arithfree.so: the shipped sources with every GF multiply-accumulate of the MAC and syndrome
+    # kernels replaced by a plain XOR of the shard granules (no table reads) -- the same grids (XCD spans), loads and
+    # stores, wrong results.  bench.py times its encode / decode in the same run as the ceiling of the product's own
+    # access pattern (measurement only; -Bsymbolic: its C ABI binds to itself when both libraries are loaded)
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    af = os.path.join(ROOT, "tools", "libkfec_arithfree.so")
+    if force or _stale(af, deps):
+        _compile_link(af + ".tmp", ["-DKFEC_MAC_XORONLY=1", "-DKFEC_SYN_XORONLY=2"], FILE_FLAGS, link_extra=["-Wl,-Bsymbolic"])
+        os.replace(af + ".tmp", af)
+    out.append(af)
     # tools/ceiling: the XOR-only HBM calibration kernels, also the FETCH_SIZE / WRITE_SIZE
     # calibration target of tools/gpu_profile_all.sh, so it must exist in the tree that travels to the box
     src = os.path.join(ROOT, "tools", "ceiling.hip")

@@ -66,6 +66,11 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #endif
 #ifndef KFEC_SYN_XORONLY
 #define KFEC_SYN_XORONLY 0  // ablation (timing only, wrong results): the syndrome MACs as plain XORs, same loads / stores
+                            // (1: the E / C table reads kept; 2: no table reads -- the arithmetic-free ceiling build)
+#endif
+#ifndef KFEC_MAC_XORONLY
+#define KFEC_MAC_XORONLY 0  // ablation (timing only, wrong results): mac_kernel's MACs as plain XORs of the shard granules,
+                            // no table reads -- same grid, loads and stores (tools/libkfec_arithfree.so: bench.py's ceiling)
 #endif
 #ifndef KFEC_SYN_TPRE
 #define KFEC_SYN_TPRE 1  // syn_loop: the next shard's E tables loaded into SGPRs one shard ahead (0: at use; A/B knob)
@@ -1358,7 +1363,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 const uint32_t s1 = (xv >> 3) & 0x07070707u;
                 const uint32_t s2 = (xv >> 6) & 0x03030303u;
 #pragma unroll
-                for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+                for (int r = 0; r < MT; ++r) acc[r][w] = KFEC_MAC_XORONLY ? acc[r][w] ^ xv : perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
             }
         };
         // PD shards in flight.  Every load is unconditional (past the end it re-reads the last shard, a
@@ -1394,7 +1399,8 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                         const uint32_t s1 = (xv >> 3) & 0x07070707u;
                         const uint32_t s2 = (xv >> 6) & 0x03030303u;
 #pragma unroll
-                        for (int r = 0; r < MT; ++r) acc[r][w] = perm_mac(acc[r][w], tt[u] + 5 * r, s0, s1, s2);
+                        for (int r = 0; r < MT; ++r)
+                            acc[r][w] = KFEC_MAC_XORONLY ? acc[r][w] ^ xv : perm_mac(acc[r][w], tt[u] + 5 * r, s0, s1, s2);
                     }
                 }
 #pragma unroll
@@ -1564,7 +1570,8 @@ __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][G
 #pragma unroll
             for (int r = 0; r < RT; ++r)
                 if ((ROWS >> r) & 1u)
-                    acc[r][w] = KFEC_SYN_XORONLY ? acc[r][w] ^ xv ^ t[5 * r] : perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
+                    acc[r][w] = KFEC_SYN_XORONLY == 2 ? acc[r][w] ^ xv
+                                : KFEC_SYN_XORONLY ? acc[r][w] ^ xv ^ t[5 * r] : perm_mac(acc[r][w], t + 5 * r, s0, s1, s2);
         }
     };
     // PD shards in flight, every load unconditional (see mac_kernel)
@@ -1612,7 +1619,7 @@ __device__ __forceinline__ void syn_final(const SynArgs &a, const uint32_t (&acc
                 for (int r = 0; r < RT; ++r) {
                     if (!((ROWS >> r) & 1u)) continue;  // (C[u][r] = 0 for a row no lane of the wave uses)
                     const uint32_t yv = acc[r][w];
-                    v = KFEC_SYN_XORONLY ? v ^ yv ^ t[5 * r]
+                    v = KFEC_SYN_XORONLY == 2 ? v ^ yv : KFEC_SYN_XORONLY ? v ^ yv ^ t[5 * r]
                                          : perm_mac(v, t + 5 * r, yv & 0x07070707u, (yv >> 3) & 0x07070707u, (yv >> 6) & 0x03030303u);
                 }
                 o[w] = v;

@@ -85,9 +85,11 @@ def test_bench_eight_ranks_match_single_rank():
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    common = ["--config", "20:3", "--no-cpu", "--steps", "2", "--warmup", "1"]
-    eight = _run([sys.executable, "bench.py", "--gpus", "8", "--groups", "2048"] + common, parts=8, timeout=300)
-    one = _run([sys.executable, "bench.py", "--gpus", "1", "--groups", "16384"] + common, parts=8)
+    common = ["--config", "20:3", "--steps", "2", "--warmup", "1"]
+    # the CPU leg runs at N > 1 too (rank 0, after every rank's GPU work): a small sample here
+    eight = _run([sys.executable, "bench.py", "--gpus", "8", "--groups", "2048", "--cpu-seconds", "1",
+                  "--cpu-groups", "1024"] + common, parts=8, timeout=300)
+    one = _run([sys.executable, "bench.py", "--gpus", "1", "--groups", "16384", "--no-cpu"] + common, parts=8)
     assert eight["verified_bit_exact"] and one["verified_bit_exact"]
     assert eight["config"]["ranks"] == 8 and eight["n_gpus"] == min(8, torch.cuda.device_count())
     assert eight["config"]["global_groups"] == one["config"]["global_groups"] == 16384
@@ -99,6 +101,14 @@ def test_bench_eight_ranks_match_single_rank():
     assert all(r["encode_ms"] > 0 and r["decode_ms"] > 0 and r["groups"] == 2048 for r in pr)
     assert eight["multi_rank"]["devices"] == eight["n_gpus"]
     assert 0 < eight["multi_rank"]["scaling_efficiency"] <= 1.5
+    # every rank measured its own GPU's ceilings and reports its own fractions (north_star: per-GPU roofline)
+    for r in pr:
+        assert 0 < r["frac"] < 1.5 and r["read_ceiling"] > 0 and r["mix_ceiling"] > 0
+        assert r["frac_of_ceiling"] > 0 and r["frac_of_mix_ceiling"] > 0
+    # the reference CPU path in the same run, at N > 1 as at N = 1
+    cb = eight["cpu_baseline"]
+    assert cb and "error" not in cb, cb
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("reference", "port")
 
 
 def test_bench_refuses_more_ranks_than_gpus():
