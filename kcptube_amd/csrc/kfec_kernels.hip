@@ -1001,7 +1001,7 @@ __device__ __forceinline__ void block_chunk_tile(uint32_t b, uint32_t tiles, uin
     }
     const uint32_t k = b >> 3;
     tile = k % tiles;
-    chunk = (k / tiles) * 8 + (b & 7);
+    chunk = xcd_tile_chunk(k / tiles, b & 7, gridDim.x / tiles);
 }
 
 // expand coefficients of shards [c0, c0+nj) for group slots [0, ng) into LDS entries
@@ -1919,7 +1919,7 @@ static int run_mac(MacArgs a, hipStream_t s)
     const size_t lds = (DEC && KFEC_DEC_TTAB && MT == 8) ? kTBytes + kDecGfBytes + (size_t)a.gmax * a.JC * kDecEntry
                                                          : (size_t)a.gmax * a.JC * L::ENTRY;
     const uint32_t chunks = (a.total + kMacBlock - 1) / kMacBlock;
-    const uint32_t nb = a.tiles > 1 ? ((chunks + 7) & ~7u) * a.tiles : xcd_grid(chunks);
+    const uint32_t nb = a.tiles > 1 ? xcd_tile_chunks(chunks) * a.tiles : xcd_grid(chunks);
     hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -220,6 +220,8 @@ CASES = [
     (9, 12, 1024, 1024, 50, None, "MT=3, K=9: two burst trips and a 1-shard tail, random erasures"),
     (10, 13, 1400, 1400, 3001, None, "516 chunks: XCD span order (KFEC_XCD_ORDER) with a padded last run, random"),
     (8, 12, 256, 256, 16411, 4, "513 chunks: XCD span order, one chunk past the threshold, MT=4"),
+    (12, 24, 256, 256, 16400, 12, "R=12, 2 row tiles over 513 chunks: tile XCD spans (KFEC_XCD_TILE_SPAN), padded"),
+    (30, 50, 512, 512, 8200, None, "R=20, 3 row tiles over 513 chunks, random erasures: tile spans, T-table decode"),
 ]
 
 
