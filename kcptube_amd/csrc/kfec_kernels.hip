@@ -103,6 +103,9 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #define KFEC_SYN_ROWMASK 1  // listed syndrome decode: 0 every parity row, 1 only the rows the group uses,
                             // 2 as 1 but single-row groups run a two-row variant (A/B knob)
 #endif
+#ifndef KFEC_PREP_SYN_T
+#define KFEC_PREP_SYN_T 1  // decode_prep_perm's syndrome-record form as its own instantiation (0: runtime flag; A/B knob)
+#endif
 #ifndef KFEC_MINW
 #define KFEC_MINW 1  // __launch_bounds__ minimum waves per SIMD of the MAC kernels
 #endif
@@ -487,7 +490,9 @@ __device__ __forceinline__ uint32_t pm_apply(uint32_t acc, const uint32_t *t, ui
 // perm MAC instead of log/antilog lookups.  A row of [S | I] is one dword each for S and I (MAXM <= 4
 // bytes); Gauss-Jordan normalises and eliminates whole rows with one perm MAC per dword; the coefficient
 // product runs over dwords of the parity rows with the MAXM^2 tables of Sinv held in VGPRs.
-template <int MAXM>
+// SYN: the syndrome-form records only (a compile-time branch: without the coefficient-form path's tables the
+// kernel needs far fewer registers -- 145 -> fewer VGPRs at MAXM = 3 -- and more groups are in flight per SIMD)
+template <int MAXM, bool SYN = false>
 __global__ void __launch_bounds__(kBlock) decode_prep_perm(PrepArgs a)
 {
     static_assert(MAXM >= 1 && MAXM <= 4, "rows are packed into one dword");
@@ -562,7 +567,7 @@ __global__ void __launch_bounds__(kBlock) decode_prep_perm(PrepArgs a)
             write_empty(a, g, 2);
             continue;
         }
-        if (a.syn) {
+        if (SYN || a.syn) {
             write_syn<MAXM>(a, g, m, M, P, w, [&](int u, int t) { return (Iv[u] >> (8 * t)) & 0xFFu; });
             continue;
         }
@@ -2098,7 +2103,14 @@ int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N,
         const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((G + kBlock - 1) / kBlock,
                                                                                 (size_t)std::max(di.cus, 1) * 64));
         const size_t lds4 = 768 + (size_t)R * (((size_t)K + 3) & ~size_t(3));
-        if (mmax == 1) hipLaunchKernelGGL((decode_prep_perm<1>), dim3(blocks), dim3(kBlock), lds4, s, p);
+        if (syn && KFEC_PREP_SYN_T) {
+            if (mmax == 1) hipLaunchKernelGGL((decode_prep_perm<1, true>), dim3(blocks), dim3(kBlock), lds4, s, p);
+            else if (mmax == 2) hipLaunchKernelGGL((decode_prep_perm<2, true>), dim3(blocks), dim3(kBlock), lds4, s, p);
+            else if (mmax == 3) hipLaunchKernelGGL((decode_prep_perm<3, true>), dim3(blocks), dim3(kBlock), lds4, s, p);
+            else if (mmax == 4) hipLaunchKernelGGL((decode_prep_perm<4, true>), dim3(blocks), dim3(kBlock), lds4, s, p);
+            else hipLaunchKernelGGL((decode_prep_small<8>), dim3(blocks), dim3(kBlock), lds, s, p);
+        }
+        else if (mmax == 1) hipLaunchKernelGGL((decode_prep_perm<1>), dim3(blocks), dim3(kBlock), lds4, s, p);
         else if (mmax == 2) hipLaunchKernelGGL((decode_prep_perm<2>), dim3(blocks), dim3(kBlock), lds4, s, p);
         else if (mmax == 3) hipLaunchKernelGGL((decode_prep_perm<3>), dim3(blocks), dim3(kBlock), lds4, s, p);
         else if (mmax == 4) hipLaunchKernelGGL((decode_prep_perm<4>), dim3(blocks), dim3(kBlock), lds4, s, p);
