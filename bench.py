@@ -193,6 +193,7 @@ class ArithFree:
         path = os.path.join(ROOT, "tools", "libkfec_arithfree.so")
         self.lib = ctypes.CDLL(path) if os.path.exists(path) else None
         self.ctx = ctypes.c_void_p()
+        self.last = {}
         if not self.lib:
             return
         vp, sz = ctypes.c_void_p, ctypes.c_size_t
@@ -205,19 +206,36 @@ class ArithFree:
         if self.lib.kfec_create(K, N, ctypes.byref(self.ctx)) != 0:
             self.lib = None
 
+    # occupancy caps tried (KFEC_AF_WAVES: at most n waves per SIMD, by LDS padding; None = the kernel's own): without
+    # its GF arithmetic the kernel needs fewer registers and runs more waves than the product, which can be slower
+    CAPS = (None, 4, 3, 2)
+
+    def _best(self, torch, launch):
+        times = {}
+        for cap in self.CAPS:
+            if cap is None:
+                os.environ.pop("KFEC_AF_WAVES", None)
+            else:
+                os.environ["KFEC_AF_WAVES"] = str(cap)
+            times[cap] = best_ms(torch, launch, reps=3)
+        os.environ.pop("KFEC_AF_WAVES", None)
+        ok = {k: v for k, v in times.items() if v}
+        self.last = {("own" if k is None else f"{k}w"): round(v, 4) for k, v in ok.items()}
+        return min(ok.values()) if ok else None
+
     def encode_ms(self, torch, data, parity, B):
         if not self.lib:
             return None
         G, _, pitch = data.shape
-        return best_ms(torch, lambda st: self.lib.kfec_encode_batch(self.ctx, G, B, pitch, data.data_ptr(),
-                                                                    parity.data_ptr(), st))
+        return self._best(torch, lambda st: self.lib.kfec_encode_batch(self.ctx, G, B, pitch, data.data_ptr(),
+                                                                       parity.data_ptr(), st))
 
     def decode_ms(self, torch, data, parity, present, out, out_idx, status, B, dev):
         if not self.lib:
             return None
         G, _, pitch = data.shape
         ws = torch.empty(max(self.lib.kfec_decode_workspace_size(self.ctx, G), 16), dtype=torch.uint8, device=dev)
-        return best_ms(torch, lambda st: self.lib.kfec_decode_batch(
+        return self._best(torch, lambda st: self.lib.kfec_decode_batch(
             self.ctx, G, B, pitch, data.data_ptr(), parity.data_ptr(), present.data_ptr(), out.data_ptr(),
             out_idx.data_ptr(), status.data_ptr(), ws.data_ptr(), st))
 
@@ -242,6 +260,11 @@ class Calib:
             self.lib.calib_issue_instructions.restype = ctypes.c_uint64
             self.lib.calib_mix.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                            ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+            self.has_occ = hasattr(self.lib, "calib_mix_occ")
+            if self.has_occ:
+                self.lib.calib_mix_occ.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                                   ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+        self.mix_last = {}
 
     def _time(self, torch, launch, reps=5):
         return best_ms(torch, launch, reps)
@@ -266,9 +289,16 @@ class Calib:
         if groups <= 0 or r16 <= 0:
             return None
         sink = torch.zeros(16, dtype=torch.int32, device=src.device)
-        ms = self._time(torch, lambda st: self.lib.calib_mix(src.data_ptr(), dst.data_ptr(), groups, r16, w16,
-                                                            sink.data_ptr(), st))
-        return None if ms is None else groups * (r16 + w16) / (ms * 1e-3) / 1e9
+        runs = {"own": self._time(torch, lambda st: self.lib.calib_mix(src.data_ptr(), dst.data_ptr(), groups, r16, w16,
+                                                                      sink.data_ptr(), st))}
+        # also at 4 / 3 / 2 workgroups (waves) per SIMD, LDS-capped: fewer, longer streams, as the product kernels run
+        for n in ((4, 3, 2) if self.has_occ else ()):
+            pad = 160 * 1024 // (n + 1) + 64
+            runs[f"{n}w"] = self._time(torch, lambda st, pad=pad: self.lib.calib_mix_occ(
+                src.data_ptr(), dst.data_ptr(), groups, r16, w16, pad, sink.data_ptr(), st), reps=3)
+        ok = {k: v for k, v in runs.items() if v}
+        self.mix_last = {k: round(groups * (r16 + w16) / (v * 1e-3) / 1e9, 1) for k, v in ok.items()}
+        return max(self.mix_last.values()) if ok else None
 
     def gfmac_ceiling(self, torch, dev, cus):
         """Issue bound of the perm MAC on this box, byte-MACs/s: every SIMD issuing nothing but the
@@ -572,6 +602,7 @@ def main():
                                  "arithfree" if (af_rate or 0) >= (mix_calib or 0) else "calib_mix"),
             "mix_ceiling_calib": round(mix_calib, 1) if mix_calib else None,
             "arithfree_ms": round(af_ms, 4) if af_ms else None,
+            "arithfree_ms_by_occupancy": af.last, "mix_calib_GBps_by_occupancy": calib.mix_last,
             "arithfree_GBps": round(af_rate, 1) if af_rate else None,
             "mix_ceiling_bytes_per_group": [mix_r, round(mix_w, 1)],
             "frac_of_mix_ceiling": round(achieved / mix_ceiling, 4) if mix_ceiling else None}

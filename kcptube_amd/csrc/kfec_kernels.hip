@@ -1917,12 +1917,29 @@ static int pick_vec_mac(size_t pitch, size_t B, std::initializer_list<const void
 static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
 
 
+#if KFEC_MAC_XORONLY || KFEC_SYN_XORONLY
+// The arithmetic-free ceiling build only (tools/libkfec_arithfree.so): KFEC_AF_WAVES = n caps a launch at n 256-lane
+// workgroups (n waves) per SIMD by padding its LDS, so bench.py can time the access pattern at the product's own
+// occupancy too -- without its GF arithmetic the kernel needs fewer registers and would otherwise run more waves
+// than the product (20:3 encode: 74 VGPRs against 129), which measured slower than the product itself.
+static size_t af_lds(size_t lds)
+{
+    const char *e = std::getenv("KFEC_AF_WAVES");
+    const long n = e ? std::strtol(e, nullptr, 10) : 0;
+    if (n < 2) return lds;
+    const size_t need = (size_t)160 * 1024 / (size_t)(n + 1) + 64;  // > 1/(n+1) of the CU's 160 KiB
+    return std::max(lds, std::min<size_t>(need, 64 * 1024));
+}
+#else
+static size_t af_lds(size_t lds) { return lds; }
+#endif
+
 template <int VEC, int MT, bool DEC, int PDX = 0>
 static int run_mac(MacArgs a, hipStream_t s)
 {
     using L = MacLayout<MT>;
-    const size_t lds = (DEC && KFEC_DEC_TTAB && MT == 8) ? kTBytes + kDecGfBytes + (size_t)a.gmax * a.JC * kDecEntry
-                                                         : (size_t)a.gmax * a.JC * L::ENTRY;
+    const size_t lds = af_lds((DEC && KFEC_DEC_TTAB && MT == 8) ? kTBytes + kDecGfBytes + (size_t)a.gmax * a.JC * kDecEntry
+                                                                : (size_t)a.gmax * a.JC * L::ENTRY);
     const uint32_t chunks = (a.total + kMacBlock - 1) / kMacBlock;
     const uint32_t nb = a.tiles > 1 ? xcd_tile_chunks(chunks) * a.tiles : xcd_grid(chunks);
     hipLaunchKernelGGL((mac_kernel<VEC, MT, DEC, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), lds, s, a);
@@ -1994,7 +2011,7 @@ template <int VEC, int RT, int PDX = 0>
 static int run_syn(SynArgs a, size_t lds, int cus, hipStream_t s)
 {
     const uint32_t nb = xcd_grid((a.total + kMacBlock - 1) / kMacBlock);
-    hipLaunchKernelGGL((syn_kernel<VEC, RT, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), lds, s, a);
+    hipLaunchKernelGGL((syn_kernel<VEC, RT, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), af_lds(lds), s, a);
     if (!a.list_count) return hipGetLastError() == hipSuccess ? 0 : -3;  // dense only
     // the listed shape: persistent, ~8 workgroups per CU, at most one wave per (group, 64 columns) task
     const uint64_t tasks = (uint64_t)a.G * (a.cols_pad / 64);

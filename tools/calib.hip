@@ -104,6 +104,18 @@ int calib_mix(const void *src, void *dst, size_t groups, size_t rbytes, size_t w
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// calib_mix with `lds_pad` bytes of (unused) LDS per workgroup: caps the workgroups -- waves -- per SIMD, so the ceiling
+// is also measured at the fewer, longer streams per SIMD the product kernels run at (bench.py takes the best)
+int calib_mix_occ(const void *src, void *dst, size_t groups, size_t rbytes, size_t wbytes, size_t lds_pad, uint32_t *sink,
+                  void *stream)
+{
+    if (groups == 0 || groups > 0x7FFFFFFFu || rbytes < 16 || rbytes % 16 || wbytes % 16 || lds_pad > 64 * 1024) return -1;
+    hipLaunchKernelGGL(mix_stream, dim3((uint32_t)groups), dim3(256), lds_pad, (hipStream_t)stream,
+                       static_cast<const uint8_t *>(src), static_cast<uint8_t *>(dst), (uint32_t)(rbytes / 16),
+                       (uint32_t)(wbytes / 16), sink);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 // bytes actually read by calib_read for a buffer of `bytes`
 size_t calib_read_bytes(size_t bytes) { return bytes / (4 * 256 * 16) * (4 * 256 * 16); }
 

@@ -13,7 +13,7 @@ prof = os.path.join(root, "profiles")
 rnd = os.path.join(go, "round")
 for name in ("bench_203.json", "bench_103dec.json", "bench_20055.json", "bench_203loss1.json", "wire.json",
              "wire_ragged.json", "seal.json", "pipeline_threads.json", "latency.json", "gtest.log", "smoke.log",
-             "box.txt"):
+             "box.txt", "e2e.json"):
     src = os.path.join(rnd, name)
     if os.path.exists(src):
         # (the round pass's latency line goes beside the curated <tag>_latency.json, never over it)

@@ -22,4 +22,5 @@ KFEC_WORKER=0 timeout -k 10 120 ./tools/latency_bench > $out/latency_launch.json
 timeout -k 10 120 ./tools/side_effects 400 > $out/side_effects.jsonl || exit 1
 timeout -k 10 300 python tools/concurrent_bench.py > $out/concurrent.json || exit 1
 for mode in none chacha20; do for G in 16 256 4096; do F=$(( G >= 4096 ? 5 : 33 )); PB_SEAL=$mode timeout -k 10 120 ./tools/pipeline_bench 20 23 1440 $G $F 3 1 || exit 1; done; done > $out/pipeline_sealed.jsonl
+timeout -k 10 600 python tools/e2e.py > $out/e2e.json 2> $out/e2e.err || { tail $out/e2e.err; exit 1; }
 echo round-done
