@@ -48,7 +48,8 @@ trf = json.load(open(trf_path)) if os.path.exists(trf_path) else {}
 dominant = re.compile(r"syn_kernel<\d+, \d+(, \d+)?>" if args.config.endswith("dec")
                       else r"mac_kernel<\d+, \d+, false(, \d+)?>")
 for k, d in summary.items():
-    if dominant.search(k) and "hbm_bytes_per_launch" in d:
+    # (the product's kernel, not the arithmetic-free ceiling build's namesake, kfec_af::, timed in the same run)
+    if dominant.search(k) and "kfec_af::" not in k and "hbm_bytes_per_launch" in d:
         key = f"{args.config}@p{args.pitch}" if args.pitch else args.config
         trf[key] = {"groups": args.groups, "kernel": k, "hbm_bytes_per_launch": int(d["hbm_bytes_per_launch"]),
                     "source": f"profiles/{args.tag}_pmc.json"}
