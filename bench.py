@@ -406,6 +406,12 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but the launcher formed a world of {world} ranks", file=sys.stderr)
         sys.exit(2)
 
+    # stdout carries exactly one line, rank 0's JSON: everything else the process writes to fd 1 -- gloo's
+    # "[Gloo] Rank r is connected to n peer ranks" at rendezvous, runtime chatter -- goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
@@ -677,7 +683,7 @@ def main():
         except Exception as e:  # the GPU number stands on its own
             result["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     if world > 1:
         dist.barrier()  # (the other ranks wait for rank 0's CPU leg instead of tearing the group down under it)
         dist.destroy_process_group()

@@ -39,6 +39,10 @@ def _run(cmd, parts, rehearsal=True, timeout=240):
                KFEC_BENCH_REHEARSAL="1" if rehearsal else "0")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, f"rc={r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    # the contract: rank 0 prints ONE JSON line and nothing else reaches stdout (gloo's rendezvous chatter, the
+    # runtime's messages go to stderr) -- under torch.distributed.run too
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
     return _last_json(r.stdout)
 
 
