@@ -103,6 +103,17 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #define KFEC_SYN_ROWMASK 1  // listed syndrome decode: 0 every parity row, 1 only the rows the group uses,
                             // 2 as 1 but single-row groups run a two-row variant (A/B knob)
 #endif
+#ifndef KFEC_MAC_PAIR
+#define KFEC_MAC_PAIR 1  // encode MAC, 8-row tiles (R > 8): two shards per row step, acc ^= c_a x_a ^ c_b x_b as three
+                         // 3-input XORs over the six permutes (instead of 2 x (v_bitop3 + v_xor)), rows outer;
+                         // 200:55 encode 151.1 -> 133.8 ms, 40:20 13.24 -> 11.98 ms (profiles/r06_mac_pair_ab.txt)
+#endif
+#ifndef KFEC_MAC_PAIR_SMALL
+#define KFEC_MAC_PAIR_SMALL 0  // the pairing in the encode burst loop (3..4-row tiles) (A/B knob)
+#endif
+#ifndef KFEC_DEC_PAIR
+#define KFEC_DEC_PAIR 0  // the same pairing in the T-table decode MAC (8-row tiles) (A/B knob)
+#endif
 #ifndef KFEC_PREP_SYN_T
 #define KFEC_PREP_SYN_T 1  // decode_prep_perm's syndrome-record form as its own instantiation (0: runtime flag; A/B knob)
 #endif
@@ -1395,6 +1406,28 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                         tt[u][4 * i] = q.x; tt[u][4 * i + 1] = q.y; tt[u][4 * i + 2] = q.z; tt[u][4 * i + 3] = q.w;
                     }
                 }
+                if constexpr (KFEC_MAC_PAIR_SMALL && !KFEC_MAC_XORONLY && PD % 2 == 0) {
+#pragma unroll
+                    for (int u = 0; u < PD; u += 2) {
+#pragma unroll
+                        for (int w = 0; w < W; ++w) {
+                            const uint32_t xa = x[u].d[w], xb = x[u + 1].d[w];
+                            const uint32_t sa0 = xa & 0x07070707u, sa1 = (xa >> 3) & 0x07070707u, sa2 = (xa >> 6) & 0x03030303u;
+                            const uint32_t sb0 = xb & 0x07070707u, sb1 = (xb >> 3) & 0x07070707u, sb2 = (xb >> 6) & 0x03030303u;
+#pragma unroll
+                            for (int r = 0; r < MT; ++r) {
+                                const uint32_t *ta = tt[u] + 5 * r, *tb = tt[u + 1] + 5 * r;
+                                const uint32_t a0 = __builtin_amdgcn_perm(ta[1], ta[0], sa0);
+                                const uint32_t a1 = __builtin_amdgcn_perm(ta[3], ta[2], sa1);
+                                const uint32_t a2 = __builtin_amdgcn_perm(ta[4], ta[4], sa2);
+                                const uint32_t b0 = __builtin_amdgcn_perm(tb[1], tb[0], sb0);
+                                const uint32_t b1 = __builtin_amdgcn_perm(tb[3], tb[2], sb1);
+                                const uint32_t b2 = __builtin_amdgcn_perm(tb[4], tb[4], sb2);
+                                acc[r][w] = xor3(xor3(xor3(acc[r][w], a0, a1), a2, b0), b1, b2);
+                            }
+                        }
+                    }
+                } else {
 #pragma unroll
                 for (int u = 0; u < PD; ++u) {
 #pragma unroll
@@ -1406,6 +1439,82 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
 #pragma unroll
                         for (int r = 0; r < MT; ++r)
                             acc[r][w] = KFEC_MAC_XORONLY ? acc[r][w] ^ xv : perm_mac(acc[r][w], tt[u] + 5 * r, s0, s1, s2);
+                    }
+                }
+                }
+#pragma unroll
+                for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
+            } else if constexpr (!DEC && MT == 8 && VEC >= 32 && PD == 2 && KFEC_MAC_PAIR) {
+                // the two shards of the trip together, row by row: 6 permutes and three 3-input XORs per row and dword
+                // (one VALU op fewer than two separate MACs); the selectors of both granules stay live across the
+                // rows, each row's two tables are read from LDS just before use (not all 8 rows' at once)
+                uint32_t sa[W][3], sb[W][3];
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint32_t xa = x[0].d[w], xb = x[1].d[w];
+                    sa[w][0] = xa & 0x07070707u; sa[w][1] = (xa >> 3) & 0x07070707u; sa[w][2] = (xa >> 6) & 0x03030303u;
+                    sb[w][0] = xb & 0x07070707u; sb[w][1] = (xb >> 3) & 0x07070707u; sb[w][2] = (xb >> 6) & 0x03030303u;
+                }
+                const uint32_t *tA = reinterpret_cast<const uint32_t *>(ent0 + jb * ENT + 16);
+                const uint32_t *tB = reinterpret_cast<const uint32_t *>(ent0 + (jb + 1) * ENT + 16);
+#pragma unroll
+                for (int r = 0; r < MT; ++r) {
+                    uint32_t ta[5], tb[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) {
+                        ta[i] = tA[5 * r + i];
+                        tb[i] = tB[5 * r + i];
+                    }
+#pragma unroll
+                    for (int w = 0; w < W; ++w) {
+                        const uint32_t a0 = __builtin_amdgcn_perm(ta[1], ta[0], sa[w][0]);
+                        const uint32_t a1 = __builtin_amdgcn_perm(ta[3], ta[2], sa[w][1]);
+                        const uint32_t a2 = __builtin_amdgcn_perm(ta[4], ta[4], sa[w][2]);
+                        const uint32_t b0 = __builtin_amdgcn_perm(tb[1], tb[0], sb[w][0]);
+                        const uint32_t b1 = __builtin_amdgcn_perm(tb[3], tb[2], sb[w][1]);
+                        const uint32_t b2 = __builtin_amdgcn_perm(tb[4], tb[4], sb[w][2]);
+                        acc[r][w] = xor3(xor3(xor3(acc[r][w], a0, a1), a2, b0), b1, b2);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
+            } else if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT == 8 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR) {
+                // the decode's form of the same pairing: each row's two tables are read from T at the addresses the
+                // two entries hold (dec_expand added T's base)
+                typedef const volatile __attribute__((address_space(3))) uint16_t lds_u16;
+                typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+                typedef const __attribute__((address_space(3))) v4u lds_u4;
+                typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+                const lds_u16 *qa = (const lds_u16 *)(ent0 + jb * ENT + 8);
+                const lds_u16 *qb = (const lds_u16 *)(ent0 + (jb + 1) * ENT + 8);
+                uint32_t oa[MT], ob[MT];
+#pragma unroll
+                for (int r = 0; r < MT; ++r) {
+                    oa[r] = qa[r];
+                    ob[r] = qb[r];
+                }
+                uint32_t sa[W][3], sb[W][3];
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint32_t xa = x[0].d[w], xb = x[1].d[w];
+                    sa[w][0] = xa & 0x07070707u; sa[w][1] = (xa >> 3) & 0x07070707u; sa[w][2] = (xa >> 6) & 0x03030303u;
+                    sb[w][0] = xb & 0x07070707u; sb[w][1] = (xb >> 3) & 0x07070707u; sb[w][2] = (xb >> 6) & 0x03030303u;
+                }
+#pragma unroll
+                for (int r = 0; r < MT; ++r) {
+                    const v4u qa4 = *(const lds_u4 *)(uintptr_t)oa[r];
+                    const v4u qb4 = *(const lds_u4 *)(uintptr_t)ob[r];
+                    const uint32_t ta4 = *(const lds_u32 *)(uintptr_t)(oa[r] + 16);
+                    const uint32_t tb4 = *(const lds_u32 *)(uintptr_t)(ob[r] + 16);
+#pragma unroll
+                    for (int w = 0; w < W; ++w) {
+                        const uint32_t a0 = __builtin_amdgcn_perm(qa4.y, qa4.x, sa[w][0]);
+                        const uint32_t a1 = __builtin_amdgcn_perm(qa4.w, qa4.z, sa[w][1]);
+                        const uint32_t a2 = __builtin_amdgcn_perm(ta4, ta4, sa[w][2]);
+                        const uint32_t b0 = __builtin_amdgcn_perm(qb4.y, qb4.x, sb[w][0]);
+                        const uint32_t b1 = __builtin_amdgcn_perm(qb4.w, qb4.z, sb[w][1]);
+                        const uint32_t b2 = __builtin_amdgcn_perm(tb4, tb4, sb[w][2]);
+                        acc[r][w] = xor3(xor3(xor3(acc[r][w], a0, a1), a2, b0), b1, b2);
                     }
                 }
 #pragma unroll
@@ -1426,6 +1535,8 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 }
             }
         }
+        if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT == 8 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR)
+            read_ofs(jb);  // (the paired loop read its offsets itself: the tail's MAC takes shard jb's)
 #pragma unroll
         for (int u = 0; u < PD; ++u)
             if (jb + u < nj) mac(x[u], jb + u);
