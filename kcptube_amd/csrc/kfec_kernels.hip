@@ -109,10 +109,12 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
                          // 200:55 encode 151.1 -> 133.8 ms, 40:20 13.24 -> 11.98 ms (profiles/r06_mac_pair_ab.txt)
 #endif
 #ifndef KFEC_MAC_PAIR_SMALL
-#define KFEC_MAC_PAIR_SMALL 0  // the pairing in the encode burst loop (3..4-row tiles) (A/B knob)
+#define KFEC_MAC_PAIR_SMALL 1  // the pairing in the encode burst loop (3..4-row tiles): 8:4 encode 3.39 -> 3.33 ms,
+                               // 20:3 and 10:3 unchanged (HBM-bound) (profiles/r06_pair_small_ab.txt)
 #endif
 #ifndef KFEC_DEC_PAIR
-#define KFEC_DEC_PAIR 0  // the same pairing in the T-table decode MAC (8-row tiles) (A/B knob)
+#define KFEC_DEC_PAIR 1  // the same pairing in the T-table decode MAC (8-row tiles): 200:55 decode 151.4 -> 137.5 ms,
+                         // 40:20 14.09 -> 13.30 ms, 20:20 15.50 -> 15.07 ms (profiles/r06_dec_pair_ab.txt)
 #endif
 #ifndef KFEC_PREP_SYN_T
 #define KFEC_PREP_SYN_T 1  // decode_prep_perm's syndrome-record form as its own instantiation (0: runtime flag; A/B knob)
@@ -2118,11 +2120,20 @@ static size_t syn_td(int rt)
     }
 }
 
+#ifndef KFEC_SYN_WAVES
+#define KFEC_SYN_WAVES 0  // syn_kernel capped at this many workgroups (= waves) per SIMD by padding its LDS (0: no cap)
+#endif
+static size_t syn_cap(size_t lds)
+{
+    if (KFEC_SYN_WAVES < 2) return lds;
+    return std::max(lds, std::min<size_t>((size_t)160 * 1024 / (KFEC_SYN_WAVES + 1) + 64, 64 * 1024));
+}
+
 template <int VEC, int RT, int PDX = 0>
 static int run_syn(SynArgs a, size_t lds, int cus, hipStream_t s)
 {
     const uint32_t nb = xcd_grid((a.total + kMacBlock - 1) / kMacBlock);
-    hipLaunchKernelGGL((syn_kernel<VEC, RT, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), af_lds(lds), s, a);
+    hipLaunchKernelGGL((syn_kernel<VEC, RT, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), af_lds(syn_cap(lds)), s, a);
     if (!a.list_count) return hipGetLastError() == hipSuccess ? 0 : -3;  // dense only
     // the listed shape: persistent, ~8 workgroups per CU, at most one wave per (group, 64 columns) task
     const uint64_t tasks = (uint64_t)a.G * (a.cols_pad / 64);
