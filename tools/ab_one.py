@@ -26,8 +26,10 @@ elif mode == "none":  # nothing lost
     c.erasure_masks(masks, 1, K, 0, 0)
 elif mode.startswith("iid:"):  # i.i.d. loss, ppm per shard
     c.erasure_masks(masks, 0x5EED0001, N, int(mode[4:]), 2)
-else:
+elif mode == "data":  # the first min(R, K) data shards of every group lost
     c.erasure_masks(masks, 1, K, min(R, K))
+else:
+    sys.exit(f"AB_ERASE={mode!r}: expected data, random, none or iid:<ppm>")
 s = torch.cuda.current_stream()
 e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
 enc, dec = [], []

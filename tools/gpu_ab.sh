@@ -46,7 +46,8 @@ if [ -n "$TESTS" ]; then
 fi
 libs=""; for v in ${VARIANTS:-base}; do libs="$libs $(lib_of "$v")"; done
 for s in $SHAPES; do
-  IFS=: read -r K N B G E P <<< "$s"
+  IFS=: read -r K N B G E P X <<< "$s"
+  if [ "$E" = iid ]; then E="iid:$P"; P=$X; fi  # (the erase field iid:<ppm> holds a colon itself)
   tag="${K}_${N}_${B}_${E:-data}${P:+_p$P}"
   AB_ERASE=${E:-data} AB_PITCH=${P:-0} timeout -k 10 $LIMIT python tools/ab.py $ROUNDS $libs -- $K $N $B $G > $out/ab_$tag.txt || { cat $out/ab_$tag.txt; exit 1; }
   echo "== $s"; cut -c1-160 $out/ab_$tag.txt
