@@ -75,6 +75,10 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
 #ifndef KFEC_SYN_TPRE
 #define KFEC_SYN_TPRE 1  // syn_loop: the next shard's E tables loaded into SGPRs one shard ahead (0: at use; A/B knob)
 #endif
+#ifndef KFEC_SYN_PAIR
+#define KFEC_SYN_PAIR 0  // syn_loop: two shards per row step, as KFEC_MAC_PAIR (RT <= 4): bit 0 syn_kernel, bit 1
+                         // syn_list_kernel (A/B knob)
+#endif
 #ifndef KFEC_PREP_FUSED
 #define KFEC_PREP_FUSED 1  // decode_prep_lagrange: denominators and numerators in one pass (0: two loops; A/B knob)
 #endif
@@ -1640,7 +1644,7 @@ __device__ __forceinline__ void syn_expand_one(const uint8_t *rec, uint32_t ur, 
 // A group that lost m data shards uses m parity rows: syn_list_kernel (one group per task, so the mask is
 // uniform) leaves out the rows its group does not use -- at ~1% loss mostly 2 of 3 (fec=20:3 listed decode
 // 1.41 -> 1.23 ms, profiles/r04_rowmask_ab.txt).
-template <int VEC, int RT, int PD, uint32_t ROWS = (1u << RT) - 1u>
+template <int VEC, int RT, int PD, uint32_t ROWS = (1u << RT) - 1u, bool PAIR = (KFEC_SYN_PAIR & 1) != 0>
 __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][Gran<VEC>::W], __amdgpu_buffer_rsrc_t rd,
                                          __amdgpu_buffer_rsrc_t rp, uint32_t drow, uint32_t prow, uint32_t used,
                                          uint64_t p0, const uint8_t *rec)
@@ -1697,6 +1701,50 @@ __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][G
 #pragma unroll
     for (int u = 0; u < PD; ++u) x[u] = bload<VEC>(rd, dofs(min((uint32_t)u, K - 1)));
     uint32_t jb = 0;
+    if constexpr (PAIR && KFEC_SYN_TPRE && !KFEC_SYN_XORONLY && PD % 2 == 0 && RT <= 4) {
+        // two shards per row step (mac_kernel's KFEC_MAC_PAIR): both shards' tables prefetched one pair ahead
+        uint32_t tm[5 * RT];
+        auto tload2 = [&](uint32_t j) {
+            tload(j);
+            const cu32 *tg = (const cu32 *)(a.etab + (size_t)min(j + 1, K - 1) * a.etab_rows * 5);
+#pragma unroll
+            for (int i = 0; i < 5 * RT; ++i) tm[i] = tg[i];
+        };
+        tload2(0);
+        for (; jb + PD <= K; jb += PD) {
+#pragma unroll
+            for (int u = 0; u < PD; u += 2) {
+                uint32_t ta[5 * RT], tb[5 * RT];
+#pragma unroll
+                for (int i = 0; i < 5 * RT; ++i) {
+                    ta[i] = tn[i];
+                    tb[i] = tm[i];
+                }
+                tload2(jb + u + 2);
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint32_t xa = x[u].d[w], xb = x[u + 1].d[w];
+                    const uint32_t sa0 = xa & 0x07070707u, sa1 = (xa >> 3) & 0x07070707u, sa2 = (xa >> 6) & 0x03030303u;
+                    const uint32_t sb0 = xb & 0x07070707u, sb1 = (xb >> 3) & 0x07070707u, sb2 = (xb >> 6) & 0x03030303u;
+#pragma unroll
+                    for (int r = 0; r < RT; ++r) {
+                        if (!((ROWS >> r) & 1u)) continue;
+                        const uint32_t *pa = ta + 5 * r, *pb = tb + 5 * r;
+                        const uint32_t a0 = __builtin_amdgcn_perm(pa[1], pa[0], sa0);
+                        const uint32_t a1 = __builtin_amdgcn_perm(pa[3], pa[2], sa1);
+                        const uint32_t a2 = __builtin_amdgcn_perm(pa[4], pa[4], sa2);
+                        const uint32_t b0 = __builtin_amdgcn_perm(pb[1], pb[0], sb0);
+                        const uint32_t b1 = __builtin_amdgcn_perm(pb[3], pb[2], sb1);
+                        const uint32_t b2 = __builtin_amdgcn_perm(pb[4], pb[4], sb2);
+                        acc[r][w] = xor3(xor3(xor3(acc[r][w], a0, a1), a2, b0), b1, b2);
+                    }
+                }
+                x[u] = bload<VEC>(rd, dofs(min(jb + u + PD, K - 1)));
+                x[u + 1] = bload<VEC>(rd, dofs(min(jb + u + 1 + PD, K - 1)));
+            }
+        }
+        tload(jb);  // the tail's single MACs take their tables through tn, shard jb first
+    } else
     for (; jb + PD <= K; jb += PD) {
         // (the encode's burst order, KFEC_MAC_BURST, measured slower here, also at 3 or 2 waves per SIMD:
         // profiles/r05_syn_burst_ab.txt)
@@ -1820,7 +1868,7 @@ __global__ void __launch_bounds__(kMacBlock) syn_list_kernel(SynArgs a)
                     (void *)(a.data + (uint64_t)g * a.K * a.pitch), (short)0, (int)(a.K * a.pitch), 0x00020000);
                 const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
                     (void *)(a.parity + (uint64_t)g * a.R * a.pitch), (short)0, (int)(a.R * a.pitch), 0x00020000);
-                syn_loop<VEC, RT, PD, ROWS>(a, acc, rd, rp, off, off, used, p0, rec);
+                syn_loop<VEC, RT, PD, ROWS, (KFEC_SYN_PAIR & 2) != 0>(a, acc, rd, rp, off, off, used, p0, rec);
             }
             // the tables were written by lanes of this wave: LDS operations of one wave complete in order, the
             // fence keeps the compiler from moving the reads above the writes
