@@ -301,9 +301,13 @@ class Calib:
         return max(self.mix_last.values()) if ok else None
 
     def gfmac_ceiling(self, torch, dev, cus):
-        """Issue bound of the perm MAC on this box, byte-MACs/s: every SIMD issuing nothing but the
-        3 v_perm_b32 + v_bitop3_b32 + v_xor_b32 that make 4 byte-MACs per lane, at the rates measured by
-        tools/calib.hip's instruction chains (8 waves per SIMD).  An upper bound for any kernel built on it."""
+        """Issue bound of the perm MAC on this box, byte-MACs/s: every SIMD issuing nothing but the permutes and
+        XORs of the fastest formulation the product uses, at the rates measured by tools/calib.hip's instruction
+        chains (8 waves per SIMD).  The 8-row MAC multiplies two shards per row step (KFEC_MAC_PAIR): 6 v_perm_b32 +
+        3 v_bitop3_b32 per 8 byte-MACs per lane, i.e. 3 + 1.5 per 4 -- the returned bound.  self.mac_last also keeps
+        the single-shard form's (3 v_perm_b32 + v_bitop3_b32 + v_xor_b32 per 4), which rounds 1-5 reported against.
+        An upper bound for any kernel built on these instructions."""
+        self.mac_last = {}
         if not self.lib:
             return None
         sink = torch.zeros(16, dtype=torch.int32, device=dev)
@@ -316,7 +320,9 @@ class Calib:
             # seconds per wave-instruction on one SIMD
             secs.append(ms * 1e-3 / (self.lib.calib_issue_instructions(blocks) / (4.0 * cus)))
         t_perm, t_bitop3, t_xor = secs
-        return 4 * 64 * 4 * cus / (3 * t_perm + t_bitop3 + t_xor)
+        self.mac_last = {"single": 4 * 64 * 4 * cus / (3 * t_perm + t_bitop3 + t_xor),
+                         "paired": 4 * 64 * 4 * cus / (3 * t_perm + 1.5 * t_bitop3)}
+        return self.mac_last["paired"]
 
 
 def device_ident(torch, dev, local_dev: int) -> str:
@@ -624,8 +630,11 @@ def main():
                      "decode_achieved": round(dec_mac, 0),
                      "decode_frac": round(dec_mac / ceil_mac, 4) if ceil_mac else None,
                      "hbm_achieved": round(achieved, 1), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "ceiling_kernel": "issue bound: 4 byte-MACs per lane per (3 v_perm_b32 + v_bitop3_b32 + "
-                                       "v_xor_b32) at the rates tools/calib.hip measures on this box"})
+                     "ceiling_kernel": "issue bound of the paired perm MAC: 8 byte-MACs per lane per (6 v_perm_b32 + "
+                                       "3 v_bitop3_b32) at the rates tools/calib.hip measures on this box",
+                     "issue_bound_single": round(calib.mac_last["single"], 0) if calib.mac_last else None,
+                     "frac_of_single_bound": (round(enc_mac / calib.mac_last["single"], 4)
+                                              if calib.mac_last else None)})
 
     # every rank's own timing, device and fractions, gathered after the timed region (per_rank in the JSON line)
     my_rec = {"rank": rank, "device": device_ident(torch, dev, local_dev), "name": torch.cuda.get_device_name(dev),

@@ -1450,7 +1450,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 }
 #pragma unroll
                 for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
-            } else if constexpr (!DEC && MT == 8 && VEC >= 32 && PD == 2 && KFEC_MAC_PAIR) {
+            } else if constexpr (!DEC && MT == 8 && VEC >= 32 && PD == 2 && KFEC_MAC_PAIR && !KFEC_MAC_XORONLY) {
                 // the two shards of the trip together, row by row: 6 permutes and three 3-input XORs per row and dword
                 // (one VALU op fewer than two separate MACs); the selectors of both granules stay live across the
                 // rows, each row's two tables are read from LDS just before use (not all 8 rows' at once)
@@ -1484,7 +1484,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 }
 #pragma unroll
                 for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
-            } else if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT == 8 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR) {
+            } else if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT == 8 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR && !KFEC_MAC_XORONLY) {
                 // the decode's form of the same pairing: each row's two tables are read from T at the addresses the
                 // two entries hold (dec_expand added T's base)
                 typedef const volatile __attribute__((address_space(3))) uint16_t lds_u16;
@@ -1541,7 +1541,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 }
             }
         }
-        if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT == 8 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR)
+        if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT == 8 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR && !KFEC_MAC_XORONLY)
             read_ofs(jb);  // (the paired loop read its offsets itself: the tail's MAC takes shard jb's)
 #pragma unroll
         for (int u = 0; u < PD; ++u)

@@ -25,6 +25,11 @@ for cfg, groups, ptag in (("20:3", 1 << 20, "203"), ("10:3dec", 1 << 20, "103dec
     if os.path.isdir(d):
         subprocess.check_call([sys.executable, os.path.join(root, "tools", "pmc_summary.py"), d, f"{tag}_{ptag}",
                                "--config", cfg, "--groups", str(groups)])
+        # the bench line the traced command printed (its HIP-event times, to set beside the trace's)
+        kl = os.path.join(d, "kt.log")
+        lines = [ln for ln in open(kl) if ln.startswith('{"metric"')] if os.path.exists(kl) else []
+        if lines:
+            open(os.path.join(prof, f"{tag}_bench_{ptag}_under_rocprof.json"), "w").write(lines[-1])
 for name in ("wire", "seal"):
     f = os.path.join(go, f"prof_{name}", "kt_kernel_stats.csv")
     if os.path.exists(f):
