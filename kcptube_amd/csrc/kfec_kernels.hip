@@ -992,7 +992,7 @@ __device__ __forceinline__ uint32_t gran_off(uint32_t col, uint32_t B)
 
 template <int MT>
 struct MacLayout {
-    static_assert(MT >= 1 && MT <= 8, "row tile");
+    static_assert(MT >= 1 && MT <= 16, "row tile");
     static constexpr int TBL_DW = ((5 * MT + 3) / 4) * 4;  // table dwords per (group, shard): 5 per row
     static constexpr int ENTRY = 16 + 4 * TBL_DW;          // + 8-byte share pointer, 8 pad
 };
@@ -1450,7 +1450,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 }
 #pragma unroll
                 for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
-            } else if constexpr (!DEC && MT == 8 && VEC >= 32 && PD == 2 && KFEC_MAC_PAIR && !KFEC_MAC_XORONLY) {
+            } else if constexpr (!DEC && MT >= 8 && VEC >= 32 && PD == 2 && KFEC_MAC_PAIR && !KFEC_MAC_XORONLY) {
                 // the two shards of the trip together, row by row: 6 permutes and three 3-input XORs per row and dword
                 // (one VALU op fewer than two separate MACs); the selectors of both granules stay live across the
                 // rows, each row's two tables are read from LDS just before use (not all 8 rows' at once)
@@ -2077,6 +2077,17 @@ static int pick_vec_mac(size_t pitch, size_t B, std::initializer_list<const void
 // granules amortise each table read over the most bytes).
 static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
 
+// The encode's row tile for 32-byte granules: for R > 8 the 8- or 10-row tile that computes fewer rows (ties: 10, fewer
+// tiles re-reading the data).  Both run at 3 waves per SIMD (152 / 167 VGPRs) at about the same cost per row, so the
+// rows a last partial tile wastes decide: 40:20 encode 11.86 -> 9.98 ms and 30:20 9.03 -> 7.78 ms with 10-row tiles,
+// 200:55 132.2 -> 140.4 ms (60 rows instead of 56); 11-row tiles need 175 VGPRs, 2 waves (profiles/r06_mt_tall_ab.txt)
+static int pick_mt_enc(int R)
+{
+    if (R <= 8) return pick_mt(R);
+    const int rows8 = (R + 7) / 8 * 8, rows10 = (R + 9) / 10 * 10;
+    return rows10 <= rows8 ? 10 : 8;
+}
+
 
 #if KFEC_MAC_XORONLY || KFEC_SYN_XORONLY
 // The arithmetic-free ceiling build only (tools/libkfec_arithfree.so): KFEC_AF_WAVES = n caps a launch at n 256-lane
@@ -2128,6 +2139,8 @@ static int dispatch_mac(int vec, int mt, MacArgs a, hipStream_t s)
         }
     }
     if (vec == 32) {
+        if constexpr (!DEC)
+            if (mt == 10) return run_mac<32, 10, false>(a, s);
         switch (mt) {
         case 1: return run_mac<32, 1, DEC>(a, s);
         case 2: return run_mac<32, 2, DEC>(a, s);
@@ -2152,6 +2165,7 @@ static int entry_bytes(int mt)
     case 2: return MacLayout<2>::ENTRY;
     case 3: return MacLayout<3>::ENTRY;
     case 4: return MacLayout<4>::ENTRY;
+    case 10: return MacLayout<10>::ENTRY;
     default: return MacLayout<8>::ENTRY;
     }
 }
@@ -2233,8 +2247,8 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     const int R = N - K;
     if (R == 0 || G == 0 || B == 0) return 0;
     int vec = pick_vec_mac(pitch, B, {d_data, d_parity});
-    const int mt = pick_mt(R);
     if (G <= kLatencyGroups && vec >= 4) vec = kLatencyVec;
+    const int mt = vec == 32 ? pick_mt_enc(R) : pick_mt(R);
     const int vb = vec >= 4 ? vec : 4;
     const size_t cols = (B + vb - 1) / vb;
     const int tiles = (R + mt - 1) / mt;

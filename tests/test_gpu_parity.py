@@ -221,7 +221,9 @@ CASES = [
     (10, 13, 1400, 1400, 3001, None, "516 chunks: XCD span order (KFEC_XCD_ORDER) with a padded last run, random"),
     (8, 12, 256, 256, 16411, 4, "513 chunks: XCD span order, one chunk past the threshold, MT=4"),
     (12, 24, 256, 256, 16400, 12, "R=12, 2 row tiles over 513 chunks: tile XCD spans (KFEC_XCD_TILE_SPAN), padded"),
-    (30, 50, 512, 512, 8200, None, "R=20, 3 row tiles over 513 chunks, random erasures: tile spans, T-table decode"),
+    (30, 50, 512, 512, 8200, None, "R=20, 2 encode row tiles of 10 over 513 chunks, random erasures: tile spans, T-table decode"),
+    (25, 50, 1440, 1440, 40, 25, "R=25 -> three 10-row encode tiles, the last computing 5 rows"),
+    (9, 18, 1440, 1440, 30, 9, "R=9 -> one 10-row encode tile with a slack row"),
 ]
 
 
