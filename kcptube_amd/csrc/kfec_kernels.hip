@@ -112,6 +112,11 @@ static constexpr int kMacBlock = KFEC_MAC_BLOCK;  // workgroup of the flattened 
                          // 3-input XORs over the six permutes (instead of 2 x (v_bitop3 + v_xor)), rows outer;
                          // 200:55 encode 151.1 -> 133.8 ms, 40:20 13.24 -> 11.98 ms (profiles/r06_mac_pair_ab.txt)
 #endif
+#ifndef KFEC_ENC_MT_MID
+#define KFEC_ENC_MT_MID 1  // encode R = 5..7 (32-byte granules): 0 an 8-row tile, 1 an R-row tile with the paired MAC, 2 an
+                           // R-row tile in the plain loop. 1: 20:5 9.30 -> 7.49 ms, 20:6 9.56 -> 8.50, 16:7 8.10 -> 7.86,
+                           // 10:6 5.33 -> 4.94 (2: 4.85 there, slower elsewhere) (profiles/r06_mt_mid_ab.txt)
+#endif
 #ifndef KFEC_MAC_PAIR_SMALL
 #define KFEC_MAC_PAIR_SMALL 1  // the pairing in the encode burst loop (3..4-row tiles): 8:4 encode 3.39 -> 3.33 ms,
                                // 20:3 and 10:3 unchanged (HBM-bound) (profiles/r06_pair_small_ab.txt)
@@ -1241,7 +1246,8 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     // shards in flight per lane (~64 B per lane); PDX: the latency shape (a handful of groups, often read
     // straight from pinned host memory) keeps many more loads in flight so the PCIe round trips overlap
     // (MT = 8, the VALU-bound tall tiles: 2, to keep 3 waves per SIMD)
-    constexpr int PD = PDX ? PDX : (VEC >= 32 ? (MT >= 8 ? 2 : KFEC_MAC_PD) : 2 * KFEC_PD);
+    constexpr bool PAIRED = !DEC && (MT >= 8 || (KFEC_ENC_MT_MID == 1 && MT >= 5));
+    constexpr int PD = PDX ? PDX : (VEC >= 32 ? (MT >= 8 || PAIRED ? 2 : KFEC_MAC_PD) : 2 * KFEC_PD);
     constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
 
@@ -1450,7 +1456,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 }
 #pragma unroll
                 for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
-            } else if constexpr (!DEC && MT >= 8 && VEC >= 32 && PD == 2 && KFEC_MAC_PAIR && !KFEC_MAC_XORONLY) {
+            } else if constexpr (PAIRED && VEC >= 32 && PD == 2 && KFEC_MAC_PAIR && !KFEC_MAC_XORONLY) {
                 // the two shards of the trip together, row by row: 6 permutes and three 3-input XORs per row and dword
                 // (one VALU op fewer than two separate MACs); the selectors of both granules stay live across the
                 // rows, each row's two tables are read from LDS just before use (not all 8 rows' at once)
@@ -2083,7 +2089,7 @@ static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
 // 200:55 132.2 -> 140.4 ms (60 rows instead of 56); 11-row tiles need 175 VGPRs, 2 waves (profiles/r06_mt_tall_ab.txt)
 static int pick_mt_enc(int R)
 {
-    if (R <= 8) return pick_mt(R);
+    if (R <= 8) return KFEC_ENC_MT_MID != 0 && R >= 5 ? R : pick_mt(R);
     const int rows8 = (R + 7) / 8 * 8, rows10 = (R + 9) / 10 * 10;
     return rows10 <= rows8 ? 10 : 8;
 }
@@ -2139,8 +2145,14 @@ static int dispatch_mac(int vec, int mt, MacArgs a, hipStream_t s)
         }
     }
     if (vec == 32) {
-        if constexpr (!DEC)
+        if constexpr (!DEC) {
             if (mt == 10) return run_mac<32, 10, false>(a, s);
+            if constexpr (KFEC_ENC_MT_MID != 0) {
+                if (mt == 5) return run_mac<32, 5, false>(a, s);
+                if (mt == 6) return run_mac<32, 6, false>(a, s);
+                if (mt == 7) return run_mac<32, 7, false>(a, s);
+            }
+        }
         switch (mt) {
         case 1: return run_mac<32, 1, DEC>(a, s);
         case 2: return run_mac<32, 2, DEC>(a, s);
@@ -2165,6 +2177,9 @@ static int entry_bytes(int mt)
     case 2: return MacLayout<2>::ENTRY;
     case 3: return MacLayout<3>::ENTRY;
     case 4: return MacLayout<4>::ENTRY;
+    case 5: return MacLayout<5>::ENTRY;
+    case 6: return MacLayout<6>::ENTRY;
+    case 7: return MacLayout<7>::ENTRY;
     case 10: return MacLayout<10>::ENTRY;
     default: return MacLayout<8>::ENTRY;
     }

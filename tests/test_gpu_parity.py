@@ -224,6 +224,8 @@ CASES = [
     (30, 50, 512, 512, 8200, None, "R=20, 2 encode row tiles of 10 over 513 chunks, random erasures: tile spans, T-table decode"),
     (25, 50, 1440, 1440, 40, 25, "R=25 -> three 10-row encode tiles, the last computing 5 rows"),
     (9, 18, 1440, 1440, 30, 9, "R=9 -> one 10-row encode tile with a slack row"),
+    (20, 25, 1440, 1440, 40, 5, "R=5 -> one 5-row encode tile, paired MAC"),
+    (16, 23, 1440, 1440, 30, None, "R=7 -> one 7-row encode tile (odd K pairs + tail), random erasures"),
 ]
 
 
