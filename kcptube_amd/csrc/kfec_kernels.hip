@@ -315,7 +315,12 @@ __device__ __forceinline__ void write_empty(const PrepArgs &a, uint64_t g, uint8
 // read), so the kernels read zeros beyond m.
 // Row tile of the syndrome form (the C rows a syn kernel reads: RT x RT bytes) and the record stride: the
 // header, the present bits and RT rows of C -- 64 bytes at R = 3, one whole line per group
-__host__ __device__ constexpr int syn_rt(int R) { return R <= 4 ? (R > 0 ? R : 1) : 8; }
+#ifndef KFEC_SYN_RT_MID
+#define KFEC_SYN_RT_MID 1  // syndrome decode for R = 5..7: RT = R instead of 8 (166 VGPRs at RT 5, 3 waves per SIMD, against
+                           // RT 8's 256): 20:5 decode 12.83 -> 9.18 ms, 20:6 13.40 -> 11.05, 16:7 11.87 -> 10.90, 10:6
+                           // random 7.31 -> 5.89, 20:6 at 1% loss 3.93 -> 2.53 (profiles/r06_syn_rt_mid_ab.txt)
+#endif
+__host__ __device__ constexpr int syn_rt(int R) { return R <= 4 ? (R > 0 ? R : 1) : (KFEC_SYN_RT_MID && R <= 7 ? R : 8); }
 __host__ __device__ inline size_t syn_record_stride(size_t K, size_t R)
 {
     return KFEC_SYN_REC_COMPACT ? (size_t)((40 + 8 * syn_rt((int)R) + 15) & ~15) : record_stride(K, R);
@@ -2193,6 +2198,9 @@ static size_t syn_td(int rt)
     case 2: return SynLayout<2>::TD;
     case 3: return SynLayout<3>::TD;
     case 4: return SynLayout<4>::TD;
+    case 5: return SynLayout<5>::TD;
+    case 6: return SynLayout<6>::TD;
+    case 7: return SynLayout<7>::TD;
     default: return SynLayout<8>::TD;
     }
 }
@@ -2221,19 +2229,25 @@ static int run_syn(SynArgs a, size_t lds, int cus, hipStream_t s)
 
 static int dispatch_syn(int vec, int rt, SynArgs a, size_t lds, int cus, hipStream_t s)
 {
-#define KFEC_RT_CASES(V, P)                               \
-    switch (rt) {                                         \
-    case 1: return run_syn<V, 1, P>(a, lds, cus, s);      \
-    case 2: return run_syn<V, 2, P>(a, lds, cus, s);      \
-    case 3: return run_syn<V, 3, P>(a, lds, cus, s);      \
-    case 4: return run_syn<V, 4, P>(a, lds, cus, s);      \
-    default: return run_syn<V, 8, P>(a, lds, cus, s);     \
-    }
-    if (vec == kLatencyVec) KFEC_RT_CASES(4, 16)
+#define KFEC_RT_CASES(V, P)                                                          \
+    do {                                                                             \
+        switch (rt) {                                                                \
+        case 1: return run_syn<V, 1, P>(a, lds, cus, s);                             \
+        case 2: return run_syn<V, 2, P>(a, lds, cus, s);                             \
+        case 3: return run_syn<V, 3, P>(a, lds, cus, s);                             \
+        case 4: return run_syn<V, 4, P>(a, lds, cus, s);                             \
+        case 5: if constexpr (KFEC_SYN_RT_MID != 0) return run_syn<V, 5, P>(a, lds, cus, s); break; \
+        case 6: if constexpr (KFEC_SYN_RT_MID != 0) return run_syn<V, 6, P>(a, lds, cus, s); break; \
+        case 7: if constexpr (KFEC_SYN_RT_MID != 0) return run_syn<V, 7, P>(a, lds, cus, s); break; \
+        default: break;                                                              \
+        }                                                                            \
+        return run_syn<V, 8, P>(a, lds, cus, s);                                     \
+    } while (0)
+    if (vec == kLatencyVec) KFEC_RT_CASES(4, 16);
 #if KFEC_SYN_SMALLK_PD > 0
-    if (a.K <= 12) KFEC_RT_CASES(32, KFEC_SYN_SMALLK_PD)
+    if (a.K <= 12) KFEC_RT_CASES(32, KFEC_SYN_SMALLK_PD);
 #endif
-    KFEC_RT_CASES(32, 0)
+    KFEC_RT_CASES(32, 0);
 #undef KFEC_RT_CASES
 }
 

@@ -208,7 +208,7 @@ CASES = [
     (6, 9, 2048, 2048, 5, 3, "B = 2048"),
     (6, 9, 2049, 2064, 5, 3, "B = 2049, pitch > B"),
     (3, 10, 100, 100, 50, None, "K < R: syndrome form RT=8 with prep MAXM=3"),
-    (5, 11, 1440, 1440, 40, None, "R=6 -> syndrome RT=8, slack rows, random erasures"),
+    (5, 11, 1440, 1440, 40, None, "R=6 -> syndrome RT=6 (K < R), random erasures"),
     (100, 104, 64, 64, 20, 4, "K > 64 with R <= 8: second present word"),
     (250, 255, 16, 16, 10, 5, "K > 192 with R <= 8: fourth present word"),
     (20, 23, 1440, 1440, 64, 0, "zero loss: nothing recovered, nothing read"),
@@ -226,6 +226,8 @@ CASES = [
     (9, 18, 1440, 1440, 30, 9, "R=9 -> one 10-row encode tile with a slack row"),
     (20, 25, 1440, 1440, 40, 5, "R=5 -> one 5-row encode tile, paired MAC"),
     (16, 23, 1440, 1440, 30, None, "R=7 -> one 7-row encode tile (odd K pairs + tail), random erasures"),
+    (20, 25, 1440, 1440, 41, None, "R=5 -> syndrome decode RT=5, random erasures"),
+    (20, 26, 1440, 1440, 20000, None, "R=6 -> syndrome RT=6 over 513+ chunks, random erasures (dense and listed shapes)"),
 ]
 
 
