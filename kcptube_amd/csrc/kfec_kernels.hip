@@ -2088,15 +2088,24 @@ static int pick_vec_mac(size_t pitch, size_t B, std::initializer_list<const void
 // granules amortise each table read over the most bytes).
 static int pick_mt(int R) { return R <= 4 ? std::max(R, 1) : 8; }
 
-// The encode's row tile for 32-byte granules: for R > 8 the 8- or 10-row tile that computes fewer rows (ties: 10, fewer
-// tiles re-reading the data).  Both run at 3 waves per SIMD (152 / 167 VGPRs) at about the same cost per row, so the
-// rows a last partial tile wastes decide: 40:20 encode 11.86 -> 9.98 ms and 30:20 9.03 -> 7.78 ms with 10-row tiles,
-// 200:55 132.2 -> 140.4 ms (60 rows instead of 56); 11-row tiles need 175 VGPRs, 2 waves (profiles/r06_mt_tall_ab.txt)
+// The encode's row tile for 32-byte granules.  R <= 8: one tile of R rows (R = 5..7 with the paired MAC, KFEC_ENC_MT_MID).
+// R > 8: the height among 5..8 and 10 of least modelled VALU per (shard, dword) -- tiles x (4.5 per row for the paired
+// MAC + 5 for the selector extractions every tile repeats), ties to the taller tile.  All of them run at 3 or more
+// waves per SIMD (127-167 VGPRs) at about the same cost per row, so the rows a partial last tile wastes decide:
+// 40:20 and 30:20 two 10-row tiles instead of three 8-row ones (11.86 -> 9.98 ms, 9.03 -> 7.78), 30:12 two of 6
+// (26.05 -> 22.54 ms), 20:13 two of 7 (18.7 -> 17.7), 25:25 five of 5 (19.9 -> 18.8); 200:55 keeps 7 x 8 (10-row tiles
+// compute 60 rows: 140.4 against 132.2 ms); 11-row tiles need 175 VGPRs, 2 waves (profiles/r06_mt_tall_ab.txt,
+// profiles/r06_mt_model_ab.txt)
 static int pick_mt_enc(int R)
 {
     if (R <= 8) return KFEC_ENC_MT_MID != 0 && R >= 5 ? R : pick_mt(R);
-    const int rows8 = (R + 7) / 8 * 8, rows10 = (R + 9) / 10 * 10;
-    return rows10 <= rows8 ? 10 : 8;
+    int best = 8, best_cost = 1 << 30;
+    for (int mt : {10, 8, 7, 6, 5}) {
+        if (KFEC_ENC_MT_MID == 0 && mt < 8) continue;
+        const int cost = (R + mt - 1) / mt * (9 * mt + 10);
+        if (cost < best_cost) best = mt, best_cost = cost;
+    }
+    return best;
 }
 
 
