@@ -315,6 +315,11 @@ __device__ __forceinline__ void write_empty(const PrepArgs &a, uint64_t g, uint8
 // read), so the kernels read zeros beyond m.
 // Row tile of the syndrome form (the C rows a syn kernel reads: RT x RT bytes) and the record stride: the
 // header, the present bits and RT rows of C -- 64 bytes at R = 3, one whole line per group
+#ifndef KFEC_SYN_FINAL_ROWS
+#define KFEC_SYN_FINAL_ROWS 1  // syn_list_kernel's final mix at RT 5, 6, 8 with the syndromes outer (260 -> 176 VGPRs at RT
+                               // 8): 1%-loss decode 20:8 3.89 -> 3.44 ms, 20:5 2.18 -> 2.13, 20:6 2.49 -> 2.46; RT 7 measured
+                               // 6% slower and keeps the row order (profiles/r06_syn_final_rows_ab.txt)
+#endif
 #ifndef KFEC_SYN_RT_MID
 #define KFEC_SYN_RT_MID 1  // syndrome decode for R = 5..7: RT = R instead of 8 (166 VGPRs at RT 5, 3 waves per SIMD, against
                            // RT 8's 256): 20:5 decode 12.83 -> 9.18 ms, 20:6 13.40 -> 11.05, 16:7 11.87 -> 10.90, 10:6
@@ -1771,13 +1776,47 @@ __device__ __forceinline__ void syn_loop(const SynArgs &a, uint32_t (&acc)[RT][G
 }
 
 // out_u = XOR_r C[u][r] * y_r for u < m, stored to recovered slot u of group g
-template <int VEC, int RT, uint32_t ROWS = (1u << RT) - 1u>
+template <int VEC, int RT, uint32_t ROWS = (1u << RT) - 1u, bool OUTER = false>
 __device__ __forceinline__ void syn_final(const SynArgs &a, const uint32_t (&acc)[RT][Gran<VEC>::W], const uint32_t *ct,
                                           uint32_t m, uint32_t g, uint32_t off, uint32_t col)
 {
     constexpr int W = Gran<VEC>::W;
     constexpr int TD = SynLayout<RT>::TD;
     const uint64_t obase = ((uint64_t)g * a.R) * a.pitch + off;
+    if constexpr (OUTER && RT >= 5 && RT != 7 && !KFEC_SYN_XORONLY) {
+        // syndromes outer: y_r's selectors once per r, its contribution to every output row, then y_r is dead --
+        // the output-row order below keeps all RT x W x 3 selectors live (192 VGPRs at RT 8)
+        uint32_t o[RT][W];
+#pragma unroll
+        for (int u = 0; u < RT; ++u)
+#pragma unroll
+            for (int w = 0; w < W; ++w) o[u][w] = 0;
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+            if (!((ROWS >> r) & 1u)) continue;
+            uint32_t sl[W][3];
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint32_t yv = acc[r][w];
+                sl[w][0] = yv & 0x07070707u; sl[w][1] = (yv >> 3) & 0x07070707u; sl[w][2] = (yv >> 6) & 0x03030303u;
+            }
+#pragma unroll
+            for (int u = 0; u < RT; ++u) {
+                if ((uint32_t)u < m) {
+                    const uint32_t *tp = ct + u * TD + 5 * r;
+                    uint32_t t[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) t[i] = tp[i];
+#pragma unroll
+                    for (int w = 0; w < W; ++w) o[u][w] = perm_mac(o[u][w], t, sl[w][0], sl[w][1], sl[w][2]);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < RT; ++u)
+            if ((uint32_t)u < m) store_gran<VEC>(a.out + obase + (uint64_t)u * a.pitch, o[u], col, a.B);
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < RT; ++u) {
         if ((uint32_t)u < m) {
@@ -1884,7 +1923,7 @@ __global__ void __launch_bounds__(kMacBlock) syn_list_kernel(SynArgs a)
             // the tables were written by lanes of this wave: LDS operations of one wave complete in order, the
             // fence keeps the compiler from moving the reads above the writes
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (in) syn_final<VEC, RT, ROWS>(a, acc, ct, m, g, off, col);
+            if (in) syn_final<VEC, RT, ROWS, KFEC_SYN_FINAL_ROWS != 0>(a, acc, ct, m, g, off, col);
         });
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the next task rewrites the tables
     }

@@ -284,7 +284,8 @@ def test_batch_vs_oracle(dev, oracle, K, N, B, pitch, G, erase, note):
         assert (_np(out)[:, :, hi:] == 0).all(), note
 
 
-@pytest.mark.parametrize("K,N,B,G", [(20, 23, 1440, 700), (10, 13, 1400, 500), (5, 11, 3000, 90), (3, 5, 40, 3000)])
+@pytest.mark.parametrize("K,N,B,G", [(20, 23, 1440, 700), (10, 13, 1400, 500), (5, 11, 3000, 90), (3, 5, 40, 3000),
+                                     (16, 24, 1440, 600), (20, 25, 1440, 600)])
 def test_sparse_losses_take_the_listed_shape(dev, oracle, K, N, B, G):
     """Few groups lost data (a live link): the decode runs over the device-built list of those groups only
     (syn_list_kernel); every other group must come back 'nothing recovered' and untouched output slots."""
