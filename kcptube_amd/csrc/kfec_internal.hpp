@@ -28,8 +28,21 @@ inline size_t record_stride(size_t K, size_t R)
 // padding), per-1024-group chunk counts / offsets, then the list of up to G group ids (uint32 each)
 inline size_t decode_list_offset(size_t G, size_t K, size_t R) { return (G * record_stride(K, R) + 255) & ~size_t(255); }
 inline size_t decode_list_chunks(size_t G) { return (G + 1023) / 1024; }
+// Hybrid decode (R in [KFEC_DEC_HYBRID_MIN_R, 8]): both record forms are prepared, the syndrome records after the
+// list (at most 112 bytes per group, RT <= 8), and the device picks the listed syndrome kernel for sparse loss or the
+// coefficient-form MAC for dense loss
+#ifndef KFEC_DEC_HYBRID_MIN_R
+#define KFEC_DEC_HYBRID_MIN_R 7  // R = 7, 8: dense decode 14-22% faster, sparse unchanged (profiles/r06_dec_hybrid_ab.txt;
+                                 // at R = 6 the coefficient form was not faster)
+#endif
+inline bool decode_hybrid_r(size_t R) { return R >= KFEC_DEC_HYBRID_MIN_R && R <= 8; }
+inline size_t decode_hybrid_syn_offset(size_t G, size_t K, size_t R)
+{
+    return (decode_list_offset(G, K, R) + 256 + 4 * decode_list_chunks(G) + 4 * G + 255) & ~size_t(255);
+}
 inline size_t decode_workspace_bytes(size_t G, size_t K, size_t R)
 {
+    if (decode_hybrid_r(R)) return decode_hybrid_syn_offset(G, K, R) + 112 * G;
     return decode_list_offset(G, K, R) + 256 + 4 * decode_list_chunks(G) + 4 * G;
 }
 
@@ -62,7 +75,8 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
                   uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s);
 int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, const uint64_t *d_present,
                        uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s, bool syn = false,
-                       bool factored = false);
+                       bool factored = false, const uint32_t *skip_listed = nullptr, uint32_t cols = 0,
+                       uint32_t cols_pad = 0);
 int launch_synth(uint64_t seed, int N, size_t g0, size_t G, size_t s0, size_t ns, size_t B, size_t pitch,
                  void *d_out, hipStream_t s);
 int launch_erasure_masks(uint64_t seed, int N, size_t g0, size_t G, size_t pool, size_t count_max,

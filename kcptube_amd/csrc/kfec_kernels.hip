@@ -257,7 +257,15 @@ struct PrepArgs {
     uint32_t rec_stride;
     int syn;       // write syndrome-form records (R <= 8) instead of the coefficient form
     int factored;  // decode_prep_lagrange: write the factored form (dec_expand rebuilds each coefficient)
+    // hybrid decode: the coefficient-form prep exits when the listed syndrome shape takes the launch (syn_listed)
+    const uint32_t *skip_listed;
+    uint32_t cols, cols_pad;
 };
+
+__device__ __forceinline__ bool prep_skip(const PrepArgs &a)
+{
+    return a.skip_listed && (uint64_t)*a.skip_listed * a.cols_pad < a.G * a.cols;
+}
 
 // Factored coefficient-form record (decode_prep_lagrange for the mac_kernel decode, KFEC_DEC_FACTORED): the
 // m x K coefficients of a group are coef[u][j] = exp(lnum_u - log(xm_u ^ xs_j) - lden_j) (see the prep), so the
@@ -368,6 +376,7 @@ __device__ __forceinline__ void write_syn(const PrepArgs &a, uint64_t g, int m, 
 template <int MAXM>
 __global__ void __launch_bounds__(kBlock) decode_prep_small(PrepArgs a)
 {
+    if (prep_skip(a)) return;  // (whole grid)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *s_exp = smem, *s_log = smem + 512, *s_E = smem + 768;  // s_E: parity rows, R x K
     stage_gf(s_exp, s_log);
@@ -528,6 +537,7 @@ template <int MAXM, bool SYN = false>
 __global__ void __launch_bounds__(kBlock) decode_prep_perm(PrepArgs a)
 {
     static_assert(MAXM >= 1 && MAXM <= 4, "rows are packed into one dword");
+    if (prep_skip(a)) return;  // (whole grid)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *s_exp = smem, *s_log = smem + 512, *s_E = smem + 768;  // s_E: parity rows, R x K4 (zero padded)
     stage_gf(s_exp, s_log);
@@ -933,6 +943,8 @@ struct MacArgs {
     uint32_t gmax;          // group slots per chunk
     uint32_t tiles;         // row tiles of MT output rows
     uint32_t factored;      // decode: factored records (fac_record_stride), coefficients rebuilt by dec_expand
+    const uint32_t *list_count;  // hybrid decode: the listed groups' count; the kernel exits when the listed shape runs
+    uint32_t cols_pad;
 };
 
 template <int VEC>
@@ -1261,6 +1273,9 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
 
+    if constexpr (DEC) {  // hybrid decode: the listed syndrome kernel has it (same rule as syn_listed)
+        if (a.list_count && (uint64_t)*a.list_count * a.cols_pad < (uint64_t)a.G * a.cols) return;
+    }
     uint32_t chunk, tile;
     block_chunk_tile(blockIdx.x, a.tiles, chunk, tile);
     const uint32_t base = chunk * kMacBlock;
@@ -1597,6 +1612,7 @@ struct SynArgs {
     const uint32_t *list_count;
     uint64_t pitch;
     uint32_t total, cols, cols_pad, G, K, R, B, rec_stride, etab_rows;
+    uint32_t no_dense;        // hybrid decode: the coefficient-form MAC takes the dense shape (no syn_kernel launch)
 };
 
 template <int RT>
@@ -2266,7 +2282,8 @@ template <int VEC, int RT, int PDX = 0>
 static int run_syn(SynArgs a, size_t lds, int cus, hipStream_t s)
 {
     const uint32_t nb = xcd_grid((a.total + kMacBlock - 1) / kMacBlock);
-    hipLaunchKernelGGL((syn_kernel<VEC, RT, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), af_lds(syn_cap(lds)), s, a);
+    if (!a.no_dense)
+        hipLaunchKernelGGL((syn_kernel<VEC, RT, PDX>), dim3(std::max(1u, nb)), dim3(kMacBlock), af_lds(syn_cap(lds)), s, a);
     if (!a.list_count) return hipGetLastError() == hipSuccess ? 0 : -3;  // dense only
     // the listed shape: persistent, ~8 workgroups per CU, at most one wave per (group, 64 columns) task
     const uint64_t tasks = (uint64_t)a.G * (a.cols_pad / 64);
@@ -2355,7 +2372,8 @@ int launch_encode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
 // records) of every group into d_workspace (+ d_out_idx, d_status).  The MAC kernels here and in
 // kfec_frame.hip consume them.
 int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size_t G, const uint64_t *d_present,
-                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s, bool syn, bool factored)
+                       uint8_t *d_out_idx, uint8_t *d_status, void *d_workspace, hipStream_t s, bool syn, bool factored,
+                       const uint32_t *skip_listed, uint32_t cols, uint32_t cols_pad)
 {
     const int R = N - K;
     if (G == 0) return 0;
@@ -2373,6 +2391,9 @@ int launch_decode_prep(const DeviceInfo &di, const uint8_t *d_enc, int K, int N,
     p.rec_stride = (uint32_t)rs;
     p.syn = syn ? 1 : 0;
     p.factored = factored ? 1 : 0;
+    p.skip_listed = skip_listed;
+    p.cols = cols;
+    p.cols_pad = cols_pad;
     const int mmax = std::min(K, R);
     if (mmax <= 8) {
         const size_t lds = 768 + (size_t)R * K;
@@ -2430,6 +2451,67 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
                      G * (size_t)R < (size_t(1) << 32);
     // (the mac_kernel decode rebuilds the coefficients of factored records; the prep writes them for K, R > 8)
     const bool factored = !syn && KFEC_DEC_FACTORED && KFEC_DEC_TTAB && std::min(K, R) > 8;
+    // hybrid (decode_hybrid_r): the listed syndrome kernel for sparse loss, the coefficient-form MAC (3 waves per
+    // SIMD against the RT >= 6 syndrome kernel's 2) for dense loss, chosen on the device by the same rule
+    const bool hybrid = syn && decode_hybrid_r(R) && vec == 32 && G > kLatencyGroups && B > 0 &&
+                        G * cols <= kMaxItemsPerLaunch && KFEC_DEC_TTAB;
+    if (hybrid) {
+        // syndrome records and the list first; the coefficient records only when the dense shape will run (the
+        // prep exits at once otherwise)
+        uint8_t *rec_syn = rec + decode_hybrid_syn_offset(G, K, R);
+        if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, rec_syn, s, true, false)) return -3;
+        uint32_t *count = reinterpret_cast<uint32_t *>(rec + decode_list_offset(G, K, R));
+        uint32_t *chunk_cnt = count + 64;
+        uint32_t *list = chunk_cnt + decode_list_chunks(G);
+        const size_t cols_pad = (cols + 63) / 64 * 64;
+        const uint32_t nch = (uint32_t)((G + kActChunk - 1) / kActChunk);
+        hipLaunchKernelGGL(active_count_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)G, (uint32_t)R, d_out_idx, chunk_cnt);
+        hipLaunchKernelGGL(active_scan_kernel, dim3(1), dim3(kBlock), 0, s, nch, chunk_cnt, count);
+        hipLaunchKernelGGL(active_scatter_kernel, dim3(nch), dim3(kBlock), 0, s, (uint64_t)G, (uint32_t)R, d_out_idx,
+                           (const uint32_t *)chunk_cnt, list);
+        if (hipGetLastError() != hipSuccess) return -3;
+        if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s, false, false, count,
+                               (uint32_t)cols, (uint32_t)cols_pad))
+            return -3;
+        SynArgs sa{};
+        sa.data = static_cast<const uint8_t *>(d_data);
+        sa.parity = static_cast<const uint8_t *>(d_parity);
+        sa.out = static_cast<uint8_t *>(d_out);
+        sa.rec = rec_syn;
+        sa.etab = reinterpret_cast<const uint32_t *>(d_enc + enc_tab_offset(K, N));
+        sa.list = list;
+        sa.list_count = count;
+        sa.etab_rows = (uint32_t)enc_tab_rows(R);
+        sa.pitch = pitch;
+        sa.total = (uint32_t)(G * cols);
+        sa.cols = (uint32_t)cols;
+        sa.cols_pad = (uint32_t)cols_pad;
+        sa.G = (uint32_t)G;
+        sa.K = K; sa.R = R; sa.B = (uint32_t)B;
+        sa.rec_stride = (uint32_t)syn_record_stride(K, R);
+        sa.no_dense = 1;
+        if (dispatch_syn(vec, rt, sa, lds_syn, di.cus, s)) return -3;
+        const uint32_t gmax = (uint32_t)std::min<size_t>(G, (kMacBlock - 1) / cols + 2);
+        MacArgs a{};
+        a.data = static_cast<const uint8_t *>(d_data);
+        a.parity = static_cast<const uint8_t *>(d_parity);
+        a.out = static_cast<uint8_t *>(d_out);
+        a.enc = d_enc;
+        a.rec = rec;
+        a.pitch = pitch;
+        a.total = (uint32_t)(G * cols);
+        a.cols = (uint32_t)cols;
+        a.G = (uint32_t)G;
+        a.K = K; a.R = R; a.B = (uint32_t)B;
+        a.rec_stride = (uint32_t)rs;
+        a.factored = 0;
+        a.JC = (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kDecLdsBudget / (kDecEntry * gmax)));
+        a.gmax = gmax;
+        a.tiles = 1;
+        a.list_count = count;
+        a.cols_pad = (uint32_t)cols_pad;
+        return dispatch_mac<true>(vec, 8, a, s);
+    }
     if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s, syn, factored)) return -3;
     if (R == 0 || B == 0) return 0;
     if (syn) {
