@@ -328,6 +328,11 @@ __device__ __forceinline__ void write_empty(const PrepArgs &a, uint64_t g, uint8
                                // 8): 1%-loss decode 20:8 3.89 -> 3.44 ms, 20:5 2.18 -> 2.13, 20:6 2.49 -> 2.46; RT 7 measured
                                // 6% slower and keeps the row order (profiles/r06_syn_final_rows_ab.txt)
 #endif
+#ifndef KFEC_DEC_MT_MID
+#define KFEC_DEC_MT_MID 1  // the hybrid decode's coefficient-form MAC for R = 5..7 as an R-row tile (129-149 VGPRs):
+                           // with the hybrid from R = 5, dense 20:6 11.05 -> 9.87 ms, 10:6 random 5.99 -> 5.00, 16:7
+                           // 9.63 -> 9.19, 20:5 9.06 -> 8.88; sparse unchanged (profiles/r06_dec_mt_mid_ab.txt)
+#endif
 #ifndef KFEC_SYN_RT_MID
 #define KFEC_SYN_RT_MID 1  // syndrome decode for R = 5..7: RT = R instead of 8 (166 VGPRs at RT 5, 3 waves per SIMD, against
                            // RT 8's 256): 20:5 decode 12.83 -> 9.18 ms, 20:6 13.40 -> 11.05, 16:7 11.87 -> 10.90, 10:6
@@ -1134,7 +1139,7 @@ __device__ __forceinline__ void dec_expand(const MacArgs &a, uint8_t *s_ent, uin
                                            uint32_t nj, uint32_t row0, const uint8_t *s_exp, const uint8_t *s_log,
                                            uint32_t tbase)
 {
-    static_assert(MT == 8, "entry: 8 offsets");
+    static_assert(MT >= 1 && MT <= 8, "entry: 8 offsets (rows past MT take the zero table)");
     const uint32_t items = ng * nj, K4 = (a.K + 3) & ~3u;
     constexpr int EB = 4;  // entries per thread whose loads are issued together
     for (uint32_t e0 = 0; e0 < items; e0 += EB * blockDim.x) {
@@ -1187,12 +1192,12 @@ __device__ __forceinline__ void dec_expand(const MacArgs &a, uint8_t *s_ent, uin
                     cv[b][r] = s_exp[ex];
                 }
             }
-            uint32_t o[MT];
+            uint32_t o[8];
 #pragma unroll
-            for (int r = 0; r < MT; ++r) o[r] = tbase + ((ok && row0 + r < m) ? cv[b][r] * 32u : 0u);  // T[0] = zero tables
+            for (int r = 0; r < 8; ++r) o[r] = tbase + ((r < MT && ok && row0 + r < m) ? cv[b][r < MT ? r : 0] * 32u : 0u);  // T[0] = zero tables
             uint32_t *ow = reinterpret_cast<uint32_t *>(ent + 8);
 #pragma unroll
-            for (int r = 0; r < MT; r += 2) ow[r / 2] = o[r] | (o[r + 1] << 16);
+            for (int r = 0; r < 8; r += 2) ow[r / 2] = o[r] | (o[r + 1] << 16);
         }
     }
 }
@@ -1207,7 +1212,7 @@ __device__ __forceinline__ void dec_expand_fac(const MacArgs &a, uint8_t *s_ent,
                                                uint32_t nj, uint32_t row0, const uint8_t *s_exp, const uint8_t *s_log,
                                                const uint16_t *s_taddr, uint32_t tbase, bool staged_sync)
 {
-    static_assert(MT == 8, "entry: 8 offsets");
+    static_assert(MT >= 1 && MT <= 8, "entry: 8 offsets (rows past MT take the zero table)");
     typedef const __attribute__((address_space(4))) uint32_t cu32;
     const uint32_t K = a.K, K4 = (K + 3) & ~3u, L0 = fac_lnum_off(K), R8 = fac_r8(a.R);
     const bool has = threadIdx.x < nj;
@@ -1236,13 +1241,13 @@ __device__ __forceinline__ void dec_expand_fac(const MacArgs &a, uint8_t *s_ent,
             const uint32_t src = sv[b];
             const uint32_t xs = src ? (uint32_t)s_exp[src] : 0u;  // the point of the column's share (x_0 = 0)
             const uint32_t base = 510u - lv[b];
-            uint32_t o[MT];
+            uint32_t o[8];
 #pragma unroll
-            for (int r = 0; r < MT; ++r) {
+            for (int r = 0; r < 8; ++r) {
                 // coef = exp(lnum_u - log(xm_u ^ xs_j) - lden_j); rows past the group's m take T[0] (zero tables)
                 const uint32_t lnr = ((r < 4 ? ln0 : ln1) >> (8 * (r & 3))) & 0xFFu;
                 const uint32_t xmr = ((r < 4 ? xm0 : xm1) >> (8 * (r & 3))) & 0xFFu;
-                o[r] = (uint32_t)r < nrow ? (uint32_t)s_taddr[lnr + base - s_log[xmr ^ xs]] : tbase;
+                o[r] = (r < MT && (uint32_t)r < nrow) ? (uint32_t)s_taddr[lnr + base - s_log[xmr ^ xs]] : tbase;
             }
             if (has) {
                 const uint8_t *p = (src < K) ? a.data + (g * K + src) * a.pitch : a.parity + (g * a.R + (src - K)) * a.pitch;
@@ -1250,7 +1255,7 @@ __device__ __forceinline__ void dec_expand_fac(const MacArgs &a, uint8_t *s_ent,
                 *reinterpret_cast<const uint8_t **>(ent) = p;
                 uint32_t *ow = reinterpret_cast<uint32_t *>(ent + 8);
 #pragma unroll
-                for (int r = 0; r < MT; r += 2) ow[r / 2] = o[r] | (o[r + 1] << 16);
+                for (int r = 0; r < 8; r += 2) ow[r / 2] = o[r] | (o[r + 1] << 16);
             }
         }
     }
@@ -1269,7 +1274,8 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     // straight from pinned host memory) keeps many more loads in flight so the PCIe round trips overlap
     // (MT = 8, the VALU-bound tall tiles: 2, to keep 3 waves per SIMD)
     constexpr bool PAIRED = !DEC && (MT >= 8 || (KFEC_ENC_MT_MID == 1 && MT >= 5));
-    constexpr int PD = PDX ? PDX : (VEC >= 32 ? (MT >= 8 || PAIRED ? 2 : KFEC_MAC_PD) : 2 * KFEC_PD);
+    constexpr int PD = PDX ? PDX : (VEC >= 32 ? (MT >= 8 || PAIRED || (DEC && KFEC_DEC_MT_MID && MT >= 5) ? 2 : KFEC_MAC_PD)
+                                               : 2 * KFEC_PD);
     constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
 
@@ -1283,7 +1289,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     const uint32_t row0 = tile * MT;
     const uint32_t K = a.K, cols = a.cols;
     const bool enc_once = !DEC && K <= a.JC;
-    constexpr bool ttab = DEC && KFEC_DEC_TTAB && MT == 8;
+    constexpr bool ttab = DEC && KFEC_DEC_TTAB && (MT == 8 || (KFEC_DEC_MT_MID && MT >= 5 && MT < 8));
     uint8_t *s_T = s_ent;
     // ttab: T, then (factored records) the GF exp / log tables, then the entries
     constexpr uint32_t kGfBytes = ttab ? kDecGfBytes : 0u;
@@ -1515,7 +1521,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 }
 #pragma unroll
                 for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
-            } else if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT == 8 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR && !KFEC_MAC_XORONLY) {
+            } else if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT >= 5 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR && !KFEC_MAC_XORONLY) {
                 // the decode's form of the same pairing: each row's two tables are read from T at the addresses the
                 // two entries hold (dec_expand added T's base)
                 typedef const volatile __attribute__((address_space(3))) uint16_t lds_u16;
@@ -1572,7 +1578,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 }
             }
         }
-        if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT == 8 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR && !KFEC_MAC_XORONLY)
+        if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT >= 5 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR && !KFEC_MAC_XORONLY)
             read_ofs(jb);  // (the paired loop read its offsets itself: the tail's MAC takes shard jb's)
 #pragma unroll
         for (int u = 0; u < PD; ++u)
@@ -2185,7 +2191,7 @@ template <int VEC, int MT, bool DEC, int PDX = 0>
 static int run_mac(MacArgs a, hipStream_t s)
 {
     using L = MacLayout<MT>;
-    const size_t lds = af_lds((DEC && KFEC_DEC_TTAB && MT == 8) ? kTBytes + kDecGfBytes + (size_t)a.gmax * a.JC * kDecEntry
+    const size_t lds = af_lds((DEC && KFEC_DEC_TTAB && (MT == 8 || (KFEC_DEC_MT_MID && MT >= 5 && MT < 8))) ? kTBytes + kDecGfBytes + (size_t)a.gmax * a.JC * kDecEntry
                                                                 : (size_t)a.gmax * a.JC * L::ENTRY);
     const uint32_t chunks = (a.total + kMacBlock - 1) / kMacBlock;
     const uint32_t nb = a.tiles > 1 ? xcd_tile_chunks(chunks) * a.tiles : xcd_grid(chunks);
@@ -2200,6 +2206,11 @@ static int dispatch_mac(int vec, int mt, MacArgs a, hipStream_t s)
     if constexpr (DEC) {  // coefficient-form decode: R > 8, 8-row tiles only
         (void)mt;
         if (vec == kLatencyVec) return run_mac<4, 8, true, 16>(a, s);
+        if constexpr (KFEC_DEC_MT_MID != 0) {
+            if (vec == 32 && mt == 5) return run_mac<32, 5, true>(a, s);
+            if (vec == 32 && mt == 6) return run_mac<32, 6, true>(a, s);
+            if (vec == 32 && mt == 7) return run_mac<32, 7, true>(a, s);
+        }
         if (vec == 32) return run_mac<32, 8, true>(a, s);
         return run_mac<1, 8, true>(a, s);
     }
@@ -2510,7 +2521,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.tiles = 1;
         a.list_count = count;
         a.cols_pad = (uint32_t)cols_pad;
-        return dispatch_mac<true>(vec, 8, a, s);
+        return dispatch_mac<true>(vec, KFEC_DEC_MT_MID && R < 8 ? R : 8, a, s);
     }
     if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s, syn, factored)) return -3;
     if (R == 0 || B == 0) return 0;
