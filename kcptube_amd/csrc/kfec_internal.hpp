@@ -32,8 +32,9 @@ inline size_t decode_list_chunks(size_t G) { return (G + 1023) / 1024; }
 // list (at most 112 bytes per group, RT <= 8), and the device picks the listed syndrome kernel for sparse loss or the
 // coefficient-form MAC for dense loss
 #ifndef KFEC_DEC_HYBRID_MIN_R
-#define KFEC_DEC_HYBRID_MIN_R 5  // R = 7, 8: dense decode 14-22% faster, sparse unchanged (profiles/r06_dec_hybrid_ab.txt);
-                                 // R = 5, 6 with R-row coefficient tiles (KFEC_DEC_MT_MID): 2-16% (r06_dec_mt_mid_ab.txt)
+#define KFEC_DEC_HYBRID_MIN_R 4  // R = 7, 8: dense decode 14-22% faster, sparse unchanged (profiles/r06_dec_hybrid_ab.txt);
+                                 // R = 5, 6 with R-row coefficient tiles (KFEC_DEC_MT_MID): 2-16% (r06_dec_mt_mid_ab.txt);
+                                 // R = 4 (KFEC_DEC_MT_SMALL): 6%; R = 3 slower (r06_dec_mt_small_ab.txt)
 #endif
 inline bool decode_hybrid_r(size_t R) { return R >= KFEC_DEC_HYBRID_MIN_R && R <= 8; }
 inline size_t decode_hybrid_syn_offset(size_t G, size_t K, size_t R)

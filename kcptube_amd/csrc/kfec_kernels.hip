@@ -333,6 +333,16 @@ __device__ __forceinline__ void write_empty(const PrepArgs &a, uint64_t g, uint8
                            // with the hybrid from R = 5, dense 20:6 11.05 -> 9.87 ms, 10:6 random 5.99 -> 5.00, 16:7
                            // 9.63 -> 9.19, 20:5 9.06 -> 8.88; sparse unchanged (profiles/r06_dec_mt_mid_ab.txt)
 #endif
+#ifndef KFEC_DEC_MT_SMALL
+#define KFEC_DEC_MT_SMALL 1  // the hybrid decode's coefficient-form MAC for R = 4 as a 4-row tile: dense 8:4 decode 3.97 ->
+                             // 3.72 ms; for R = 3 it was slower than the syndrome kernel (20:3 6.2-6.6 -> 6.7, 10:3 random
+                             // 3.11 -> 3.28), so R = 3 stays syndrome-only (profiles/r06_dec_mt_small_ab.txt)
+#endif
+// the coefficient-form decode MAC reads its tables from T (KFEC_DEC_TTAB) for these row tiles
+__host__ __device__ constexpr bool dec_ttab(int MT)
+{
+    return KFEC_DEC_TTAB && (MT == 8 || (KFEC_DEC_MT_MID && MT >= 5 && MT < 8) || (KFEC_DEC_MT_SMALL && MT == 4));
+}
 #ifndef KFEC_SYN_RT_MID
 #define KFEC_SYN_RT_MID 1  // syndrome decode for R = 5..7: RT = R instead of 8 (166 VGPRs at RT 5, 3 waves per SIMD, against
                            // RT 8's 256): 20:5 decode 12.83 -> 9.18 ms, 20:6 13.40 -> 11.05, 16:7 11.87 -> 10.90, 10:6
@@ -1274,7 +1284,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     // straight from pinned host memory) keeps many more loads in flight so the PCIe round trips overlap
     // (MT = 8, the VALU-bound tall tiles: 2, to keep 3 waves per SIMD)
     constexpr bool PAIRED = !DEC && (MT >= 8 || (KFEC_ENC_MT_MID == 1 && MT >= 5));
-    constexpr int PD = PDX ? PDX : (VEC >= 32 ? (MT >= 8 || PAIRED || (DEC && KFEC_DEC_MT_MID && MT >= 5) ? 2 : KFEC_MAC_PD)
+    constexpr int PD = PDX ? PDX : (VEC >= 32 ? (MT >= 8 || PAIRED || (DEC && dec_ttab(MT)) ? 2 : KFEC_MAC_PD)
                                                : 2 * KFEC_PD);
     constexpr int VB = VEC >= 4 ? VEC : 4;  // bytes per granule
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ent[];
@@ -1289,7 +1299,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
     const uint32_t row0 = tile * MT;
     const uint32_t K = a.K, cols = a.cols;
     const bool enc_once = !DEC && K <= a.JC;
-    constexpr bool ttab = DEC && KFEC_DEC_TTAB && (MT == 8 || (KFEC_DEC_MT_MID && MT >= 5 && MT < 8));
+    constexpr bool ttab = DEC && dec_ttab(MT);
     uint8_t *s_T = s_ent;
     // ttab: T, then (factored records) the GF exp / log tables, then the entries
     constexpr uint32_t kGfBytes = ttab ? kDecGfBytes : 0u;
@@ -1521,7 +1531,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 }
 #pragma unroll
                 for (int u = 0; u < PD; ++u) x[u] = load_gran<VEC>(share_ptr(min(jb + u + PD, nj - 1)), col, a.B);
-            } else if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT >= 5 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR && !KFEC_MAC_XORONLY) {
+            } else if constexpr (DEC && ttab && KFEC_DEC_OFS16 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR && !KFEC_MAC_XORONLY) {
                 // the decode's form of the same pairing: each row's two tables are read from T at the addresses the
                 // two entries hold (dec_expand added T's base)
                 typedef const volatile __attribute__((address_space(3))) uint16_t lds_u16;
@@ -1578,7 +1588,7 @@ __global__ void __launch_bounds__(kMacBlock, KFEC_MINW) mac_kernel(MacArgs a)
                 }
             }
         }
-        if constexpr (DEC && ttab && KFEC_DEC_OFS16 && MT >= 5 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR && !KFEC_MAC_XORONLY)
+        if constexpr (DEC && ttab && KFEC_DEC_OFS16 && VEC >= 32 && PD == 2 && KFEC_DEC_PAIR && !KFEC_MAC_XORONLY)
             read_ofs(jb);  // (the paired loop read its offsets itself: the tail's MAC takes shard jb's)
 #pragma unroll
         for (int u = 0; u < PD; ++u)
@@ -2191,7 +2201,7 @@ template <int VEC, int MT, bool DEC, int PDX = 0>
 static int run_mac(MacArgs a, hipStream_t s)
 {
     using L = MacLayout<MT>;
-    const size_t lds = af_lds((DEC && KFEC_DEC_TTAB && (MT == 8 || (KFEC_DEC_MT_MID && MT >= 5 && MT < 8))) ? kTBytes + kDecGfBytes + (size_t)a.gmax * a.JC * kDecEntry
+    const size_t lds = af_lds((DEC && dec_ttab(MT)) ? kTBytes + kDecGfBytes + (size_t)a.gmax * a.JC * kDecEntry
                                                                 : (size_t)a.gmax * a.JC * L::ENTRY);
     const uint32_t chunks = (a.total + kMacBlock - 1) / kMacBlock;
     const uint32_t nb = a.tiles > 1 ? xcd_tile_chunks(chunks) * a.tiles : xcd_grid(chunks);
@@ -2206,6 +2216,8 @@ static int dispatch_mac(int vec, int mt, MacArgs a, hipStream_t s)
     if constexpr (DEC) {  // coefficient-form decode: R > 8, 8-row tiles only
         (void)mt;
         if (vec == kLatencyVec) return run_mac<4, 8, true, 16>(a, s);
+        if constexpr (KFEC_DEC_MT_SMALL != 0)
+            if (vec == 32 && mt == 4) return run_mac<32, 4, true>(a, s);
         if constexpr (KFEC_DEC_MT_MID != 0) {
             if (vec == 32 && mt == 5) return run_mac<32, 5, true>(a, s);
             if (vec == 32 && mt == 6) return run_mac<32, 6, true>(a, s);
@@ -2521,7 +2533,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         a.tiles = 1;
         a.list_count = count;
         a.cols_pad = (uint32_t)cols_pad;
-        return dispatch_mac<true>(vec, KFEC_DEC_MT_MID && R < 8 ? R : 8, a, s);
+        return dispatch_mac<true>(vec, (KFEC_DEC_MT_MID && R >= 5 && R < 8) || (KFEC_DEC_MT_SMALL && R == 4) ? R : 8, a, s);
     }
     if (launch_decode_prep(di, d_enc, K, N, G, d_present, d_out_idx, d_status, d_workspace, s, syn, factored)) return -3;
     if (R == 0 || B == 0) return 0;
