@@ -343,6 +343,11 @@ __host__ __device__ constexpr bool dec_ttab(int MT)
 {
     return KFEC_DEC_TTAB && (MT == 8 || (KFEC_DEC_MT_MID && MT >= 5 && MT < 8) || (KFEC_DEC_MT_SMALL && MT == 4));
 }
+#ifndef KFEC_DEC_MT4_WIDE
+#define KFEC_DEC_MT4_WIDE 1  // R > 8 coefficient-form decode in 4-row tiles where they compute fewer rows: 40:20 13.40 ->
+                             // 12.62 ms, 30:20 random 6.97 -> 6.38, 30:12 14.57 -> 12.72, 40:20 at 1% loss 4.58 -> 3.23;
+                             // 200:55 keeps 8-row tiles (profiles/r06_dec_mt4_ab.txt)
+#endif
 #ifndef KFEC_SYN_RT_MID
 #define KFEC_SYN_RT_MID 1  // syndrome decode for R = 5..7: RT = R instead of 8 (166 VGPRs at RT 5, 3 waves per SIMD, against
                            // RT 8's 256): 20:5 decode 12.83 -> 9.18 ms, 20:6 13.40 -> 11.05, 16:7 11.87 -> 10.90, 10:6
@@ -2578,7 +2583,9 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
         });
     }
 #if KFEC_SYN_MAX_R > 0
-    const int mt = 8;  // coefficient form: R > 8 (or tiny shards), 8-row tiles
+    // coefficient form: R > 8 (or tiny shards), 8-row tiles; KFEC_DEC_MT4_WIDE: 4-row tiles where they compute fewer
+    // rows (the factored records' scalar loads need row0 % 4 == 0)
+    const int mt = (KFEC_DEC_MT4_WIDE && KFEC_DEC_MT_SMALL && vec == 32 && (R + 3) / 4 * 4 < (R + 7) / 8 * 8) ? 4 : 8;
 #else
     const int mt = pick_mt(R);  // A/B build: coefficient form for every R
 #endif
@@ -2586,7 +2593,7 @@ int launch_decode(const DeviceInfo &di, const uint8_t *d_enc, int K, int N, size
     const size_t ent = entry_bytes(mt);
     return for_group_ranges(G, cols, tiles, [&](size_t g0, size_t gn) {
         const uint32_t gmax = (uint32_t)std::min<size_t>(gn, (kMacBlock - 1) / cols + 2);
-        const uint32_t JC = (KFEC_DEC_TTAB && mt == 8) ? (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kDecLdsBudget / (kDecEntry * gmax)))
+        const uint32_t JC = dec_ttab(mt) ? (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kDecLdsBudget / (kDecEntry * gmax)))
                                           : (uint32_t)std::max<size_t>(1, std::min<size_t>(K, kLdsBudget / (ent * gmax)));
         MacArgs a{};
         a.data = static_cast<const uint8_t *>(d_data) + g0 * K * pitch;
